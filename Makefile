@@ -1,0 +1,49 @@
+# Build of the MI355X (gfx950) candidate scorer — in-tree, no cmake.
+#   make            -> sspp_amd/lib/libsspp_hip.so + sspp/_sspp*.so (pybind11 drop-in) + oracle
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+PY       ?= python3
+JOBS     ?= 8
+CXXSTD    = -std=c++17
+# -ffp-contract=off: every fma in the kernels is explicit (bitwise parity with oracle/)
+HIPFLAGS  = $(CXXSTD) -O3 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
+            -Wall -Wno-unused-function -Wno-unused-result
+HOSTFLAGS = $(CXXSTD) -O2 -fPIC -ffp-contract=off -Wall -mfma
+
+SRC      = sspp_amd/csrc
+LIBDIR   = sspp_amd/lib
+OBJDIR   = build/obj
+LIB      = $(LIBDIR)/libsspp_hip.so
+PYEXT    = $(shell $(PY) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+PYMOD    = sspp/_sspp$(PYEXT)
+PYINC    = $(shell $(PY) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PBINC    = $(shell $(PY) -c "import pybind11;print(pybind11.get_include())")
+
+HDRS = include/sspp_hip.h $(SRC)/model.h $(SRC)/sspp_device.h $(SRC)/xml_lite.h
+
+all: $(LIB) $(PYMOD) oracle
+
+$(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
+
+$(OBJDIR)/sspp_kernels.o: $(SRC)/sspp_kernels.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJDIR)/sspp_kernels.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(PYMOD): $(SRC)/sspp_pybind.cpp $(LIB) include/sspp_hip.h
+	g++ $(CXXSTD) -O2 -fPIC -shared -I$(PYINC) -I$(PBINC) -Iinclude $< -o $@ \
+	    -L$(LIBDIR) -lsspp_hip -Wl,-rpath,'$$ORIGIN/../sspp_amd/lib'
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf build $(LIB) $(PYMOD)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,267 @@
+"""Benchmark: candidate paths scored per second (BASELINE.json metric), MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config robocrane|stacking]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one pass of the hot path over one batch of synthetic candidates: on-device Philox
+sampling of the perturbed control points, B-spline evaluation, free-joint FK, collision against
+the scene, arc-length cost and the argmin over feasible candidates (include/sspp.h:194-225).
+Default workload = BASELINE.json configs[1]: SamplingPathPlanner7 on the robocrane scene,
+4096 candidates x 128 waypoints per GPU (weak scaling: every rank scores its own 4096
+candidates with globally unique Philox ids; the per-step global argmin is one RCCL all-gather
+of a 32-byte record per rank, reduced on the device).
+
+Printed (rank 0): one JSON line with value = candidates scored per second over all ranks,
+a `roofline` object for the dominant kernel (k_sspp), a `roofline_fp64` object, and a
+`cpu_baseline` object (the oracle — test infrastructure, oracle/ — timed on a bounded sample
+of the same workload on the host cores, N=1 only, with a parity check on that sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6    # FP64 vector (VALU) spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="robocrane", choices=["robocrane", "stacking"])
+    ap.add_argument("--batch", type=int, default=0, help="candidates per GPU per step (default: config)")
+    ap.add_argument("--waypoints", type=int, default=128)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-launches", type=int, default=200)
+    return ap.parse_args()
+
+
+def setup_robocrane(args, device):
+    import sspp_amd as S
+    model = S.Model(os.path.join(S.SCENE_DIR, "robocrane.xml"))
+    scene = S.Scene(model, 0, 7)
+    start = np.array([0.5, 0.15, 0.136, 0.707, 0.0, 0.0, 0.707])
+    end = np.array([0.5, -0.05, 0.136, 0.707, 0.0, 0.0, 0.707])
+    n, W = 10, args.waypoints
+    u = np.array([i / (n - 1) for i in range(n)])
+    knots, ctrl0 = S.interpolate(np.array([(1 - t) * start + t * end for t in u]), 3, u)
+    B = args.batch or 4096
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=S.DEFAULT_SEED, max_batch=B)
+    bufs = job.alloc(B, device=device)
+    bufs["ctrl"] = None
+
+    def step(first_id, best=None, ctrl_out=None):
+        job.sample_score(first_id, B, bufs["arc"], bufs["feasible"],
+                         bufs["best"] if best is None else best, ctrl_out=ctrl_out)
+
+    def kernel_only(first_id):
+        job.sample_score(first_id, B, bufs["arc"], bufs["feasible"], None)
+
+    n_, D, p = 10, 7, 3
+    # SURVEY §8(d) algorithmic work per candidate
+    bytes_per = n_ * D * 8 + 8 + 1
+    flops_per = (2 * W + 1) * 2 * (p + 1) * D + (W - 1) * (3 * D + 1) + \
+        (W + 1) * (40 + 42 + 48 + 8 * 450 + 300)
+    meta = dict(workload="robocrane SamplingPathPlanner7 (block_green free joint), sigma 0.08",
+                candidates_per_gpu=B, waypoints=W, init_points=n_, degree=p, dof=D)
+    ctx = dict(kind="sspp", job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p)
+    return B, step, kernel_only, bytes_per, flops_per, meta, ctx
+
+
+def setup_stacking(args, device):
+    import sspp_amd as S
+    model = S.Model(os.path.join(S.SCENE_DIR, "stacking.xml"))
+    scene = S.Scene(model, 1, "block1")
+    start = model.body_point("block1") + np.array([0, 0, 0.02, 0])
+    end = model.body_point("block2") + np.array([0, 0, 0.22, 0])
+    K, cp = 1, args.waypoints
+    mean = (start + 0.5 * (end - start)).reshape(1, 4)
+    sigma = np.full((1, 4), 0.2)
+    lo, hi = np.array([-0.5, -0.5, 0.0, -1.6]), np.array([0.5, 0.5, 0.6, 1.6])
+    B = args.batch or 16384
+    job = S.TspJob(scene, start, end, K, cp, mean=mean, sigma=sigma, lo=lo, hi=hi, z_min=0.0,
+                   max_batch=B)
+    bufs = job.alloc(B, device=device)
+
+    def step(first_id, best=None, ctrl_out=None):
+        job.sample_score(first_id, B, bufs["L"], bufs["Cnf"], bufs["Cwf"], bufs["status"],
+                         bufs["cost"], bufs["best"] if best is None else best, vias_out=ctrl_out)
+
+    def kernel_only(first_id):
+        job.sample_score(first_id, B, bufs["L"], bufs["Cnf"], bufs["Cwf"], bufs["status"],
+                         bufs["cost"], None)
+
+    n_, D = K + 2, 4
+    bytes_per = n_ * D * 8 + 8 + 1
+    flops_per = (2 * cp + 1) * 2 * 3 * D + cp * (3 * D + 1) + cp * (40 + 42 + 48 + 2 * 450)
+    meta = dict(workload="stacking.xml TaskSpacePlanner (block1), K=1 via, sigma 0.2",
+                candidates_per_gpu=B, waypoints=cp, vias=K, degree=2, dof=4)
+    ctx = dict(kind="tsp", job=job, start=start, end=end, mean=mean, sigma=sigma, lo=lo, hi=hi,
+               cp=cp, scene_path=model.path, body=model.body_id("block1"))
+    return B, step, kernel_only, bytes_per, flops_per, meta, ctx
+
+
+def cpu_baseline(args, ctx, B, device):
+    """Oracle (CPU restatement, oracle/) timed on a bounded sample of the same workload."""
+    import torch
+    from oracle import mjcf_ref
+    from oracle import oracle as O
+    import sspp_amd as S
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
+        min(16, os.cpu_count() or 1)
+    model = mjcf_ref.load(ctx["scene_path"])
+    if ctx["kind"] == "sspp":
+        job = ctx["job"]
+        osc = O.Scene(model, 0, 7)
+        out = job.alloc(B, device=device, with_ctrl=True)
+        job.sample_score(0, B, out["arc"], out["feasible"], out["best"], ctrl_out=out["ctrl"])
+        torch.cuda.synchronize()
+        ctrl = out["ctrl"].cpu().numpy()
+        arc_g, feas_g = out["arc"].cpu().numpy(), out["feasible"].cpu().numpy()
+
+        def run(lo, hi):
+            return O.sspp_score(osc, ctx["knots"], ctx["p"], ctrl[lo:hi], ctx["W"], nthreads=threads)
+    else:
+        job = ctx["job"]
+        osc = O.Scene(model, 1, ctx["body"])
+        out = job.alloc(B, device=device, with_vias=True)
+        job.sample_score(0, B, out["L"], out["Cnf"], out["Cwf"], out["status"], out["cost"],
+                         out["best"], vias_out=out["vias"])
+        torch.cuda.synchronize()
+        ctrl = out["vias"].cpu().numpy()
+        arc_g, feas_g = out["cost"].cpu().numpy(), out["status"].cpu().numpy()
+
+        def run(lo, hi):
+            L, Cnf, Cwf, st, cost = O.tsp_score(osc, ctx["start"], ctx["end"], ctrl[lo:hi], ctx["cp"],
+                                                nthreads=threads)
+            return cost, st
+    chunk = 256
+    done, t0 = 0, time.perf_counter()
+    arcs, feas = [], []
+    while done < B and time.perf_counter() - t0 < args.cpu_seconds:
+        a, f = run(done, min(B, done + chunk))
+        arcs.append(a)
+        feas.append(f)
+        done = min(B, done + chunk)
+    dt = time.perf_counter() - t0
+    arc_c, feas_c = np.concatenate(arcs), np.concatenate(feas)
+    fin = np.isfinite(arc_c) & np.isfinite(arc_g[:done])
+    parity = dict(candidates=int(done),
+                  max_abs_cost_diff=float(np.abs(arc_c[fin] - arc_g[:done][fin]).max()) if fin.any() else 0.0,
+                  feasible_identical=bool(np.array_equal(feas_c, feas_g[:done])),
+                  argmin_identical=bool(O.argmin(arc_c, feas_c)[0] == O.argmin(arc_g[:done], feas_g[:done])[0]))
+    return dict(value=done / dt, unit="candidate paths scored/s", cores=threads, kind="port",
+                sample="first %d candidates of the GPU's step-0 batch (same ctrl points), %.1f s, "
+                       "OpenMP schedule(dynamic,1) over candidates" % (done, dt),
+                parity=parity)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    import sspp_amd as S
+
+    setup = setup_robocrane if args.config == "robocrane" else setup_stacking
+    B, step, kernel_only, bytes_per, flops_per, meta, ctx = setup(args, device)
+
+    gathered = torch.zeros((world, 4), dtype=torch.int64, device=device)
+    gbest = S.best_tensor(device)
+    local_best = S.best_tensor(device)
+
+    def full_step(i):
+        first = (i * world + rank) * B  # globally unique candidate ids
+        step(first, best=local_best)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, local_best)
+            S.reduce_best_device(gathered, gbest)
+
+    for i in range(args.warmup):
+        full_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        full_step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # roofline of the dominant kernel: HIP events on the stream the kernel runs on
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for i in range(args.roofline_launches):
+        kernel_only(i * B)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    kernel_s = e0.elapsed_time(e1) / 1e3 / args.roofline_launches
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, ctx, B, device)
+
+    if rank == 0:
+        total = args.steps * B * world
+        value = total / elapsed
+        ach_gbs = bytes_per * B / kernel_s / 1e9
+        ach_tf = flops_per * B / kernel_s / 1e12
+        line = {
+            "metric": "candidate paths scored/sec (7-DoF, 128 waypts) at 1/2/4/8 MI355X; HBM %peak"
+            if args.config == "robocrane" else "candidate paths scored/sec (stacking.xml TSP)",
+            "value": value,
+            "unit": "candidate paths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (on-device Philox candidates around a linear init spline)",
+            "config": dict(meta, parallelism="dp%d (candidate shards, RCCL all-gather argmin)" % world),
+            "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_sspp" if ctx["kind"] == "sspp" else "k_tsp",
+                         "kernel_us": kernel_s * 1e6, "bytes_per_candidate": bytes_per},
+            "roofline_fp64": {"bound": "fp64_valu", "achieved": ach_tf, "peak": FP64_PEAK_TFLOPS,
+                              "unit": "TFLOP/s", "frac": ach_tf / FP64_PEAK_TFLOPS,
+                              "flops_per_candidate": flops_per},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+/*
+ * sspp_hip.h — C ABI of the MI355X-native sampled-spline candidate scorer.
+ *
+ * This is the drop-in boundary underneath `from sspp import _sspp` (the pybind11 module
+ * in sspp_amd/csrc/sspp_pybind.cpp) and any other FFI (ctypes stub in INTEGRATION.md).
+ * Plain C types only: no torch, no Eigen, no MuJoCo.  All functions return an int status
+ * (SSPP_OK = 0, negative on error) and set a thread-local message (sspp_last_error()).
+ *
+ * Each entry point names the reference interface it replaces (paths under the reference
+ * repository Geryyy/sspp @ 2025-09-12):
+ *
+ *   sspp_model_load_mjcf     <- SamplingPathPlanner(const std::string&)  include/sspp.h:44-63
+ *                               (mj_loadXML; restricted to free joints + plane/sphere/box/cylinder)
+ *   sspp_model_body_point    <- Utility::get_body_point                  include/utility.h:228-259
+ *   sspp_scene_create        <- SamplingPathPlanner::initializeDataCopies include/sspp.h:235-244
+ *                               / tsp::CollisionWorld                     include/sspp/tsp_collision_world.h:12-41
+ *   sspp_interpolate         <- SamplingPathPlanner::initializePath      include/sspp.h:82-97
+ *                               (Eigen SplineFitting::Interpolate) and PathModel::fromVias
+ *                               include/sspp/tsp_path_model.h:32-43
+ *   sspp_spline_eval         <- SamplingPathPlanner::evaluate             include/sspp.h:99-107
+ *   sspp_job_create_sspp     <- SamplingPathPlanner::plan (set-up part)   include/sspp.h:194-200
+ *   sspp_job_sample_score    <- plan's candidate loop                     include/sspp.h:203-219
+ *                               = sampleWithNoise (114-130) + checkCollision (132-150)
+ *                               + computeArcLength (152-169) + findBestPath (171-192)
+ *   sspp_job_score_ctrl      <- checkCollision + computeArcLength + findBestPath on
+ *                               caller-supplied splines (sspp_bindings.cpp:36-41)
+ *   sspp_job_create_tsp      <- tsp::Planner (evaluation config)          include/sspp/tsp_planner.h:31-51
+ *   sspp_job_tsp_sample_score<- Planner::plan eval loop + best pick       include/sspp/tsp_planner.h:89-138
+ *                               = Sampler::sample_set (tsp_sampler.h:40-51) + PathModel::fromVias
+ *                               + Evaluator::eval_one_pass (tsp_evaluator.h:18-32)
+ *   sspp_job_tsp_score_vias  <- the same on caller-supplied via sets
+ *
+ * Device pointers: every `d_` argument is device memory (hipMalloc / torch.cuda); the job
+ * run functions issue only asynchronous work on `stream` (hipStream_t passed as void*; NULL =
+ * default stream), allocate nothing and never synchronise, so they can be captured into a
+ * hipGraph.  Host pointers are read during the call only.
+ */
+#ifndef SSPP_HIP_H
+#define SSPP_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SSPP_OK 0
+#define SSPP_E_INVAL (-1)
+#define SSPP_E_HIP (-2)
+#define SSPP_E_SCENE (-3)
+#define SSPP_E_NOMEM (-4)
+#define SSPP_E_UNSUPPORTED (-5)
+#define SSPP_E_IO (-6)
+
+/* MuJoCo mjtGeom codes for the supported primitives */
+#define SSPP_GEOM_PLANE 0
+#define SSPP_GEOM_SPHERE 2
+#define SSPP_GEOM_CAPSULE 3
+#define SSPP_GEOM_CYLINDER 5
+#define SSPP_GEOM_BOX 6
+#define SSPP_GEOM_MESH 7
+
+#define SSPP_MODE_QPOS 0 /* SamplingPathPlanner: q (D values) -> qpos[0:D] */
+#define SSPP_MODE_BODY 1 /* TaskSpacePlanner: (x,y,z,yaw) -> free body     */
+
+typedef struct sspp_model sspp_model;
+typedef struct sspp_scene sspp_scene;
+typedef struct sspp_job sspp_job;
+
+/* Flat, read-only view of a parsed model (MuJoCo-like arrays; body 0 = world). */
+typedef struct sspp_model_view {
+    int nbody;
+    const int32_t* body_parent;
+    const int32_t* body_jnt_type; /* -1 none, 0 free */
+    const int32_t* body_qpos_adr;
+    const double* body_pos;       /* [nbody][3] */
+    const double* body_quat;      /* [nbody][4] normalised */
+    int ngeom;
+    const int32_t* geom_type;
+    const int32_t* geom_body;
+    const int32_t* geom_contype;
+    const int32_t* geom_conaffinity;
+    const double* geom_size;      /* [ngeom][3] */
+    const double* geom_pos;       /* [ngeom][3] */
+    const double* geom_quat;      /* [ngeom][4] */
+    const double* geom_margin;
+    int nexclude;
+    const int32_t* exclude;       /* [nexclude][2] */
+    int nq;
+    const double* qpos0;
+} sspp_model_view;
+
+/* Result of one batch: global argmin over feasible candidates (lowest id on ties). */
+typedef struct sspp_best {
+    double cost;      /* +inf when no candidate is feasible */
+    int64_t index;    /* global candidate id, -1 when none */
+    int64_t count;    /* number of feasible candidates in the batch */
+    int64_t reserved;
+} sspp_best;
+
+typedef struct sspp_scene_info {
+    int n_moving_geoms;
+    int n_static_geoms;
+    int n_pairs;            /* moving pairs evaluated per waypoint */
+    int n_static_pairs;     /* env-env pairs (evaluated once at creation) */
+    int static_contacts;    /* contacts among env-env pairs at qpos0 */
+    int n_movers;
+    double static_cost;     /* Collision.h cost of env-env contacts (per waypoint) */
+} sspp_scene_info;
+
+typedef struct sspp_sspp_args {
+    const double* knots;    /* host [n + degree + 1] */
+    int degree;
+    const double* init_ctrl;/* host [n][dof] */
+    int n_ctrl;
+    int dof;
+    double sigma;
+    const double* limits;   /* host [dof] */
+    int check_points;       /* W: collision at i/W, i=0..W; arc on W points */
+    uint64_t seed;
+} sspp_sspp_args;
+
+typedef struct sspp_tsp_args {
+    const double* start;    /* host [4] (x, y, z, yaw) */
+    const double* end;      /* host [4] */
+    int n_vias;             /* K (total_points - 2) */
+    int check_points;       /* cp */
+    double w_collision;
+    const double* mean;     /* host [K][4] sampling mean (Distribution::mean_vias) */
+    const double* sigma;    /* host [K][4] */
+    const double* lo;       /* host [4] Sampler limits_min */
+    const double* hi;       /* host [4] Sampler limits_max */
+    double z_min;           /* PlannerConfig::z_min (sample_set clamp) */
+    uint64_t seed;
+    double floor_z_min, floor_margin, floor_scale; /* Evaluator (0, 0.01, 10) */
+} sspp_tsp_args;
+
+const char* sspp_last_error(void);
+int sspp_version(void);
+int sspp_device_count(int* n);
+
+/* ---- model ---- */
+int sspp_model_load_mjcf(const char* xml_path, sspp_model** out);
+int sspp_model_view_get(const sspp_model* m, sspp_model_view* out);
+int sspp_model_body_id(const sspp_model* m, const char* name);
+int sspp_model_geom_id(const sspp_model* m, const char* name);
+int sspp_model_body_point(const sspp_model* m, const char* name, double out_xyzyaw[4]);
+void sspp_model_free(sspp_model* m);
+
+/* ---- scene (model + moving set, device-resident tables) ---- */
+int sspp_scene_create(const sspp_model* m, int mode, int arg /* dof or body id */,
+                      int count_static_contacts, sspp_scene** out);
+int sspp_scene_get_info(const sspp_scene* s, sspp_scene_info* out);
+void sspp_scene_free(sspp_scene* s);
+
+/* ---- splines (host) ---- */
+int sspp_interpolate(const double* pts /* [n][D] */, int n, int D, int degree,
+                     const double* u /* [n] */, double* knots_out /* [n+degree+1] */,
+                     double* ctrl_out /* [n][D] */);
+int sspp_spline_eval(const double* knots, int n_knots, int degree, const double* ctrl /* [n][D] */,
+                     int D, double u, double* out /* [D] */);
+
+/* ---- SamplingPathPlanner job ---- */
+int sspp_job_create_sspp(const sspp_scene* scene /* NULL = no collision */,
+                         const sspp_sspp_args* args, int64_t max_batch, sspp_job** out);
+int sspp_job_sample_score(sspp_job* job, int64_t first_id, int64_t B, double* d_arc,
+                          uint8_t* d_feasible, double* d_ctrl_out /* nullable [B][n][D] */,
+                          sspp_best* d_best, void* stream);
+int sspp_job_score_ctrl(sspp_job* job, const double* d_ctrl /* [B][n][D] */, int64_t first_id,
+                        int64_t B, double* d_arc, uint8_t* d_feasible, sspp_best* d_best,
+                        void* stream);
+
+/* ---- TaskSpacePlanner job ---- */
+int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args* args, int64_t max_batch,
+                        sspp_job** out);
+int sspp_job_tsp_sample_score(sspp_job* job, int64_t first_id, int64_t B, double* d_L,
+                              double* d_Cnf, double* d_Cwf, uint8_t* d_status, double* d_cost,
+                              double* d_vias_out /* nullable [B][K][4] */, sspp_best* d_best,
+                              void* stream);
+int sspp_job_tsp_score_vias(sspp_job* job, const double* d_vias /* [B][K][4] */,
+                            int64_t first_id, int64_t B, double* d_L, double* d_Cnf,
+                            double* d_Cwf, uint8_t* d_status, double* d_cost, sspp_best* d_best,
+                            void* stream);
+int sspp_job_info(const sspp_job* job, int* lanes_per_candidate, int* candidates_per_block,
+                  int* block_threads, size_t* lds_bytes);
+void sspp_job_free(sspp_job* job);
+
+/* ---- multi-GPU helpers: reduce gathered per-rank results (lowest cost, lowest id) ---- */
+int sspp_best_reduce(const sspp_best* parts, int n, sspp_best* out);          /* host */
+int sspp_best_reduce_device(const sspp_best* d_parts, int n, sspp_best* d_out,
+                            void* stream);                                    /* device, async */
+
+/* ---- host-synchronous conveniences (host buffers in/out; used by the _sspp drop-in) ----
+ * sspp_plan_sspp  <- SamplingPathPlanner::plan (include/sspp.h:194-225) in one call:
+ *   initializePath (linear vias, degree 3, init_points) + sample_count candidates scored on the
+ *   GPU.  Outputs: knots [init_points+4], ctrl [sample_count][init_points][dof] (nullable),
+ *   feasible [sample_count], arc [sample_count], best.                                   */
+int sspp_plan_sspp(const sspp_scene* scene, int dof, const double* start, const double* end,
+                   double sigma, const double* limits, int sample_count, int check_points,
+                   int init_points, uint64_t seed, double* knots_out, double* ctrl_out,
+                   uint8_t* feasible_out, double* arc_out, sspp_best* best_out);
+/* checkCollision / computeArcLength / findBestPath on host splines sharing one knot vector:
+ * scene NULL = arc length only (everything feasible).                                    */
+int sspp_score_ctrl_host(const sspp_scene* scene, const double* knots, int degree,
+                         const double* ctrl /* [B][n][D] */, int64_t B, int n, int D, int W,
+                         double* arc_out, uint8_t* feasible_out, sspp_best* best_out);
+/* sampleWithNoise (include/sspp.h:114-130) for candidate ids [first_id, first_id + B). */
+int sspp_sample_ctrl_host(const double* knots, int degree, const double* init_ctrl, int n, int D,
+                          double sigma, const double* limits, uint64_t seed, int64_t first_id,
+                          int64_t B, double* ctrl_out /* [B][n][D] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

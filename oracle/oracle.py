@@ -1,0 +1,286 @@
+"""ctypes wrapper around oracle/build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+The product (sspp_amd/, sspp/) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "build", "liboracle.so")
+
+_d = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_u8 = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+_i32 = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+class _Model(C.Structure):
+    _fields_ = [
+        ("nbody", C.c_int), ("body_parent", C.c_void_p), ("body_jnt_type", C.c_void_p),
+        ("body_qpos_adr", C.c_void_p), ("body_pos", C.c_void_p), ("body_quat", C.c_void_p),
+        ("ngeom", C.c_int), ("geom_type", C.c_void_p), ("geom_body", C.c_void_p),
+        ("geom_contype", C.c_void_p), ("geom_conaffinity", C.c_void_p),
+        ("geom_size", C.c_void_p), ("geom_pos", C.c_void_p), ("geom_quat", C.c_void_p),
+        ("geom_margin", C.c_void_p), ("nexclude", C.c_int), ("exclude", C.c_void_p),
+        ("nq", C.c_int), ("qpos0", C.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = C.CDLL(_LIB)
+        L.or_scene_create.restype = C.c_void_p
+        L.or_scene_create.argtypes = [C.POINTER(_Model), C.c_int, C.c_int]
+        L.or_scene_destroy.argtypes = [C.c_void_p]
+        L.or_scene_npairs.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.or_knot_averaging.argtypes = [_d, C.c_int, C.c_int, _d]
+        L.or_span.argtypes = [C.c_double, C.c_int, _d, C.c_int]
+        L.or_basis.argtypes = [C.c_double, C.c_int, _d, C.c_int, _d]
+        L.or_spline_eval.argtypes = [_d, C.c_int, C.c_int, _d, C.c_int, C.c_double, _d]
+        L.or_interpolate.argtypes = [_d, C.c_int, C.c_int, C.c_int, _d, _d, _d]
+        L.or_py_knot_vector.argtypes = [C.c_int, C.c_int, _d]
+        L.or_py_B.restype = C.c_double
+        L.or_py_B.argtypes = [C.c_double, C.c_int, C.c_int, _d]
+        L.or_py_bspline.argtypes = [C.c_double, _d, C.c_int, _d, C.c_int, C.c_int, _d]
+        L.or_normal_pair.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
+                                     C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.or_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                       C.POINTER(C.c_uint32)]
+        L.or_sample_sspp.argtypes = [_d, C.c_int, C.c_int, C.c_int, C.c_double, _d, C.c_uint64,
+                                     C.c_int64, C.c_int64, _d]
+        L.or_sample_tsp.argtypes = [_d, _d, C.c_int, _d, _d, C.c_double, C.c_uint64, C.c_int64,
+                                    C.c_int64, _d]
+        L.or_point_contacts.argtypes = [C.c_void_p, _d, C.c_int, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_int)]
+        L.or_fk_geoms.argtypes = [C.c_void_p, _d, _d, _d]
+        L.or_canon_sum.restype = C.c_double
+        L.or_canon_sum.argtypes = [_d, C.c_int, C.c_int]
+        L.or_lanes_for.argtypes = [C.c_int]
+        L.or_sspp_score.argtypes = [C.c_void_p, _d, C.c_int, C.c_int, _d, C.c_int, C.c_int,
+                                    C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, _d, _u8]
+        L.or_argmin.restype = C.c_int64
+        L.or_argmin.argtypes = [_d, _u8, C.c_int64, C.POINTER(C.c_double)]
+        L.or_tsp_score.argtypes = [C.c_void_p, _d, _d, _d, C.c_int, C.c_int64, C.c_int,
+                                   C.c_double, C.c_int, C.c_int, _d, _d, _d, _u8, _d]
+        L.or_tsp_best.restype = C.c_int64
+        L.or_tsp_best.argtypes = [_d, _u8, C.c_int64, C.POINTER(C.c_double)]
+        _lib = L
+    return _lib
+
+
+def _f64(x, shape=None):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    return a.reshape(shape) if shape is not None else a
+
+
+# ------------------------------------------------------------------ splines
+def knot_averaging(u, p):
+    u = _f64(u)
+    k = np.zeros(len(u) + p + 1)
+    lib().or_knot_averaging(u, len(u), p, k)
+    return k
+
+
+def span(u, p, knots):
+    knots = _f64(knots)
+    return lib().or_span(float(u), p, knots, len(knots))
+
+
+def basis(u, p, knots):
+    knots = _f64(knots)
+    N = np.zeros(p + 1)
+    lib().or_basis(float(u), p, knots, len(knots), N)
+    return N
+
+
+def spline_eval(knots, p, ctrl, u):
+    knots, ctrl = _f64(knots), _f64(ctrl)
+    out = np.zeros(ctrl.shape[1])
+    lib().or_spline_eval(knots, len(knots), p, ctrl, ctrl.shape[1], float(u), out)
+    return out
+
+
+def interpolate(pts, p, u):
+    pts, u = _f64(pts), _f64(u)
+    n, D = pts.shape
+    knots = np.zeros(n + p + 1)
+    ctrl = np.zeros((n, D))
+    rc = lib().or_interpolate(pts, n, D, p, u, knots, ctrl)
+    if rc != 0:
+        raise RuntimeError("or_interpolate failed %d" % rc)
+    return knots, ctrl
+
+
+def py_knot_vector(n, k):
+    t = np.zeros(n + k + 1)
+    lib().or_py_knot_vector(n, k, t)
+    return t
+
+
+def py_bspline(theta, t, c, k):
+    t, c = _f64(t), _f64(c)
+    if c.ndim == 1:
+        c = c.reshape(-1, 1)
+    out = np.zeros(c.shape[1])
+    lib().or_py_bspline(float(theta), t, len(t), c, c.shape[1], k, out)
+    return out
+
+
+# ------------------------------------------------------------------ RNG / sampling
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib().or_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def normal_pair(seed, cand, idx, stream):
+    z0, z1 = C.c_double(), C.c_double()
+    lib().or_normal_pair(seed, cand, idx, stream, C.byref(z0), C.byref(z1))
+    return z0.value, z1.value
+
+
+def sample_sspp(init_ctrl, p, sigma, limits, seed, first, B):
+    init_ctrl = _f64(init_ctrl)
+    n, D = init_ctrl.shape
+    out = np.zeros((B, n, D))
+    lib().or_sample_sspp(init_ctrl, n, D, p, float(sigma), _f64(limits).reshape(D), seed,
+                         first, B, out)
+    return out
+
+
+def sample_tsp(mean, sigma, lo, hi, z_min, seed, first, B):
+    mean, sigma = _f64(mean).reshape(-1, 4), _f64(sigma).reshape(-1, 4)
+    K = mean.shape[0]
+    out = np.zeros((B, K, 4))
+    lib().or_sample_tsp(mean, sigma, K, _f64(lo).reshape(4), _f64(hi).reshape(4),
+                        float(z_min), seed, first, B, out)
+    return out
+
+
+# ------------------------------------------------------------------ scene
+class Scene:
+    """Oracle scene: model + moving set. mode 0 = qpos window of `arg` dofs, mode 1 = body id."""
+
+    def __init__(self, model, mode, arg):
+        self._keep = {}
+        m = _Model()
+
+        def put(name, arr, dtype):
+            a = np.ascontiguousarray(np.asarray(arr, dtype=dtype))
+            self._keep[name] = a
+            return a.ctypes.data_as(C.c_void_p)
+
+        m.nbody = len(model["body_parent"])
+        m.body_parent = put("bp", model["body_parent"], np.int32)
+        m.body_jnt_type = put("bj", model["body_jnt_type"], np.int32)
+        m.body_qpos_adr = put("ba", model["body_qpos_adr"], np.int32)
+        m.body_pos = put("bpos", model["body_pos"], np.float64)
+        m.body_quat = put("bq", model["body_quat"], np.float64)
+        m.ngeom = len(model["geom_type"])
+        m.geom_type = put("gt", model["geom_type"], np.int32)
+        m.geom_body = put("gb", model["geom_body"], np.int32)
+        m.geom_contype = put("gc", model["geom_contype"], np.int32)
+        m.geom_conaffinity = put("ga", model["geom_conaffinity"], np.int32)
+        m.geom_size = put("gs", model["geom_size"], np.float64)
+        m.geom_pos = put("gp", model["geom_pos"], np.float64)
+        m.geom_quat = put("gq", model["geom_quat"], np.float64)
+        m.geom_margin = put("gm", model["geom_margin"], np.float64)
+        ex = np.asarray(model["exclude"], np.int32).reshape(-1, 2)
+        m.nexclude = ex.shape[0]
+        m.exclude = put("ex", ex, np.int32)
+        m.nq = len(model["qpos0"])
+        m.qpos0 = put("q0", model["qpos0"] if len(model["qpos0"]) else [0.0], np.float64)
+        self._m = m
+        self.mode, self.arg = mode, arg
+        self.ngeom = m.ngeom
+        self.ptr = lib().or_scene_create(C.byref(m), mode, arg)
+        if not self.ptr:
+            raise RuntimeError("or_scene_create failed")
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.or_scene_destroy(self.ptr)
+            self.ptr = None
+
+    def npairs(self):
+        a, b = C.c_int(), C.c_int()
+        lib().or_scene_npairs(self.ptr, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def contacts(self, q, count_static=False):
+        c, nd = C.c_double(), C.c_int()
+        n = lib().or_point_contacts(self.ptr, _f64(q), int(count_static), C.byref(c), C.byref(nd))
+        return n, c.value, nd.value
+
+    def fk(self, q):
+        xp = np.zeros((self.ngeom, 3))
+        xm = np.zeros((self.ngeom, 9))
+        lib().or_fk_geoms(self.ptr, _f64(q), xp, xm)
+        return xp, xm
+
+
+# ------------------------------------------------------------------ scoring
+def canon_sum(x, lanes=None):
+    x = _f64(x)
+    if lanes is None:
+        lanes = lib().or_lanes_for(len(x))
+    return lib().or_canon_sum(x, len(x), lanes)
+
+
+def sspp_score(scene, knots, p, ctrl, W, count_static=False, sequential=False, nthreads=0):
+    knots, ctrl = _f64(knots), _f64(ctrl)
+    B, n, D = ctrl.shape
+    arc = np.zeros(B)
+    feas = np.zeros(B, np.uint8)
+    rc = lib().or_sspp_score(scene.ptr if scene is not None else None, knots, len(knots), p,
+                             ctrl, n, D, B, W, int(count_static), int(sequential), nthreads,
+                             arc, feas)
+    if rc != 0:
+        raise RuntimeError("or_sspp_score failed %d" % rc)
+    return arc, feas
+
+
+def argmin(cost, feasible):
+    cost = _f64(cost)
+    f = np.ascontiguousarray(np.asarray(feasible, np.uint8))
+    best = C.c_double()
+    idx = lib().or_argmin(cost, f, len(cost), C.byref(best))
+    return int(idx), best.value
+
+
+def tsp_score(scene, start, end, vias, cp, w_collision=1.0, sequential=False, nthreads=0):
+    vias = _f64(vias)
+    B, K, _ = vias.shape
+    L, Cnf, Cwf, cost = (np.zeros(B) for _ in range(4))
+    st = np.zeros(B, np.uint8)
+    rc = lib().or_tsp_score(scene.ptr, _f64(start).reshape(4), _f64(end).reshape(4), vias, K, B,
+                            cp, float(w_collision), int(sequential), nthreads, L, Cnf, Cwf, st,
+                            cost)
+    if rc != 0:
+        raise RuntimeError("or_tsp_score failed %d" % rc)
+    return L, Cnf, Cwf, st, cost
+
+
+def tsp_best(cost, status):
+    cost = _f64(cost)
+    st = np.ascontiguousarray(np.asarray(status, np.uint8))
+    best = C.c_double()
+    idx = lib().or_tsp_best(cost, st, len(cost), C.byref(best))
+    return int(idx), best.value

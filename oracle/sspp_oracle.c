@@ -1,0 +1,949 @@
+/*
+ * sspp_oracle.c — CPU restatement of Geryyy/sspp's candidate-scoring path.
+ * TEST INFRASTRUCTURE ONLY (see sspp_oracle.h for the contract and citations).
+ *
+ * Build: oracle/Makefile  (gcc -O2 -fopenmp -ffp-contract=off -mfma).  Every
+ * floating-point expression is written out operation by operation (explicit fma()
+ * where a fused multiply-add is meant, -ffp-contract=off everywhere else) so that the
+ * GPU kernels, which follow the same operation order, can be compared bit for bit.
+ */
+#include "sspp_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define OR_MAXP 8
+#define OR_MAXD 16
+#define OR_MINVAL 1e-15 /* mjMINVAL */
+
+/* ------------------------------------------------------------------ small math */
+static double dot3(const double* a, const double* b) {
+    return fma(a[2], b[2], fma(a[1], b[1], a[0] * b[0]));
+}
+/* row i of a row-major 3x3 times v */
+static void matvec3(const double* m, const double* v, double* r) {
+    r[0] = dot3(m + 0, v);
+    r[1] = dot3(m + 3, v);
+    r[2] = dot3(m + 6, v);
+}
+static void col3(const double* m, int j, double* c) {
+    c[0] = m[j];
+    c[1] = m[3 + j];
+    c[2] = m[6 + j];
+}
+/* mju_normalize4 (MuJoCo engine_util_blas.c) */
+static void normalize4(double* q) {
+    double s = q[0] * q[0];
+    s = fma(q[1], q[1], s);
+    s = fma(q[2], q[2], s);
+    s = fma(q[3], q[3], s);
+    double n = sqrt(s);
+    if (n < OR_MINVAL) {
+        q[0] = 1.0; q[1] = q[2] = q[3] = 0.0;
+    } else if (fabs(n - 1.0) > OR_MINVAL) {
+        double inv = 1.0 / n;
+        q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv;
+    }
+}
+/* mju_mulQuat */
+static void mulquat(const double* a, const double* b, double* r) {
+    double t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    double t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    double t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+    double t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+    r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+/* mju_quat2Mat, row-major */
+static void quat2mat(const double* q, double* m) {
+    if (q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0) {
+        m[0] = 1; m[1] = 0; m[2] = 0; m[3] = 0; m[4] = 1; m[5] = 0; m[6] = 0; m[7] = 0; m[8] = 1;
+        return;
+    }
+    double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+    double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+    double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+    m[0] = q00 + q11 - q22 - q33;
+    m[4] = q00 - q11 + q22 - q33;
+    m[8] = q00 - q11 - q22 + q33;
+    m[1] = 2.0 * (q12 - q03);
+    m[2] = 2.0 * (q13 + q02);
+    m[3] = 2.0 * (q12 + q03);
+    m[5] = 2.0 * (q23 - q01);
+    m[6] = 2.0 * (q13 - q02);
+    m[7] = 2.0 * (q23 + q01);
+}
+
+/* ------------------------------------------------------------------ splines */
+void or_knot_averaging(const double* u, int n, int p, double* knots) {
+    /* Eigen KnotAveraging: interior knot t_{j+p} = mean(u_j..u_{j+p-1}), j=1..n-p-1 */
+    int nk = n + p + 1;
+    for (int j = 1; j < n - p; ++j) {
+        double s = 0.0;
+        for (int r = 0; r < p; ++r) s = s + u[j + r];
+        knots[j + p] = s / (double)p;
+    }
+    for (int i = 0; i <= p; ++i) knots[i] = 0.0;
+    for (int i = nk - p - 1; i < nk; ++i) knots[i] = 1.0;
+}
+
+int or_span(double u, int p, const double* knots, int nknots) {
+    /* Eigen Spline::Span (Piegl & Tiller A2.1 via std::upper_bound) */
+    if (u <= knots[0]) return p;
+    int lo = p - 1, hi = nknots - p - 1; /* search [lo, hi) */
+    int first = lo, count = hi - lo;
+    while (count > 0) { /* upper_bound */
+        int step = count / 2, it = first + step;
+        if (!(u < knots[it])) { first = it + 1; count -= step + 1; }
+        else count = step;
+    }
+    return first - 1;
+}
+
+void or_basis(double u, int p, const double* knots, int nknots, double* N) {
+    /* Eigen Spline::BasisFunctions (Piegl & Tiller A2.2) */
+    int i = or_span(u, p, knots, nknots);
+    double left[OR_MAXP + 1], right[OR_MAXP + 1];
+    left[0] = 0.0; right[0] = 0.0;
+    for (int j = 1; j <= p; ++j) {
+        left[j] = u - knots[i + 1 - j];
+        right[j] = knots[i + j] - u;
+    }
+    N[0] = 1.0;
+    for (int j = 1; j <= p; ++j) {
+        double saved = 0.0;
+        for (int r = 0; r < j; ++r) {
+            double tmp = N[r] / (right[r + 1] + left[j - r]);
+            N[r] = saved + right[r + 1] * tmp;
+            saved = left[j - r] * tmp;
+        }
+        N[j] = saved;
+    }
+}
+
+void or_spline_eval(const double* knots, int nknots, int p, const double* ctrl, int D, double u,
+                    double* out) {
+    int span = or_span(u, p, knots, nknots);
+    double N[OR_MAXP + 1];
+    or_basis(u, p, knots, nknots, N);
+    const double* c0 = ctrl + (size_t)(span - p) * D;
+    for (int d = 0; d < D; ++d) {
+        double acc = N[0] * c0[d];
+        for (int r = 1; r <= p; ++r) acc = fma(N[r], c0[(size_t)r * D + d], acc);
+        out[d] = acc;
+    }
+}
+
+/* Householder QR least squares solve A X = B (A n x n row-major, B n x D row-major) */
+static int qr_solve(double* A, double* B, int n, int D) {
+    double* v = (double*)malloc(sizeof(double) * n);
+    if (!v) return -1;
+    for (int k = 0; k < n; ++k) {
+        double norm = 0.0;
+        for (int i = k; i < n; ++i) norm = fma(A[i * n + k], A[i * n + k], norm);
+        norm = sqrt(norm);
+        if (norm == 0.0) continue;
+        double alpha = A[k * n + k] > 0 ? -norm : norm;
+        for (int i = k; i < n; ++i) v[i] = A[i * n + k];
+        v[k] -= alpha;
+        double vn = 0.0;
+        for (int i = k; i < n; ++i) vn = fma(v[i], v[i], vn);
+        if (vn == 0.0) continue;
+        for (int j = k; j < n; ++j) {
+            double s = 0.0;
+            for (int i = k; i < n; ++i) s = fma(v[i], A[i * n + j], s);
+            s = 2.0 * s / vn;
+            for (int i = k; i < n; ++i) A[i * n + j] -= s * v[i];
+        }
+        for (int j = 0; j < D; ++j) {
+            double s = 0.0;
+            for (int i = k; i < n; ++i) s = fma(v[i], B[i * D + j], s);
+            s = 2.0 * s / vn;
+            for (int i = k; i < n; ++i) B[i * D + j] -= s * v[i];
+        }
+    }
+    free(v);
+    for (int j = 0; j < D; ++j) {
+        for (int i = n - 1; i >= 0; --i) {
+            double s = B[i * D + j];
+            for (int c = i + 1; c < n; ++c) s -= A[i * n + c] * B[c * D + j];
+            if (A[i * n + i] == 0.0) return -2;
+            B[i * D + j] = s / A[i * n + i];
+        }
+    }
+    return 0;
+}
+
+int or_interpolate(const double* pts, int n, int D, int p, const double* u, double* knots,
+                   double* ctrl) {
+    /* Eigen SplineFitting::Interpolate(pts, degree, knot_parameters) */
+    if (n < p + 1 || p > OR_MAXP) return -1;
+    int nk = n + p + 1;
+    or_knot_averaging(u, n, p, knots);
+    double* A = (double*)calloc((size_t)n * n, sizeof(double));
+    if (!A) return -1;
+    for (int i = 1; i < n - 1; ++i) {
+        int span = or_span(u[i], p, knots, nk);
+        double N[OR_MAXP + 1];
+        or_basis(u[i], p, knots, nk, N);
+        for (int r = 0; r <= p; ++r) A[i * n + span - p + r] = N[r];
+    }
+    A[0] = 1.0;
+    A[(n - 1) * n + n - 1] = 1.0;
+    memcpy(ctrl, pts, sizeof(double) * (size_t)n * D);
+    int rc = qr_solve(A, ctrl, n, D);
+    free(A);
+    return rc;
+}
+
+/* ------------------------------------------------------------------ BSplines.py */
+void or_py_knot_vector(int n, int k, double* t) {
+    int m = n + 1 - k; /* np.linspace(0, 1, n_knots - 2k) */
+    int o = 0;
+    for (int i = 0; i < k; ++i) t[o++] = 0.0;
+    double step = 1.0 / (double)(m - 1);
+    for (int i = 0; i < m; ++i) t[o++] = (i == m - 1) ? 1.0 : (double)i * step + 0.0;
+    for (int i = 0; i < k; ++i) t[o++] = 1.0;
+}
+
+double or_py_B(double theta, int k, int i, const double* t) {
+    if (k == 0) return (t[i] <= theta && theta < t[i + 1]) ? 1.0 : 0.0;
+    double c1, c2;
+    if (t[i + k] == t[i]) c1 = 0.0;
+    else c1 = (theta - t[i]) / (t[i + k] - t[i]) * or_py_B(theta, k - 1, i, t);
+    if (t[i + k + 1] == t[i + 1]) c2 = 0.0;
+    else c2 = (t[i + k + 1] - theta) / (t[i + k + 1] - t[i + 1]) * or_py_B(theta, k - 1, i + 1, t);
+    return c1 + c2;
+}
+
+void or_py_bspline(double theta, const double* t, int nt, const double* c, int D, int k,
+                   double* out) {
+    int n = nt - k - 1;
+    if (theta < 0) {
+        double b = or_py_B(0.0, k, 0, t);
+        for (int d = 0; d < D; ++d) out[d] = c[d] * b;
+        return;
+    }
+    if (theta >= 1) {
+        for (int d = 0; d < D; ++d) out[d] = c[(size_t)(n - 1) * D + d];
+        return;
+    }
+    for (int d = 0; d < D; ++d) out[d] = 0.0;
+    for (int i = 0; i < n; ++i) {
+        double b = or_py_B(theta, k, i, t);
+        for (int d = 0; d < D; ++d) out[d] = out[d] + c[(size_t)i * D + d] * b;
+    }
+}
+
+/* ------------------------------------------------------------------ Philox4x32-10 */
+static uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
+    uint64_t p = (uint64_t)a * (uint64_t)b;
+    *hi = (uint32_t)(p >> 32);
+    return (uint32_t)p;
+}
+void or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint32_t hi0, hi1;
+        uint32_t lo0 = mulhilo(0xD2511F53u, c0, &hi0);
+        uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, &hi1);
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void philox_words(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream, uint32_t o[4]) {
+    uint32_t ctr[4] = {idx, stream, (uint32_t)cand, (uint32_t)(cand >> 32)};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    or_philox4x32_10(ctr, key, o);
+}
+#define TWO_M53 1.1102230246251565e-16 /* 2^-53 */
+#define TWO_PI 6.283185307179586
+
+void or_normal_pair(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream, double* z0,
+                    double* z1) {
+    uint32_t o[4];
+    philox_words(seed, cand, idx, stream, o);
+    uint64_t a = (((uint64_t)o[0] << 32) | o[1]) >> 11;
+    uint64_t b = (((uint64_t)o[2] << 32) | o[3]) >> 11;
+    double u1 = (double)(a + 1) * TWO_M53; /* (0,1] */
+    double u2 = (double)b * TWO_M53;       /* [0,1) */
+    double r = sqrt(-2.0 * log(u1));
+    double th = TWO_PI * u2;
+    *z0 = r * cos(th);
+    *z1 = r * sin(th);
+}
+
+static double uniform01(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream) {
+    uint32_t o[4];
+    philox_words(seed, cand, idx, stream, o);
+    uint64_t b = (((uint64_t)o[2] << 32) | o[3]) >> 11;
+    return (double)b * TWO_M53;
+}
+
+void or_sample_sspp(const double* init_ctrl, int n, int D, int p, double sigma,
+                    const double* limits, uint64_t seed, int64_t first, int64_t B,
+                    double* ctrl_out) {
+    /* include/sspp.h:114-130: ctrl(d, j) += N(0, sigma) * limits(d), j in [p, n-p) */
+    for (int64_t b = 0; b < B; ++b) {
+        uint64_t g = (uint64_t)(first + b);
+        double* c = ctrl_out + (size_t)b * n * D;
+        memcpy(c, init_ctrl, sizeof(double) * (size_t)n * D);
+        for (int j = p; j < n - p; ++j) {
+            for (int d = 0; d < D; ++d) {
+                int k = (j - p) * D + d;
+                double z0, z1;
+                or_normal_pair(seed, g, (uint32_t)(k >> 1), 0u, &z0, &z1);
+                double z = (k & 1) ? z1 : z0;
+                double noise = (sigma * z) * limits[d];
+                c[(size_t)j * D + d] = c[(size_t)j * D + d] + noise;
+            }
+        }
+    }
+}
+
+void or_sample_tsp(const double* mean, const double* sigma, int K, const double* lo,
+                   const double* hi, double z_min, uint64_t seed, int64_t first, int64_t B,
+                   double* vias_out) {
+    /* include/sspp/tsp_sampler.h:12-51 */
+    for (int64_t b = 0; b < B; ++b) {
+        uint64_t g = (uint64_t)(first + b);
+        for (int v = 0; v < K; ++v) {
+            double* pt = vias_out + ((size_t)b * K + v) * 4;
+            const double* m = mean + v * 4;
+            const double* s = sigma + v * 4;
+            for (int i = 0; i < 3; ++i) {
+                double val = 0.0;
+                int ok = 0;
+                for (int t = 0; t < 99; ++t) {
+                    double z0, z1;
+                    or_normal_pair(seed, g, (uint32_t)(((v * 4 + i) << 7) | t), 1u, &z0, &z1);
+                    val = z0 * s[i];
+                    val = val + m[i];
+                    if (!(val < lo[i] || val > hi[i])) { ok = 1; break; }
+                }
+                if (!ok) {
+                    double u = uniform01(seed, g, (uint32_t)(((v * 4 + i) << 7) | 127), 1u);
+                    val = u * (hi[i] - lo[i]);
+                    val = val + lo[i];
+                }
+                pt[i] = val;
+            }
+            if (lo[3] != hi[3]) {
+                double z0, z1;
+                or_normal_pair(seed, g, (uint32_t)((v * 4 + 3) << 7), 1u, &z0, &z1);
+                double yaw = z0 * s[3];
+                yaw = yaw + m[3];
+                double range = hi[3] - lo[3];
+                while (yaw < lo[3]) yaw += range;
+                while (yaw > hi[3]) yaw -= range;
+                pt[3] = yaw;
+            } else {
+                pt[3] = m[3];
+            }
+            if (pt[2] < z_min) pt[2] = z_min;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ scene */
+typedef struct { int g1, g2, is_static; double margin; } or_pair;
+
+struct or_scene {
+    int mode, arg;
+    int nbody, ngeom, nq;
+    int32_t *body_parent, *body_jnt_type, *body_qpos_adr, *weld, *moving;
+    double *body_pos, *body_quat;
+    int32_t *geom_type, *geom_body;
+    double *geom_size, *geom_pos, *geom_quat, *geom_margin, *rbound;
+    double* qpos0;
+    int npair;
+    or_pair* pairs;
+};
+
+static void* dupmem(const void* p, size_t n) {
+    void* r = malloc(n ? n : 1);
+    if (r && n) memcpy(r, p, n);
+    return r;
+}
+
+static double geom_rbound(int type, const double* s) {
+    switch (type) {
+        case OR_GEOM_BOX: return sqrt(fma(s[2], s[2], fma(s[1], s[1], s[0] * s[0])));
+        case OR_GEOM_CYLINDER: return sqrt(fma(s[1], s[1], s[0] * s[0]));
+        case OR_GEOM_SPHERE: return s[0];
+        case OR_GEOM_CAPSULE: return s[0] + s[1];
+        default: return 0.0; /* plane: infinite */
+    }
+}
+
+or_scene* or_scene_create(const or_model* m, int mode, int arg) {
+    or_scene* s = (or_scene*)calloc(1, sizeof(or_scene));
+    if (!s) return NULL;
+    s->mode = mode; s->arg = arg;
+    s->nbody = m->nbody; s->ngeom = m->ngeom; s->nq = m->nq;
+    size_t nb = (size_t)m->nbody, ng = (size_t)m->ngeom;
+    s->body_parent = (int32_t*)dupmem(m->body_parent, nb * 4);
+    s->body_jnt_type = (int32_t*)dupmem(m->body_jnt_type, nb * 4);
+    s->body_qpos_adr = (int32_t*)dupmem(m->body_qpos_adr, nb * 4);
+    s->body_pos = (double*)dupmem(m->body_pos, nb * 24);
+    s->body_quat = (double*)dupmem(m->body_quat, nb * 32);
+    s->geom_type = (int32_t*)dupmem(m->geom_type, ng * 4);
+    s->geom_body = (int32_t*)dupmem(m->geom_body, ng * 4);
+    s->geom_size = (double*)dupmem(m->geom_size, ng * 24);
+    s->geom_pos = (double*)dupmem(m->geom_pos, ng * 24);
+    s->geom_quat = (double*)dupmem(m->geom_quat, ng * 32);
+    s->geom_margin = (double*)dupmem(m->geom_margin, ng * 8);
+    s->qpos0 = (double*)dupmem(m->qpos0, (size_t)m->nq * 8);
+    s->weld = (int32_t*)calloc(nb, 4);
+    s->moving = (int32_t*)calloc(nb, 4);
+    s->rbound = (double*)calloc(ng ? ng : 1, 8);
+    /* weld bodies: a body without joints is welded to its parent (MuJoCo body_weldid) */
+    for (int b = 0; b < m->nbody; ++b) {
+        if (b == 0) s->weld[b] = 0;
+        else if (m->body_jnt_type[b] != OR_JNT_NONE) s->weld[b] = b;
+        else s->weld[b] = s->weld[m->body_parent[b]];
+    }
+    /* moving weld roots */
+    for (int b = 1; b < m->nbody; ++b) {
+        if (m->body_jnt_type[b] != OR_JNT_FREE) continue;
+        if (mode == 0) { if (m->body_qpos_adr[b] < arg) s->moving[b] = 1; }
+        else if (b == arg) s->moving[b] = 1;
+    }
+    for (int g = 0; g < m->ngeom; ++g) s->rbound[g] = geom_rbound(m->geom_type[g], m->geom_size + 3 * g);
+    /* pair list in (g1 < g2) order — mj_collision filter */
+    s->pairs = (or_pair*)malloc(sizeof(or_pair) * (ng * ng / 2 + 1));
+    s->npair = 0;
+    for (int g1 = 0; g1 < m->ngeom; ++g1) {
+        for (int g2 = g1 + 1; g2 < m->ngeom; ++g2) {
+            int b1 = m->geom_body[g1], b2 = m->geom_body[g2];
+            int w1 = s->weld[b1], w2 = s->weld[b2];
+            if (w1 == w2) continue; /* same weld body (incl. static-static) */
+            int ct1 = m->geom_contype[g1], ca1 = m->geom_conaffinity[g1];
+            int ct2 = m->geom_contype[g2], ca2 = m->geom_conaffinity[g2];
+            if (!((ct1 & ca2) || (ct2 & ca1))) continue;
+            if (w1 != 0 && w2 != 0) { /* filterparent */
+                if (w1 == s->weld[m->body_parent[w2]] || w2 == s->weld[m->body_parent[w1]]) continue;
+            }
+            int excl = 0;
+            for (int e = 0; e < m->nexclude; ++e) {
+                int e1 = m->exclude[2 * e], e2 = m->exclude[2 * e + 1];
+                if ((e1 == b1 && e2 == b2) || (e1 == b2 && e2 == b1)) { excl = 1; break; }
+            }
+            if (excl) continue;
+            or_pair pr;
+            pr.g1 = g1; pr.g2 = g2;
+            pr.is_static = !(s->moving[w1] || s->moving[w2]);
+            double m1 = m->geom_margin[g1], m2 = m->geom_margin[g2];
+            pr.margin = m1 > m2 ? m1 : m2;
+            s->pairs[s->npair++] = pr;
+        }
+    }
+    return s;
+}
+
+void or_scene_destroy(or_scene* s) {
+    if (!s) return;
+    free(s->body_parent); free(s->body_jnt_type); free(s->body_qpos_adr); free(s->weld);
+    free(s->moving); free(s->body_pos); free(s->body_quat); free(s->geom_type);
+    free(s->geom_body); free(s->geom_size); free(s->geom_pos); free(s->geom_quat);
+    free(s->geom_margin); free(s->rbound); free(s->qpos0); free(s->pairs); free(s);
+}
+
+int or_scene_npairs(const or_scene* s, int* n_moving, int* n_static) {
+    int nm = 0, ns = 0;
+    for (int i = 0; i < s->npair; ++i) { if (s->pairs[i].is_static) ns++; else nm++; }
+    if (n_moving) *n_moving = nm;
+    if (n_static) *n_static = ns;
+    return s->npair;
+}
+
+/* mj_kinematics restated for free joints + fixed bodies */
+static void fk(const or_scene* s, const double* qpos, double* xpos, double* xquat, double* xmat,
+               double* gxpos, double* gxmat) {
+    xpos[0] = xpos[1] = xpos[2] = 0.0;
+    xquat[0] = 1.0; xquat[1] = xquat[2] = xquat[3] = 0.0;
+    quat2mat(xquat, xmat);
+    for (int b = 1; b < s->nbody; ++b) {
+        double* p = xpos + 3 * b;
+        double* q = xquat + 4 * b;
+        if (s->body_jnt_type[b] == OR_JNT_FREE) {
+            const double* qp = qpos + s->body_qpos_adr[b];
+            p[0] = qp[0]; p[1] = qp[1]; p[2] = qp[2];
+            q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
+        } else {
+            int pa = s->body_parent[b];
+            double t[3];
+            matvec3(xmat + 9 * pa, s->body_pos + 3 * b, t);
+            p[0] = xpos[3 * pa] + t[0];
+            p[1] = xpos[3 * pa + 1] + t[1];
+            p[2] = xpos[3 * pa + 2] + t[2];
+            mulquat(xquat + 4 * pa, s->body_quat + 4 * b, q);
+        }
+        normalize4(q);
+        quat2mat(q, xmat + 9 * b);
+    }
+    for (int g = 0; g < s->ngeom; ++g) {
+        int b = s->geom_body[g];
+        double t[3], gq[4];
+        matvec3(xmat + 9 * b, s->geom_pos + 3 * g, t);
+        gxpos[3 * g] = xpos[3 * b] + t[0];
+        gxpos[3 * g + 1] = xpos[3 * b + 1] + t[1];
+        gxpos[3 * g + 2] = xpos[3 * b + 2] + t[2];
+        mulquat(xquat + 4 * b, s->geom_quat + 4 * g, gq);
+        normalize4(gq);
+        quat2mat(gq, gxmat + 9 * g);
+    }
+}
+
+static void set_qpos(const or_scene* s, const double* q, double* qpos) {
+    memcpy(qpos, s->qpos0, sizeof(double) * (size_t)s->nq);
+    if (s->mode == 0) {
+        for (int i = 0; i < s->arg && i < s->nq; ++i) qpos[i] = q[i];
+    } else {
+        /* Utility::mj_set_point + yaw_to_quat (include/utility.h:149-206) */
+        int adr = s->body_qpos_adr[s->arg];
+        double half = q[3] * 0.5;
+        qpos[adr] = q[0]; qpos[adr + 1] = q[1]; qpos[adr + 2] = q[2];
+        qpos[adr + 3] = cos(half); qpos[adr + 4] = 0.0; qpos[adr + 5] = 0.0; qpos[adr + 6] = sin(half);
+    }
+}
+
+void or_fk_geoms(const or_scene* s, const double* q, double* gxpos, double* gxmat) {
+    double* qpos = (double*)malloc(sizeof(double) * (size_t)(s->nq ? s->nq : 1));
+    double* xpos = (double*)malloc(sizeof(double) * 3 * s->nbody);
+    double* xquat = (double*)malloc(sizeof(double) * 4 * s->nbody);
+    double* xmat = (double*)malloc(sizeof(double) * 9 * s->nbody);
+    set_qpos(s, q, qpos);
+    fk(s, qpos, xpos, xquat, xmat, gxpos, gxmat);
+    free(qpos); free(xpos); free(xquat); free(xmat);
+}
+
+/* ------------------------------------------------------------------ narrowphase
+ * Each function returns the number of contacts (dist < margin) and, in *ndeep,
+ * how many of them have dist < -1e-3 (include/Collision.h:93).                */
+#define DEEP (-1e-3)
+
+static int col_plane_box(const double* pp, const double* pm, const double* bp, const double* bm,
+                         const double* e, double margin, int* ndeep) {
+    double n[3], d[3], ax[3], a[3];
+    col3(pm, 2, n);
+    d[0] = bp[0] - pp[0]; d[1] = bp[1] - pp[1]; d[2] = bp[2] - pp[2];
+    double d0 = dot3(d, n);
+    for (int j = 0; j < 3; ++j) { col3(bm, j, ax); a[j] = dot3(n, ax) * e[j]; }
+    int nc = 0, nd = 0;
+    for (int k = 0; k < 8; ++k) {
+        double t = d0 + ((k & 1) ? a[0] : -a[0]);
+        t = t + ((k & 2) ? a[1] : -a[1]);
+        t = t + ((k & 4) ? a[2] : -a[2]);
+        if (t < margin && nc < 4) { nc++; if (t < DEEP) nd++; }
+    }
+    *ndeep = nd;
+    return nc;
+}
+
+static int col_plane_sphere(const double* pp, const double* pm, const double* sp, double r,
+                            double margin, int* ndeep) {
+    double n[3], d[3];
+    col3(pm, 2, n);
+    d[0] = sp[0] - pp[0]; d[1] = sp[1] - pp[1]; d[2] = sp[2] - pp[2];
+    double dist = dot3(d, n) - r;
+    *ndeep = dist < DEEP;
+    return dist < margin;
+}
+
+static int col_plane_cyl(const double* pp, const double* pm, const double* cp, const double* cm,
+                         const double* sz, double margin, int* ndeep) {
+    double n[3], a[3], d[3];
+    col3(pm, 2, n);
+    col3(cm, 2, a);
+    d[0] = cp[0] - pp[0]; d[1] = cp[1] - pp[1]; d[2] = cp[2] - pp[2];
+    double dn = dot3(d, n), na = dot3(n, a);
+    double s = 1.0 - na * na;
+    double rim = sz[0] * sqrt(s > 0.0 ? s : 0.0);
+    double ha = sz[1] * na;
+    int nc = 0, nd = 0;
+    for (int c = 0; c < 2; ++c) {
+        double t = (c == 0) ? dn - ha : dn + ha;
+        t = t - rim;
+        if (t < margin) { nc++; if (t < DEEP) nd++; }
+    }
+    *ndeep = nd;
+    return nc;
+}
+
+static int col_sphere_sphere(const double* p1, double r1, const double* p2, double r2,
+                             double margin, int* ndeep) {
+    double d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    double dist = sqrt(dot3(d, d)) - (r1 + r2);
+    *ndeep = dist < DEEP;
+    return dist < margin;
+}
+
+static int col_sphere_box(const double* sp, double r, const double* bp, const double* bm,
+                          const double* e, double margin, int* ndeep) {
+    double d[3] = {sp[0] - bp[0], sp[1] - bp[1], sp[2] - bp[2]}, ax[3], l[3];
+    int inside = 1;
+    double mind = 1e300, out2 = 0.0;
+    for (int j = 0; j < 3; ++j) {
+        col3(bm, j, ax);
+        l[j] = dot3(ax, d);
+        double al = fabs(l[j]);
+        if (al > e[j]) { inside = 0; double o = al - e[j]; out2 = fma(o, o, out2); }
+        double f = e[j] - al;
+        if (f < mind) mind = f;
+    }
+    double dist = inside ? (-mind - r) : (sqrt(out2) - r);
+    *ndeep = dist < DEEP;
+    return dist < margin;
+}
+
+static int col_sphere_cyl(const double* sp, double r, const double* cp, const double* cm,
+                          const double* sz, double margin, int* ndeep) {
+    double d[3] = {sp[0] - cp[0], sp[1] - cp[1], sp[2] - cp[2]}, a[3];
+    col3(cm, 2, a);
+    double z = dot3(a, d);
+    double rr = dot3(d, d) - z * z;
+    double rho = sqrt(rr > 0.0 ? rr : 0.0);
+    double dz = fabs(z) - sz[1], dr = rho - sz[0];
+    double dist;
+    if (dz <= 0.0 && dr <= 0.0) dist = (dz > dr ? dz : dr) - r;
+    else {
+        double oz = dz > 0.0 ? dz : 0.0, orr = dr > 0.0 ? dr : 0.0;
+        dist = sqrt(fma(orr, orr, oz * oz)) - r;
+    }
+    *ndeep = dist < DEEP;
+    return dist < margin;
+}
+
+/* Separating-axis test for two boxes: dist = max over the 15 axes of the signed
+ * separation; the pair is "in contact" when dist < margin and "deep" when dist < -1e-3.
+ * Early exit as soon as one axis reaches thr (exact: only the booleans are used).   */
+static int sat_box_box(const double* pa, const double* ma, const double* ea, const double* pb,
+                       const double* mb, const double* eb, double thr) {
+    double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
+    for (int j = 0; j < 3; ++j) { col3(ma, j, A[j]); col3(mb, j, Bc[j]); }
+    T[0] = pb[0] - pa[0]; T[1] = pb[1] - pa[1]; T[2] = pb[2] - pa[2];
+    for (int i = 0; i < 3; ++i) {
+        t[i] = dot3(A[i], T);
+        for (int j = 0; j < 3; ++j) { R[i][j] = dot3(A[i], Bc[j]); AR[i][j] = fabs(R[i][j]); }
+    }
+    for (int i = 0; i < 3; ++i) { /* faces of A */
+        double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
+        double sep = fabs(t[i]) - (ea[i] + rb);
+        if (sep >= thr) return 0;
+    }
+    for (int j = 0; j < 3; ++j) { /* faces of B */
+        double pr = fabs(fma(t[2], R[2][j], fma(t[1], R[1][j], t[0] * R[0][j])));
+        double ra = fma(ea[2], AR[2][j], fma(ea[1], AR[1][j], ea[0] * AR[0][j]));
+        double sep = pr - (ra + eb[j]);
+        if (sep >= thr) return 0;
+    }
+    for (int i = 0; i < 3; ++i) { /* edge x edge */
+        for (int j = 0; j < 3; ++j) {
+            double v[3] = {R[0][j], R[1][j], R[2][j]}, L[3];
+            if (i == 0) { L[0] = 0.0; L[1] = -v[2]; L[2] = v[1]; }
+            else if (i == 1) { L[0] = v[2]; L[1] = 0.0; L[2] = -v[0]; }
+            else { L[0] = -v[1]; L[1] = v[0]; L[2] = 0.0; }
+            double len2 = dot3(L, L);
+            if (len2 < 1e-12) continue;
+            double pr = fabs(dot3(t, L));
+            double ra = fma(ea[2], fabs(L[2]), fma(ea[1], fabs(L[1]), ea[0] * fabs(L[0])));
+            double rb = 0.0;
+            for (int k = 0; k < 3; ++k) {
+                double bk[3] = {R[0][k], R[1][k], R[2][k]};
+                rb = fma(eb[k], fabs(dot3(bk, L)), rb);
+            }
+            double sep = (pr - (ra + rb)) / sqrt(len2);
+            if (sep >= thr) return 0;
+        }
+    }
+    return 1;
+}
+
+/* cylinder (A) vs box (B): separating-axis test over the 7 finite axes
+ * {box faces, cylinder axis, cylinder axis x box edges}. */
+static int sat_cyl_box(const double* pa, const double* ma, const double* sz, const double* pb,
+                       const double* mb, const double* eb, double thr) {
+    double a[3], Bc[3][3], T[3];
+    col3(ma, 2, a);
+    for (int j = 0; j < 3; ++j) col3(mb, j, Bc[j]);
+    T[0] = pb[0] - pa[0]; T[1] = pb[1] - pa[1]; T[2] = pb[2] - pa[2];
+    for (int ax = 0; ax < 7; ++ax) {
+        double L[3];
+        if (ax < 3) { L[0] = Bc[ax][0]; L[1] = Bc[ax][1]; L[2] = Bc[ax][2]; }
+        else if (ax == 3) { L[0] = a[0]; L[1] = a[1]; L[2] = a[2]; }
+        else {
+            const double* b = Bc[ax - 4];
+            L[0] = a[1] * b[2] - a[2] * b[1];
+            L[1] = a[2] * b[0] - a[0] * b[2];
+            L[2] = a[0] * b[1] - a[1] * b[0];
+        }
+        double len2 = dot3(L, L);
+        if (len2 < 1e-12) continue;
+        double aL = dot3(a, L);
+        double rr = len2 - aL * aL;
+        double rc = fma(sz[1], fabs(aL), sz[0] * sqrt(rr > 0.0 ? rr : 0.0));
+        double rb = 0.0;
+        for (int k = 0; k < 3; ++k) rb = fma(eb[k], fabs(dot3(Bc[k], L)), rb);
+        double sep = (fabs(dot3(T, L)) - (rc + rb)) / sqrt(len2);
+        if (sep >= thr) return 0;
+    }
+    return 1;
+}
+
+/* dispatch; returns contact count, *ndeep deep count, -1 if unsupported */
+static int collide(int t1, const double* p1, const double* m1, const double* s1, int t2,
+                   const double* p2, const double* m2, const double* s2, double margin, int* ndeep) {
+    *ndeep = 0;
+    if (t1 > t2) { /* order by type like mj_collision's table */
+        int tt = t1; t1 = t2; t2 = tt;
+        const double* x;
+        x = p1; p1 = p2; p2 = x;
+        x = m1; m1 = m2; m2 = x;
+        x = s1; s1 = s2; s2 = x;
+    }
+    if (t1 == OR_GEOM_PLANE) {
+        if (t2 == OR_GEOM_BOX) return col_plane_box(p1, m1, p2, m2, s2, margin, ndeep);
+        if (t2 == OR_GEOM_SPHERE) return col_plane_sphere(p1, m1, p2, s2[0], margin, ndeep);
+        if (t2 == OR_GEOM_CYLINDER) return col_plane_cyl(p1, m1, p2, m2, s2, margin, ndeep);
+        if (t2 == OR_GEOM_PLANE) return 0;
+        return -1;
+    }
+    if (t1 == OR_GEOM_SPHERE) {
+        if (t2 == OR_GEOM_SPHERE) return col_sphere_sphere(p1, s1[0], p2, s2[0], margin, ndeep);
+        if (t2 == OR_GEOM_BOX) return col_sphere_box(p1, s1[0], p2, m2, s2, margin, ndeep);
+        if (t2 == OR_GEOM_CYLINDER) return col_sphere_cyl(p1, s1[0], p2, m2, s2, margin, ndeep);
+        return -1;
+    }
+    if (t1 == OR_GEOM_CYLINDER && t2 == OR_GEOM_BOX) {
+        int c = sat_cyl_box(p1, m1, s1, p2, m2, s2, margin);
+        if (!c) return 0;
+        *ndeep = sat_cyl_box(p1, m1, s1, p2, m2, s2, DEEP);
+        return 1;
+    }
+    if (t1 == OR_GEOM_BOX && t2 == OR_GEOM_BOX) {
+        int c = sat_box_box(p1, m1, s1, p2, m2, s2, margin);
+        if (!c) return 0;
+        *ndeep = sat_box_box(p1, m1, s1, p2, m2, s2, DEEP);
+        return 1;
+    }
+    return -1;
+}
+
+int or_point_contacts(const or_scene* s, const double* q, int count_static, double* deep_cost,
+                      int* n_deep) {
+    int nb = s->nbody, ng = s->ngeom;
+    double qpos_buf[256], xpos_b[3 * 64], xquat_b[4 * 64], xmat_b[9 * 64], gxpos_b[3 * 128],
+        gxmat_b[9 * 128];
+    double *qpos = qpos_buf, *xpos = xpos_b, *xquat = xquat_b, *xmat = xmat_b, *gxpos = gxpos_b,
+           *gxmat = gxmat_b;
+    int heap = (s->nq > 256 || nb > 64 || ng > 128);
+    if (heap) {
+        qpos = (double*)malloc(8 * (size_t)(s->nq + 1));
+        xpos = (double*)malloc(24 * (size_t)nb); xquat = (double*)malloc(32 * (size_t)nb);
+        xmat = (double*)malloc(72 * (size_t)nb);
+        gxpos = (double*)malloc(24 * (size_t)(ng + 1)); gxmat = (double*)malloc(72 * (size_t)(ng + 1));
+    }
+    set_qpos(s, q, qpos);
+    fk(s, qpos, xpos, xquat, xmat, gxpos, gxmat);
+    int ncon = 0, ndeep_tot = 0;
+    double cost = 0.0;
+    for (int k = 0; k < s->npair; ++k) {
+        const or_pair* pr = s->pairs + k;
+        if (pr->is_static && !(count_static || s->mode == 1)) continue;
+        int g1 = pr->g1, g2 = pr->g2;
+        double dc[3] = {gxpos[3 * g2] - gxpos[3 * g1], gxpos[3 * g2 + 1] - gxpos[3 * g1 + 1],
+                        gxpos[3 * g2 + 2] - gxpos[3 * g1 + 2]};
+        double r1 = s->rbound[g1], r2 = s->rbound[g2];
+        if (r1 > 0.0 && r2 > 0.0) { /* bounding-sphere broadphase with margin */
+            double thr = r1 + r2 + pr->margin;
+            if (dot3(dc, dc) > thr * thr) continue;
+        }
+        int nd = 0;
+        int nc = collide(s->geom_type[g1], gxpos + 3 * g1, gxmat + 9 * g1, s->geom_size + 3 * g1,
+                         s->geom_type[g2], gxpos + 3 * g2, gxmat + 9 * g2, s->geom_size + 3 * g2,
+                         pr->margin, &nd);
+        if (nc < 0) { ncon = -1000000; break; }
+        ncon += nc;
+        if (nd > 0) {
+            double cd = sqrt(dot3(dc, dc));
+            double term = -1.0 / (cd + 1e-4);
+            for (int i = 0; i < nd; ++i) cost = cost + term;
+            ndeep_tot += nd;
+        }
+    }
+    if (heap) { free(qpos); free(xpos); free(xquat); free(xmat); free(gxpos); free(gxmat); }
+    if (deep_cost) *deep_cost = cost;
+    if (n_deep) *n_deep = ndeep_tot;
+    return ncon;
+}
+
+/* ------------------------------------------------------------------ reductions
+ * Canonical order (shared with the GPU kernels): `lanes` lanes, lane l accumulates
+ * x[l], x[l+lanes], ... sequentially from 0.0; each 64-lane wave reduces its lanes by
+ * an xor butterfly (offsets 32,16,8,4,2,1); the wave sums are added in wave order. */
+int or_lanes_for(int items) {
+    int l = ((items + 63) / 64) * 64;
+    if (l < 64) l = 64;
+    if (l > 256) l = 256; /* workgroup size of the GPU kernels */
+    return l;
+}
+
+double or_canon_sum(const double* x, int n, int lanes) {
+    double part[1024], tmp[64];
+    for (int l = 0; l < lanes; ++l) {
+        double acc = 0.0;
+        for (int i = l; i < n; i += lanes) acc = acc + x[i];
+        part[l] = acc;
+    }
+    double total = 0.0;
+    for (int w = 0; w < lanes / 64; ++w) {
+        double* v = part + 64 * w;
+        for (int off = 32; off >= 1; off >>= 1) {
+            for (int l = 0; l < 64; ++l) tmp[l] = v[l] + v[l ^ off];
+            memcpy(v, tmp, sizeof(tmp));
+        }
+        total = (w == 0) ? v[0] : total + v[0];
+    }
+    return total;
+}
+
+static double seq_sum(const double* x, int n) {
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) acc = acc + x[i];
+    return acc;
+}
+
+static double dist_nd(const double* a, const double* b, int D) {
+    double d0 = b[0] - a[0];
+    double s = d0 * d0;
+    for (int d = 1; d < D; ++d) { double dd = b[d] - a[d]; s = fma(dd, dd, s); }
+    return sqrt(s);
+}
+
+/* ------------------------------------------------------------------ SamplingPathPlanner */
+int or_sspp_score(const or_scene* s, const double* knots, int nknots, int p, const double* ctrl,
+                  int n, int D, int64_t B, int W, int count_static, int sequential_sum,
+                  int nthreads, double* arc_out, uint8_t* feasible_out) {
+    if (W < 2 || D > OR_MAXD || p > OR_MAXP || nknots != n + p + 1) return -1;
+    if (s && s->mode == 0 && s->arg != D) return -2;
+    int bad = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(| : bad)
+#endif
+    for (int64_t b = 0; b < B; ++b) {
+        const double* c = ctrl + (size_t)b * n * D;
+        double q[OR_MAXD], q2[OR_MAXD];
+        /* include/sspp.h:132-150 checkCollision: points u = i/W, i = 0..W */
+        int feasible = 1;
+        if (s) {
+            for (int i = 0; i <= W; ++i) {
+                double u = (double)i / W;
+                or_spline_eval(knots, nknots, p, c, D, u, q);
+                int nc = or_point_contacts(s, q, count_static, NULL, NULL);
+                if (nc < 0) { bad = 1; break; }
+                if (nc > 0) { feasible = 0; break; }
+            }
+        }
+        /* include/sspp.h:152-169 computeArcLength: chords between u=(i-1)/(W-1), i/(W-1) */
+        double chords[4096];
+        double* ch = W - 1 <= 4096 ? chords : (double*)malloc(sizeof(double) * (size_t)(W - 1));
+        for (int i = 1; i < W; ++i) {
+            double u1 = (double)(i - 1) / (W - 1);
+            double u2 = (double)i / (W - 1);
+            or_spline_eval(knots, nknots, p, c, D, u1, q);
+            or_spline_eval(knots, nknots, p, c, D, u2, q2);
+            ch[i - 1] = dist_nd(q, q2, D);
+        }
+        arc_out[b] = sequential_sum ? seq_sum(ch, W - 1) : or_canon_sum(ch, W - 1, or_lanes_for(W - 1));
+        if (ch != chords) free(ch);
+        feasible_out[b] = (uint8_t)feasible;
+    }
+    return bad ? -3 : 0;
+}
+
+int64_t or_argmin(const double* cost, const uint8_t* feasible, int64_t B, double* best_cost) {
+    /* include/sspp.h:171-192 findBestPath: strict '<' from +inf; lowest index on ties */
+    double best = INFINITY;
+    int64_t idx = -1;
+    for (int64_t b = 0; b < B; ++b) {
+        if (!feasible[b]) continue;
+        if (cost[b] < best) { best = cost[b]; idx = b; }
+    }
+    if (best_cost) *best_cost = best;
+    return idx;
+}
+
+/* ------------------------------------------------------------------ TaskSpacePlanner */
+int or_tsp_score(const or_scene* s, const double* start, const double* end, const double* vias,
+                 int K, int64_t B, int cp, double w_collision, int sequential_sum, int nthreads,
+                 double* Lo, double* Cnfo, double* Cwfo, uint8_t* status, double* cost) {
+    if (cp < 1 || K < 0 || K > 62 || !s || s->mode != 1) return -1;
+    const int P = 2, D = 4, n = K + 2;
+    int bad = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(| : bad)
+#endif
+    for (int64_t b = 0; b < B; ++b) {
+        double pts[64 * 4], u[64], knots[64 + 3], ctrl[64 * 4];
+        /* tsp_path_model.h:11-43: [start, vias..., end] at u_i = i/(total-1) */
+        for (int i = 0; i < n; ++i) u[i] = (double)i / (n - 1);
+        for (int d = 0; d < D; ++d) { pts[d] = start[d]; pts[(n - 1) * D + d] = end[d]; }
+        for (int v = 0; v < K; ++v)
+            for (int d = 0; d < D; ++d) pts[(1 + v) * D + d] = vias[((size_t)b * K + v) * D + d];
+        if (or_interpolate(pts, n, D, P, u, knots, ctrl) != 0) { bad = 1; continue; }
+        int nk = n + P + 1;
+        /* tsp_evaluator.h:18-32 eval_one_pass */
+        double du = 1.0 / cp;
+        double prev[4], cur[4];
+        double Lb[4096], Cb[4096], Wb[4096];
+        double *Lv = Lb, *Cv = Cb, *Wv = Wb;
+        if (cp > 4096) {
+            Lv = (double*)malloc(8 * (size_t)cp); Cv = (double*)malloc(8 * (size_t)cp);
+            Wv = (double*)malloc(8 * (size_t)cp);
+        }
+        or_spline_eval(knots, nk, P, ctrl, D, 0.0, prev);
+        for (int i = 1; i <= cp; ++i) {
+            /* the reference evaluates s(i*du) and s((i-1)*du) as consecutive points;
+               each lane of the GPU kernel evaluates both, so do the same here */
+            double up = (double)(i - 1) * du, uc = (double)i * du;
+            or_spline_eval(knots, nk, P, ctrl, D, up, prev);
+            or_spline_eval(knots, nk, P, ctrl, D, uc, cur);
+            Lv[i - 1] = dist_nd(prev, cur, D);
+            double c = 0.0;
+            int nc = or_point_contacts(s, cur, 1, &c, NULL);
+            if (nc < 0) bad = 1;
+            /* floorPenalty with the evaluator's defaults */
+            double deficit = (0.0 + 0.01) - cur[2];
+            double fp = deficit > 0.0 ? (10.0 * deficit) * deficit : 0.0;
+            Cv[i - 1] = c;
+            Wv[i - 1] = c + fp;
+        }
+        double L, Cnf, Cwf;
+        if (sequential_sum) { L = seq_sum(Lv, cp); Cnf = seq_sum(Cv, cp); Cwf = seq_sum(Wv, cp); }
+        else {
+            int lanes = or_lanes_for(cp);
+            L = or_canon_sum(Lv, cp, lanes); Cnf = or_canon_sum(Cv, cp, lanes);
+            Cwf = or_canon_sum(Wv, cp, lanes);
+        }
+        if (Lv != Lb) { free(Lv); free(Cv); free(Wv); }
+        Lo[b] = L; Cnfo[b] = Cnf; Cwfo[b] = Cwf;
+        status[b] = (uint8_t)(Cnf == 0.0); /* tsp_planner.h:110 */
+        cost[b] = L + w_collision * Cwf;   /* tsp_planner.h:123 */
+    }
+    return bad ? -3 : 0;
+}
+
+int64_t or_tsp_best(const double* cost, const uint8_t* status, int64_t B, double* best_cost) {
+    /* tsp_planner.h:131-134 min_element over successes; lowest index on ties */
+    return or_argmin(cost, status, B, best_cost);
+}

@@ -1,0 +1,138 @@
+"""ctypes binding of include/sspp_hip.h (libsspp_hip.so, built in-tree by `make`).
+
+Fails loudly: if the HIP library is missing or does not export a declared symbol, importing
+the product raises — there is no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsspp_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "sspp_hip.h")
+
+SSPP_OK = 0
+MODE_QPOS = 0
+MODE_BODY = 1
+
+
+class SsppError(RuntimeError):
+    pass
+
+
+class ModelView(C.Structure):
+    _fields_ = [
+        ("nbody", C.c_int), ("body_parent", C.POINTER(C.c_int32)),
+        ("body_jnt_type", C.POINTER(C.c_int32)), ("body_qpos_adr", C.POINTER(C.c_int32)),
+        ("body_pos", C.POINTER(C.c_double)), ("body_quat", C.POINTER(C.c_double)),
+        ("ngeom", C.c_int), ("geom_type", C.POINTER(C.c_int32)),
+        ("geom_body", C.POINTER(C.c_int32)), ("geom_contype", C.POINTER(C.c_int32)),
+        ("geom_conaffinity", C.POINTER(C.c_int32)), ("geom_size", C.POINTER(C.c_double)),
+        ("geom_pos", C.POINTER(C.c_double)), ("geom_quat", C.POINTER(C.c_double)),
+        ("geom_margin", C.POINTER(C.c_double)), ("nexclude", C.c_int),
+        ("exclude", C.POINTER(C.c_int32)), ("nq", C.c_int), ("qpos0", C.POINTER(C.c_double)),
+    ]
+
+
+class Best(C.Structure):
+    _fields_ = [("cost", C.c_double), ("index", C.c_int64), ("count", C.c_int64),
+                ("reserved", C.c_int64)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("n_moving_geoms", C.c_int), ("n_static_geoms", C.c_int), ("n_pairs", C.c_int),
+                ("n_static_pairs", C.c_int), ("static_contacts", C.c_int),
+                ("n_movers", C.c_int), ("static_cost", C.c_double)]
+
+
+class SsppArgs(C.Structure):
+    _fields_ = [("knots", C.POINTER(C.c_double)), ("degree", C.c_int),
+                ("init_ctrl", C.POINTER(C.c_double)), ("n_ctrl", C.c_int), ("dof", C.c_int),
+                ("sigma", C.c_double), ("limits", C.POINTER(C.c_double)),
+                ("check_points", C.c_int), ("seed", C.c_uint64)]
+
+
+class TspArgs(C.Structure):
+    _fields_ = [("start", C.POINTER(C.c_double)), ("end", C.POINTER(C.c_double)),
+                ("n_vias", C.c_int), ("check_points", C.c_int), ("w_collision", C.c_double),
+                ("mean", C.POINTER(C.c_double)), ("sigma", C.POINTER(C.c_double)),
+                ("lo", C.POINTER(C.c_double)), ("hi", C.POINTER(C.c_double)),
+                ("z_min", C.c_double), ("seed", C.c_uint64), ("floor_z_min", C.c_double),
+                ("floor_margin", C.c_double), ("floor_scale", C.c_double)]
+
+
+_vp, _i64, _d, _i = C.c_void_p, C.c_int64, C.POINTER(C.c_double), C.c_int
+
+SIGNATURES = {
+    "sspp_last_error": (C.c_char_p, []),
+    "sspp_version": (C.c_int, []),
+    "sspp_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "sspp_model_load_mjcf": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
+    "sspp_model_view_get": (C.c_int, [_vp, C.POINTER(ModelView)]),
+    "sspp_model_body_id": (C.c_int, [_vp, C.c_char_p]),
+    "sspp_model_geom_id": (C.c_int, [_vp, C.c_char_p]),
+    "sspp_model_body_point": (C.c_int, [_vp, C.c_char_p, _d]),
+    "sspp_model_free": (None, [_vp]),
+    "sspp_scene_create": (C.c_int, [_vp, _i, _i, _i, C.POINTER(_vp)]),
+    "sspp_scene_get_info": (C.c_int, [_vp, C.POINTER(SceneInfo)]),
+    "sspp_scene_free": (None, [_vp]),
+    "sspp_interpolate": (C.c_int, [_d, _i, _i, _i, _d, _d, _d]),
+    "sspp_spline_eval": (C.c_int, [_d, _i, _i, _d, _i, C.c_double, _d]),
+    "sspp_job_create_sspp": (C.c_int, [_vp, C.POINTER(SsppArgs), _i64, C.POINTER(_vp)]),
+    "sspp_job_sample_score": (C.c_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "sspp_job_score_ctrl": (C.c_int, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "sspp_job_create_tsp": (C.c_int, [_vp, C.POINTER(TspArgs), _i64, C.POINTER(_vp)]),
+    "sspp_job_tsp_sample_score": (C.c_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                            _vp, _vp]),
+    "sspp_job_tsp_score_vias": (C.c_int, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          _vp]),
+    "sspp_job_info": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                C.POINTER(C.c_size_t)]),
+    "sspp_job_free": (None, [_vp]),
+    "sspp_best_reduce": (C.c_int, [C.POINTER(Best), _i, C.POINTER(Best)]),
+    "sspp_best_reduce_device": (C.c_int, [_vp, _i, _vp, _vp]),
+    "sspp_plan_sspp": (C.c_int, [_vp, _i, _d, _d, C.c_double, _d, _i, _i, _i, C.c_uint64, _d, _d,
+                                 C.POINTER(C.c_uint8), _d, C.POINTER(Best)]),
+    "sspp_score_ctrl_host": (C.c_int, [_vp, _d, _i, _d, _i64, _i, _i, _i, _d,
+                                       C.POINTER(C.c_uint8), C.POINTER(Best)]),
+    "sspp_sample_ctrl_host": (C.c_int, [_d, _i, _d, _i, _i, C.c_double, _d, C.c_uint64, _i64,
+                                        _i64, _d]),
+}
+
+
+def declared_symbols(header=HEADER_PATH):
+    """Function names declared in include/sspp_hip.h."""
+    txt = open(header).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(sspp_[a-z_0-9]+)\s*\(", txt)))
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SsppError("HIP library not built: %s (run `make` or __graft_entry__.build())"
+                            % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)  # AttributeError -> missing export: fail loudly
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error():
+    return lib().sspp_last_error().decode(errors="replace")
+
+
+def check(rc, what=""):
+    if rc < 0:
+        msg = last_error()
+        raise SsppError("%s failed (%d): %s" % (what, rc, msg))
+    return rc

@@ -1,0 +1,38 @@
+// model.h — host-side scene model (MuJoCo-like flat arrays) and shared host helpers.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/sspp_hip.h"
+
+struct sspp_model {
+    std::string path;
+    std::vector<std::string> body_names, geom_names;
+    std::vector<int32_t> body_parent, body_jnt_type, body_qpos_adr;
+    std::vector<double> body_pos, body_quat;
+    std::vector<int32_t> geom_type, geom_body, geom_contype, geom_conaffinity;
+    std::vector<double> geom_size, geom_pos, geom_quat, geom_margin;
+    std::vector<int32_t> exclude;
+    std::vector<double> qpos0;
+    int nbody() const { return (int)body_parent.size(); }
+    int ngeom() const { return (int)geom_type.size(); }
+};
+
+namespace sspp {
+// thread-local error message plumbing (sspp_last_error)
+int set_error(int code, const std::string& msg);
+void clear_error();
+
+// MJCF -> model (mjcf.cpp)
+int load_mjcf(const std::string& path, sspp_model& out);
+
+// spline helpers (spline_host.cpp) — Eigen Splines semantics
+void knot_averaging(const double* u, int n, int p, double* knots);
+int span_of(double u, int p, const double* knots, int nknots);
+void basis_funcs(double u, int p, const double* knots, int nknots, double* N);
+int interpolate(const double* pts, int n, int D, int p, const double* u, double* knots,
+                double* ctrl);
+// collocation inverse for fixed parameters u (PathModel::fromVias precompute)
+int collocation_inverse(const double* u, int n, int p, double* knots, double* Minv);
+}  // namespace sspp

@@ -1,0 +1,1099 @@
+// sspp_kernels.hip — MI355X (gfx950) kernels for sampled-spline candidate scoring.
+//
+// Hot path (reference include/sspp.h:194-225 and include/sspp/tsp_planner.h:95-138):
+//   candidate sampling -> B-spline evaluation -> free-joint FK -> collision -> cost -> argmin.
+//
+// Work decomposition:
+//   * a candidate owns LPC = 64*ceil(items/64) lanes (capped at 256), one waypoint per lane;
+//     a 256-thread workgroup holds CPB = 256/LPC candidates;
+//   * the workgroup prologue builds the shared basis tables (span + N_0..N_p for every
+//     waypoint parameter) and the candidates' control points in LDS (Philox + Box-Muller
+//     in-kernel, or a coalesced copy of caller-supplied control points);
+//   * each lane evaluates its waypoint(s): spline from LDS, FK of the moving body, pair
+//     loop over the scene table (wave-uniform -> scalar loads), broadphase + narrowphase;
+//   * per-candidate sums use the canonical order (lane partials, xor butterfly per wave,
+//     waves in order) that oracle/sspp_oracle.c::or_canon_sum restates;
+//   * one BlockBest per workgroup, then a one-block argmin kernel (lowest id on ties).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "model.h"
+#include "sspp_device.h"
+
+using namespace sspd;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxMovers = 2;
+
+struct KScene {
+    const DGeom* geoms;
+    const DPair* pairs;
+    const DMover* movers;
+    int npairs;
+    int static_block;   // sspp: env-env contacts counted and present -> nothing feasible
+    double static_cost; // tsp: Collision.h cost of env-env contacts, added per waypoint
+};
+
+struct BlockBest {
+    double cost;
+    long long idx;
+    long long count;
+    long long pad;
+};
+
+struct SsppK {
+    KScene sc;
+    int has_scene;
+    const double* knots;
+    int nknots, p, n, W;
+    const double* init_ctrl;
+    const double* ctrl_in;
+    double* ctrl_out;
+    double sigma;
+    const double* limits;
+    unsigned long long seed;
+    long long first_id, B;
+    double* arc;
+    unsigned char* feasible;
+    BlockBest* part;
+    int lpc, cpb, shared_endpoints;
+};
+
+struct TspK {
+    KScene sc;
+    const double* knots;
+    int nknots, n, K, cp;
+    const double* Minv;
+    double start[4], end[4], lo[4], hi[4];
+    const double* mean;
+    const double* sigma;
+    double z_min;
+    const double* vias_in;
+    double* vias_out;
+    unsigned long long seed;
+    long long first_id, B;
+    double w_col, floor_z_min, floor_margin, floor_scale;
+    double *L, *Cnf, *Cwf, *cost;
+    unsigned char* status;
+    BlockBest* part;
+    int lpc, cpb;
+};
+
+// ---------------------------------------------------------------- Philox4x32-10 + Box-Muller
+__device__ __forceinline__ void philox(unsigned c0, unsigned c1, unsigned c2, unsigned c3,
+                                       unsigned k0, unsigned k1, unsigned o[4]) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        unsigned hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        unsigned hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        unsigned n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    o[0] = c0; o[1] = c1; o[2] = c2; o[3] = c3;
+}
+__device__ __forceinline__ void philox_words(unsigned long long seed, unsigned long long g,
+                                             unsigned idx, unsigned stream, unsigned o[4]) {
+    philox(idx, stream, (unsigned)g, (unsigned)(g >> 32), (unsigned)seed, (unsigned)(seed >> 32), o);
+}
+__device__ __forceinline__ void normal_pair(unsigned long long seed, unsigned long long g,
+                                            unsigned idx, unsigned stream, double* z0, double* z1) {
+    unsigned o[4];
+    philox_words(seed, g, idx, stream, o);
+    unsigned long long a = ((((unsigned long long)o[0]) << 32) | o[1]) >> 11;
+    unsigned long long b = ((((unsigned long long)o[2]) << 32) | o[3]) >> 11;
+    double u1 = (double)(a + 1) * 1.1102230246251565e-16;
+    double u2 = (double)b * 1.1102230246251565e-16;
+    double r = sqrt(-2.0 * log(u1));
+    double th = 6.283185307179586 * u2;
+    *z0 = r * cos(th);
+    *z1 = r * sin(th);
+}
+__device__ __forceinline__ double uniform01(unsigned long long seed, unsigned long long g,
+                                            unsigned idx, unsigned stream) {
+    unsigned o[4];
+    philox_words(seed, g, idx, stream, o);
+    unsigned long long b = ((((unsigned long long)o[2]) << 32) | o[3]) >> 11;
+    return (double)b * 1.1102230246251565e-16;
+}
+
+// ---------------------------------------------------------------- spline from LDS tables
+template <int D>
+__device__ __forceinline__ void eval_pt(const double* ctrl, const double* N, int span, int p,
+                                        double* q) {
+    const double* c0 = ctrl + (span - p) * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        double acc = N[0] * c0[d];
+        for (int r = 1; r <= p; ++r) acc = fma(N[r], c0[r * D + d], acc);
+        q[d] = acc;
+    }
+}
+
+template <int D>
+__device__ __forceinline__ double dist_nd(const double* a, const double* b) {
+    double d0 = b[0] - a[0];
+    double s = d0 * d0;
+#pragma unroll
+    for (int d = 1; d < D; ++d) { double dd = b[d] - a[d]; s = fma(dd, dd, s); }
+    return sqrt(s);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------- one waypoint vs the scene
+// MODE 0: q = qpos[0:D] window (SamplingPathPlanner); MODE 1: q = (x, y, z, yaw) body point.
+// DEEP=false: returns 1 at the first contact (checkCollision's ncon > 0).
+// DEEP=true : returns 0, *cost = sum over deep contacts of -1/(center_dist + 1e-4).
+template <int D, int NM, int MODE, bool DEEP>
+__device__ int point_collide(const double* q, const KScene& sc, double* cost) {
+    double mp[NM][3], mR[NM][9];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        double qp[7];
+        if (MODE == 0) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) qp[k] = (7 * m + k < D) ? q[(7 * m + k < D) ? 7 * m + k : 0]
+                                                                : sc.movers[m].qpos0[k];
+        } else {
+            double half = q[3] * 0.5;
+            qp[0] = q[0]; qp[1] = q[1]; qp[2] = q[2];
+            qp[3] = cos(half); qp[4] = 0.0; qp[5] = 0.0; qp[6] = sin(half);
+        }
+        normalize4(qp + 3);
+        quat2mat(qp + 3, mR[m]);
+        mp[m][0] = qp[0]; mp[m][1] = qp[1]; mp[m][2] = qp[2];
+    }
+    double acc = 0.0;
+    int cur = -1;
+    double gp[3], gmat[9];
+    for (int k = 0; k < sc.npairs; ++k) {
+        const DPair pr = sc.pairs[k];
+        const DGeom& G = sc.geoms[pr.gm];
+        if (pr.gm != cur) {
+            cur = pr.gm;
+            const int m = (NM == 1) ? 0 : G.mover;
+            const double* R = mR[0];
+            const double* P = mp[0];
+            if (NM > 1 && m == 1) { R = mR[NM - 1]; P = mp[NM - 1]; }
+            double t[3];
+            matvec3(R, G.pos, t);
+            gp[0] = P[0] + t[0]; gp[1] = P[1] + t[1]; gp[2] = P[2] + t[2];
+            matmul3(R, G.mat, gmat);
+        }
+        const DGeom& O = sc.geoms[pr.go];
+        double op_[3], om_[9];
+        const double* op = O.pos;
+        const double* om = O.mat;
+        if (NM > 1 && O.mover >= 0) {
+            const double* R = (O.mover == 0) ? mR[0] : mR[NM - 1];
+            const double* P = (O.mover == 0) ? mp[0] : mp[NM - 1];
+            double t[3];
+            matvec3(R, O.pos, t);
+            op_[0] = P[0] + t[0]; op_[1] = P[1] + t[1]; op_[2] = P[2] + t[2];
+            matmul3(R, O.mat, om_);
+            op = op_; om = om_;
+        }
+        double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
+        const double rg = G.rbound, ro = O.rbound;
+        if (rg > 0.0 && ro > 0.0) {
+            double thr = rg + ro + pr.margin;
+            if (dot3(dc, dc) > thr * thr) continue;
+        }
+        int nd = 0, nc;
+        const bool gfirst = (G.type < O.type) || (G.type == O.type && G.orig < O.orig);
+        if (gfirst) nc = collide<DEEP>(G.type, gp, gmat, G.size, O.type, op, om, O.size, pr.margin, &nd);
+        else nc = collide<DEEP>(O.type, op, om, O.size, G.type, gp, gmat, G.size, pr.margin, &nd);
+        if (!DEEP) {
+            if (nc > 0) return 1;
+        } else if (nd > 0) {
+            double cd = sqrt(dot3(dc, dc));
+            double term = -1.0 / (cd + 1e-4);
+            for (int i = 0; i < nd; ++i) acc = acc + term;
+        }
+    }
+    if (DEEP) *cost = acc + sc.static_cost;
+    return 0;
+}
+
+// ---------------------------------------------------------------- SamplingPathPlanner kernel
+template <int D, int NM>
+__global__ __launch_bounds__(kBlock) void k_sspp(SsppK a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, p = a.p, n = a.n, W = a.W;
+    const int P1 = p + 1, ndof = n * D;
+    const int slot = tid / lpc, lane = tid - slot * lpc;
+    const long long cand0 = (long long)blockIdx.x * cpb;
+    double* s_ctrl = smem;
+    double* s_bcol = s_ctrl + cpb * ndof;
+    double* s_barc = s_bcol + (W + 1) * P1;
+    double* s_wsum = s_barc + W * P1;
+    double* s_arc = s_wsum + kBlock / 64;
+    int* s_scol = (int*)(s_arc + 4);
+    int* s_sarc = s_scol + (W + 1);
+    int* s_flag = s_sarc + W;  // [cpb] per-candidate feasibility, [cpb] shared endpoints
+
+    // basis tables: collision grid u = i/W (i = 0..W), arc grid v = i/(W-1) (i = 0..W-1)
+    for (int r = tid; r < 2 * W + 1; r += kBlock) {
+        double u;
+        double* dst;
+        int* sd;
+        if (r <= W) { u = (double)r / W; dst = s_bcol + r * P1; sd = s_scol + r; }
+        else { int i = r - (W + 1); u = (double)i / (W - 1); dst = s_barc + i * P1; sd = s_sarc + i; }
+        int sp = span_of(u, p, a.knots, a.nknots);
+        double N[kMaxP + 1];
+        basis_funcs(u, p, sp, a.knots, N);
+        for (int j = 0; j <= p; ++j) dst[j] = N[j];
+        *sd = sp;
+    }
+    if (tid <= cpb) s_flag[tid] = 1;
+
+    // control points
+    const long long nvalid = min((long long)cpb, a.B - cand0);
+    if (a.ctrl_in) {
+        const double* src = a.ctrl_in + cand0 * ndof;
+        for (int e = tid; e < nvalid * ndof; e += kBlock) s_ctrl[e] = src[e];
+    } else {
+        for (int e = tid; e < cpb * ndof; e += kBlock) s_ctrl[e] = a.init_ctrl[e % ndof];
+        __syncthreads();
+        const int npert = (n - 2 * p) * D;
+        const int npairs = (npert + 1) >> 1;
+        for (int e = tid; e < cpb * npairs; e += kBlock) {
+            const int s = e / npairs, m = e - s * npairs;
+            if (s >= nvalid) continue;
+            const unsigned long long g = (unsigned long long)(a.first_id + cand0 + s);
+            double z0, z1;
+            normal_pair(a.seed, g, (unsigned)m, 0u, &z0, &z1);
+            double* c = s_ctrl + s * ndof + p * D;
+            const int k0 = 2 * m, k1 = 2 * m + 1;
+            {
+                const int d = k0 % D;
+                double noise = (a.sigma * z0) * a.limits[d];
+                c[k0] = c[k0] + noise;
+            }
+            if (k1 < npert) {
+                const int d = k1 % D;
+                double noise = (a.sigma * z1) * a.limits[d];
+                c[k1] = c[k1] + noise;
+            }
+        }
+    }
+    __syncthreads();
+    if (a.ctrl_out) {
+        double* dst = a.ctrl_out + cand0 * ndof;
+        for (int e = tid; e < nvalid * ndof; e += kBlock) dst[e] = s_ctrl[e];
+    }
+
+    const bool valid = slot < nvalid;
+    const double* myc = s_ctrl + slot * ndof;
+    double q[D], q2[D];
+
+    // checkCollision: interior points i = 1..W-1 one per lane; endpoints i = 0, W on a spare lane
+    if (a.has_scene && valid) {
+        volatile int* vflag = s_flag;
+        if (a.sc.static_block) vflag[slot] = 0;
+        for (int j = lane; j < W - 1; j += lpc) {
+            if (vflag[slot] == 0) break;
+            const int i = j + 1;
+            eval_pt<D>(myc, s_bcol + i * P1, s_scol[i], p, q);
+            if (point_collide<D, NM, 0, false>(q, a.sc, nullptr)) { vflag[slot] = 0; break; }
+        }
+        const int spare = (W - 1) % lpc == 0 ? 0 : lpc - 1;
+        bool duty0 = false, dutyW = false;
+        int fidx = slot;
+        if (a.shared_endpoints) {
+            fidx = cpb;
+            if (lane == spare) {
+                if (cpb == 1) { duty0 = dutyW = true; }
+                else { duty0 = slot == 0; dutyW = slot == 1; }
+            }
+        } else if (lane == spare) {
+            duty0 = dutyW = true;
+        }
+        if (duty0) {
+            eval_pt<D>(myc, s_bcol, s_scol[0], p, q);
+            if (point_collide<D, NM, 0, false>(q, a.sc, nullptr)) vflag[fidx] = 0;
+        }
+        if (dutyW) {
+            eval_pt<D>(myc, s_bcol + W * P1, s_scol[W], p, q);
+            if (point_collide<D, NM, 0, false>(q, a.sc, nullptr)) vflag[fidx] = 0;
+        }
+    }
+
+    // computeArcLength: chords between v_{i-1} and v_i, i = 1..W-1
+    double acc = 0.0;
+    if (valid) {
+        for (int j = lane; j < W - 1; j += lpc) {
+            const int i = j + 1;
+            eval_pt<D>(myc, s_barc + (i - 1) * P1, s_sarc[i - 1], p, q);
+            eval_pt<D>(myc, s_barc + i * P1, s_sarc[i], p, q2);
+            acc = acc + dist_nd<D>(q, q2);
+        }
+    }
+    acc = wave_sum(acc);
+    if ((tid & 63) == 0) s_wsum[tid >> 6] = acc;
+    __syncthreads();
+    if (lane == 0 && valid) {
+        const int w0 = (slot * lpc) >> 6, nw = lpc >> 6;
+        double t = s_wsum[w0];
+        for (int w = 1; w < nw; ++w) t = t + s_wsum[w0 + w];
+        const long long c = cand0 + slot;
+        const int f = s_flag[slot] & s_flag[cpb];
+        a.arc[c] = t;
+        a.feasible[c] = (unsigned char)f;
+        s_arc[slot] = f ? t : INFINITY;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        BlockBest bb;
+        bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
+        for (int s = 0; s < nvalid; ++s) {
+            if (!(s_flag[s] & s_flag[cpb])) continue;
+            bb.count++;
+            if (s_arc[s] < bb.cost) { bb.cost = s_arc[s]; bb.idx = a.first_id + cand0 + s; }
+        }
+        a.part[blockIdx.x] = bb;
+    }
+}
+
+// ---------------------------------------------------------------- TaskSpacePlanner kernel
+template <int NM>
+__global__ __launch_bounds__(kBlock) void k_tsp(TspK a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int D = 4, P = 2, P1 = 3;
+    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, K = a.K, cp = a.cp;
+    const int slot = tid / lpc, lane = tid - slot * lpc;
+    const long long cand0 = (long long)blockIdx.x * cpb;
+    const int ndof = n * D;
+    double* s_V = smem;                      // [cpb][n][4]
+    double* s_ctrl = s_V + cpb * ndof;       // [cpb][n][4]
+    double* s_b = s_ctrl + cpb * ndof;       // [(cp+1)][3]
+    double* s_wsum = s_b + (cp + 1) * P1;    // [3][4]
+    double* s_best = s_wsum + 3 * (kBlock / 64);
+    int* s_span = (int*)(s_best + 4);        // [cp+1]
+    int* s_stat = s_span + (cp + 1);         // [cpb]
+
+    const double du = 1.0 / cp;
+    for (int r = tid; r <= cp; r += kBlock) {
+        const double u = (double)r * du;
+        int sp = span_of(u, P, a.knots, a.nknots);
+        double N[kMaxP + 1];
+        basis_funcs(u, P, sp, a.knots, N);
+        for (int j = 0; j <= P; ++j) s_b[r * P1 + j] = N[j];
+        s_span[r] = sp;
+    }
+    const long long nvalid = min((long long)cpb, a.B - cand0);
+    // via points: V = [start, vias..., end]
+    for (int e = tid; e < cpb * 2 * D; e += kBlock) {
+        const int s = e / (2 * D), r = e - s * 2 * D;
+        if (r < D) s_V[s * ndof + r] = a.start[r];
+        else s_V[s * ndof + (n - 1) * D + (r - D)] = a.end[r - D];
+    }
+    if (a.vias_in) {
+        for (int e = tid; e < nvalid * K * D; e += kBlock) {
+            const int s = e / (K * D), r = e - s * K * D;
+            s_V[s * ndof + D + r] = a.vias_in[(cand0 + s) * K * D + r];
+        }
+    } else {
+        // Sampler::sample_set (tsp_sampler.h:12-51) with Philox streams per (candidate, via, dim)
+        for (int e = tid; e < cpb * K * D; e += kBlock) {
+            const int s = e / (K * D), r = e - s * K * D;
+            if (s >= nvalid) continue;
+            const int v = r / D, i = r - v * D;
+            const unsigned long long g = (unsigned long long)(a.first_id + cand0 + s);
+            const double m = a.mean[v * D + i], sg = a.sigma[v * D + i];
+            double val;
+            if (i < 3) {
+                bool ok = false;
+                val = 0.0;
+                for (int t = 0; t < 99; ++t) {
+                    double z0, z1;
+                    normal_pair(a.seed, g, (unsigned)(((v * 4 + i) << 7) | t), 1u, &z0, &z1);
+                    val = z0 * sg;
+                    val = val + m;
+                    if (!(val < a.lo[i] || val > a.hi[i])) { ok = true; break; }
+                }
+                if (!ok) {
+                    double u = uniform01(a.seed, g, (unsigned)(((v * 4 + i) << 7) | 127), 1u);
+                    val = u * (a.hi[i] - a.lo[i]);
+                    val = val + a.lo[i];
+                }
+                if (i == 2 && val < a.z_min) val = a.z_min;
+            } else if (a.lo[3] != a.hi[3]) {
+                double z0, z1;
+                normal_pair(a.seed, g, (unsigned)((v * 4 + 3) << 7), 1u, &z0, &z1);
+                val = z0 * sg;
+                val = val + m;
+                const double range = a.hi[3] - a.lo[3];
+                while (val < a.lo[3]) val += range;
+                while (val > a.hi[3]) val -= range;
+            } else {
+                val = m;
+            }
+            s_V[s * ndof + D + r] = val;
+        }
+    }
+    __syncthreads();
+    if (a.vias_out) {
+        for (int e = tid; e < nvalid * K * D; e += kBlock) {
+            const int s = e / (K * D), r = e - s * K * D;
+            a.vias_out[(cand0 + s) * K * D + r] = s_V[s * ndof + D + r];
+        }
+    }
+    // PathModel::fromVias: ctrl = A^-1 V (collocation inverse precomputed on the host)
+    for (int e = tid; e < cpb * ndof; e += kBlock) {
+        const int s = e / ndof, r = e - s * ndof, j = r / D, d = r - j * D;
+        const double* Vs = s_V + s * ndof;
+        double acc = a.Minv[j * n] * Vs[d];
+        for (int i = 1; i < n; ++i) acc = fma(a.Minv[j * n + i], Vs[i * D + d], acc);
+        s_ctrl[e] = acc;
+    }
+    __syncthreads();
+
+    // Evaluator::eval_one_pass (tsp_evaluator.h:18-32), waypoint i = 1..cp per lane
+    const bool valid = slot < nvalid;
+    const double* myc = s_ctrl + slot * ndof;
+    double aL = 0.0, aC = 0.0, aW = 0.0;
+    if (valid) {
+        for (int j = lane; j < cp; j += lpc) {
+            const int i = j + 1;
+            double pv[4], pc[4];
+            eval_pt<D>(myc, s_b + (i - 1) * P1, s_span[i - 1], P, pv);
+            eval_pt<D>(myc, s_b + i * P1, s_span[i], P, pc);
+            aL = aL + dist_nd<D>(pv, pc);
+            double c = 0.0;
+            point_collide<D, NM, 1, true>(pc, a.sc, &c);
+            const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
+            const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
+            aC = aC + c;
+            aW = aW + (c + fp);
+        }
+    }
+    aL = wave_sum(aL);
+    aC = wave_sum(aC);
+    aW = wave_sum(aW);
+    constexpr int NW = kBlock / 64;
+    if ((tid & 63) == 0) {
+        s_wsum[tid >> 6] = aL;
+        s_wsum[NW + (tid >> 6)] = aC;
+        s_wsum[2 * NW + (tid >> 6)] = aW;
+    }
+    __syncthreads();
+    if (lane == 0 && valid) {
+        const int w0 = (slot * lpc) >> 6, nw = lpc >> 6;
+        double L = s_wsum[w0], Cn = s_wsum[NW + w0], Cw = s_wsum[2 * NW + w0];
+        for (int w = 1; w < nw; ++w) {
+            L = L + s_wsum[w0 + w];
+            Cn = Cn + s_wsum[NW + w0 + w];
+            Cw = Cw + s_wsum[2 * NW + w0 + w];
+        }
+        const long long c = cand0 + slot;
+        const int st = Cn == 0.0;
+        const double cost = L + a.w_col * Cw;
+        a.L[c] = L; a.Cnf[c] = Cn; a.Cwf[c] = Cw; a.cost[c] = cost;
+        a.status[c] = (unsigned char)st;
+        s_stat[slot] = st;
+        s_best[slot] = cost;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        BlockBest bb;
+        bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
+        for (int s = 0; s < nvalid; ++s) {
+            if (!s_stat[s]) continue;
+            bb.count++;
+            if (s_best[s] < bb.cost) { bb.cost = s_best[s]; bb.idx = a.first_id + cand0 + s; }
+        }
+        a.part[blockIdx.x] = bb;
+    }
+}
+
+// ---------------------------------------------------------------- argmin over block results
+__device__ __forceinline__ bool better(double c1, long long i1, double c2, long long i2) {
+    // lexicographic (cost, index); index -1 means "none"
+    if (i2 < 0) return i1 >= 0;
+    if (i1 < 0) return false;
+    return (c1 < c2) || (c1 == c2 && i1 < i2);
+}
+
+__global__ __launch_bounds__(kBlock) void k_argmin(const BlockBest* part, int nparts,
+                                                   sspp_best* out) {
+    __shared__ double sc[kBlock];
+    __shared__ long long si[kBlock], sn[kBlock];
+    double bc = INFINITY;
+    long long bi = -1, cnt = 0;
+    for (int i = threadIdx.x; i < nparts; i += kBlock) {
+        const BlockBest b = part[i];
+        cnt += b.count;
+        if (better(b.cost, b.idx, bc, bi)) { bc = b.cost; bi = b.idx; }
+    }
+    sc[threadIdx.x] = bc; si[threadIdx.x] = bi; sn[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            const int o = threadIdx.x + s;
+            if (better(sc[o], si[o], sc[threadIdx.x], si[threadIdx.x])) {
+                sc[threadIdx.x] = sc[o]; si[threadIdx.x] = si[o];
+            }
+            sn[threadIdx.x] += sn[o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out->cost = si[0] < 0 ? INFINITY : sc[0];
+        out->index = si[0];
+        out->count = sn[0];
+        out->reserved = 0;
+    }
+}
+
+int lanes_for(int items) {
+    int l = ((items + 63) / 64) * 64;
+    return std::min(std::max(l, 64), kBlock);
+}
+
+}  // namespace
+
+// =============================================================== host side: scene + jobs
+struct sspp_scene {
+    int mode, arg, dof;
+    int count_static;
+    std::vector<DGeom> geoms;
+    std::vector<DPair> pairs;
+    std::vector<DMover> movers;
+    int n_moving_geoms = 0, n_static_geoms = 0, n_static_pairs = 0, static_contacts = 0;
+    double static_cost = 0.0;
+    DGeom* d_geoms = nullptr;
+    DPair* d_pairs = nullptr;
+    DMover* d_movers = nullptr;
+    int device = 0;
+};
+
+struct sspp_job {
+    int kind = 0;  // 0 sspp, 1 tsp
+    const sspp_scene* scene = nullptr;
+    int D = 0, p = 0, n = 0, W = 0, nknots = 0, K = 0, cp = 0;
+    int lpc = 0, cpb = 0, nm = 1, shared_endpoints = 0;
+    size_t lds = 0;
+    int64_t max_batch = 0;
+    double sigma = 0.0;
+    uint64_t seed = 0;
+    double* d_knots = nullptr;
+    double* d_init = nullptr;
+    double* d_limits = nullptr;
+    double* d_Minv = nullptr;
+    double* d_mean = nullptr;
+    double* d_sigma = nullptr;
+    BlockBest* d_part = nullptr;
+    double start[4], end[4], lo[4], hi[4];
+    double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+    return sspp::set_error(SSPP_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIPCHK(x)                                   \
+    do {                                            \
+        hipError_t e_ = (x);                        \
+        if (e_ != hipSuccess) return hip_fail(e_, #x); \
+    } while (0)
+
+template <class T>
+int upload(T** dst, const T* src, size_t count) {
+    if (count == 0) { *dst = nullptr; return SSPP_OK; }
+    HIPCHK(hipMalloc((void**)dst, sizeof(T) * count));
+    HIPCHK(hipMemcpy(*dst, src, sizeof(T) * count, hipMemcpyHostToDevice));
+    return SSPP_OK;
+}
+
+// MuJoCo-like kinematics on the host (same operation order as oracle/sspp_oracle.c::fk)
+void host_fk(const sspp_model& m, const std::vector<double>& qpos, std::vector<double>& xpos,
+             std::vector<double>& xquat, std::vector<double>& xmat, std::vector<double>& gxpos,
+             std::vector<double>& gxmat) {
+    int nb = m.nbody(), ng = m.ngeom();
+    xpos.assign(3 * nb, 0.0); xquat.assign(4 * nb, 0.0); xmat.assign(9 * nb, 0.0);
+    gxpos.assign(3 * ng, 0.0); gxmat.assign(9 * ng, 0.0);
+    xquat[0] = 1.0;
+    quat2mat(&xquat[0], &xmat[0]);
+    for (int b = 1; b < nb; ++b) {
+        double* p = &xpos[3 * b];
+        double* q = &xquat[4 * b];
+        if (m.body_jnt_type[b] == 0) {
+            const double* qp = &qpos[m.body_qpos_adr[b]];
+            p[0] = qp[0]; p[1] = qp[1]; p[2] = qp[2];
+            q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
+        } else {
+            int pa = m.body_parent[b];
+            double t[3];
+            matvec3(&xmat[9 * pa], &m.body_pos[3 * b], t);
+            p[0] = xpos[3 * pa] + t[0]; p[1] = xpos[3 * pa + 1] + t[1]; p[2] = xpos[3 * pa + 2] + t[2];
+            mulquat(&xquat[4 * pa], &m.body_quat[4 * b], q);
+        }
+        normalize4(q);
+        quat2mat(q, &xmat[9 * b]);
+    }
+    for (int g = 0; g < ng; ++g) {
+        int b = m.geom_body[g];
+        double t[3], gq[4];
+        matvec3(&xmat[9 * b], &m.geom_pos[3 * g], t);
+        gxpos[3 * g] = xpos[3 * b] + t[0];
+        gxpos[3 * g + 1] = xpos[3 * b + 1] + t[1];
+        gxpos[3 * g + 2] = xpos[3 * b + 2] + t[2];
+        mulquat(&xquat[4 * b], &m.geom_quat[4 * g], gq);
+        normalize4(gq);
+        quat2mat(gq, &gxmat[9 * g]);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int sspp_scene_create(const sspp_model* m, int mode, int arg, int count_static, sspp_scene** out) {
+    sspp::clear_error();
+    if (!m || !out) return sspp::set_error(SSPP_E_INVAL, "sspp_scene_create: null argument");
+    const int nb = m->nbody(), ng = m->ngeom();
+    std::vector<int> weld(nb, 0), moving(nb, 0);
+    for (int b = 1; b < nb; ++b)
+        weld[b] = (m->body_jnt_type[b] != -1) ? b : weld[m->body_parent[b]];
+    std::vector<int> mover_of(nb, -1);
+    std::vector<int> mover_bodies;
+    if (mode == SSPP_MODE_QPOS) {
+        if (arg < 1 || arg > 16) return sspp::set_error(SSPP_E_INVAL, "dof must be in [1, 16]");
+        if (arg > (int)m->qpos0.size())
+            return sspp::set_error(SSPP_E_SCENE, "model has nq=" + std::to_string(m->qpos0.size()) +
+                                                     " < dof=" + std::to_string(arg));
+        for (int b = 1; b < nb; ++b)
+            if (m->body_jnt_type[b] == 0 && m->body_qpos_adr[b] < arg) {
+                moving[b] = 1;
+                mover_of[b] = (int)mover_bodies.size();
+                mover_bodies.push_back(b);
+            }
+    } else if (mode == SSPP_MODE_BODY) {
+        if (arg <= 0 || arg >= nb || m->body_jnt_type[arg] != 0)
+            return sspp::set_error(SSPP_E_SCENE, "collision body must have a free joint");
+        moving[arg] = 1;
+        mover_of[arg] = 0;
+        mover_bodies.push_back(arg);
+    } else {
+        return sspp::set_error(SSPP_E_INVAL, "unknown scene mode");
+    }
+    if ((int)mover_bodies.size() > kMaxMovers)
+        return sspp::set_error(SSPP_E_UNSUPPORTED, "more than 2 moving free bodies");
+    for (size_t i = 0; i < mover_bodies.size(); ++i)
+        if (mode == SSPP_MODE_QPOS && m->body_qpos_adr[mover_bodies[i]] != 7 * (int)i)
+            return sspp::set_error(SSPP_E_UNSUPPORTED, "free joints must occupy qpos[7k:7k+7]");
+
+    auto* s = new sspp_scene();
+    s->mode = mode; s->arg = arg; s->dof = mode == SSPP_MODE_QPOS ? arg : 4;
+    s->count_static = count_static;
+    (void)hipGetDevice(&s->device);
+
+    // kinematics at qpos0: world poses of static geoms
+    std::vector<double> xpos, xquat, xmat, gxpos, gxmat;
+    host_fk(*m, m->qpos0, xpos, xquat, xmat, gxpos, gxmat);
+    // moving geoms relative to their mover root: same FK with every mover at the identity
+    std::vector<double> qrel = m->qpos0;
+    for (int b : mover_bodies) {
+        int adr = m->body_qpos_adr[b];
+        double id[7] = {0, 0, 0, 1, 0, 0, 0};
+        for (int k = 0; k < 7; ++k) qrel[adr + k] = id[k];
+    }
+    std::vector<double> rxpos, rxquat, rxmat, rgxpos, rgxmat;
+    host_fk(*m, qrel, rxpos, rxquat, rxmat, rgxpos, rgxmat);
+
+    std::vector<int> table_index(ng, -1);
+    for (int g = 0; g < ng; ++g) {
+        int b = m->geom_body[g];
+        int w = weld[b];
+        bool mv = moving[w];
+        DGeom dg{};
+        dg.type = m->geom_type[g];
+        dg.mover = mv ? mover_of[w] : -1;
+        dg.orig = g;
+        const std::vector<double>& P = mv ? rgxpos : gxpos;
+        const std::vector<double>& M = mv ? rgxmat : gxmat;
+        for (int k = 0; k < 3; ++k) dg.pos[k] = P[3 * g + k];
+        for (int k = 0; k < 9; ++k) dg.mat[k] = M[9 * g + k];
+        for (int k = 0; k < 3; ++k) dg.size[k] = m->geom_size[3 * g + k];
+        dg.rbound = geom_rbound(dg.type, dg.size);
+        table_index[g] = (int)s->geoms.size();
+        s->geoms.push_back(dg);
+        if (m->geom_contype[g] || m->geom_conaffinity[g]) {
+            if (mv) s->n_moving_geoms++; else s->n_static_geoms++;
+        }
+    }
+    // mj_collision pair filter, (g1 < g2) order
+    struct P2 { int g1, g2; double margin; bool stat; };
+    std::vector<P2> all;
+    for (int g1 = 0; g1 < ng; ++g1) {
+        for (int g2 = g1 + 1; g2 < ng; ++g2) {
+            int b1 = m->geom_body[g1], b2 = m->geom_body[g2];
+            int w1 = weld[b1], w2 = weld[b2];
+            if (w1 == w2) continue;
+            int ct1 = m->geom_contype[g1], ca1 = m->geom_conaffinity[g1];
+            int ct2 = m->geom_contype[g2], ca2 = m->geom_conaffinity[g2];
+            if (!((ct1 & ca2) || (ct2 & ca1))) continue;
+            if (w1 != 0 && w2 != 0 &&
+                (w1 == weld[m->body_parent[w2]] || w2 == weld[m->body_parent[w1]]))
+                continue;
+            bool excl = false;
+            for (size_t e = 0; e + 1 < m->exclude.size(); e += 2) {
+                int e1 = m->exclude[e], e2 = m->exclude[e + 1];
+                if ((e1 == b1 && e2 == b2) || (e1 == b2 && e2 == b1)) { excl = true; break; }
+            }
+            if (excl) continue;
+            if (!pair_supported(m->geom_type[g1], m->geom_type[g2])) {
+                delete s;
+                return sspp::set_error(SSPP_E_UNSUPPORTED,
+                                       "unsupported collision pair: geom '" + m->geom_names[g1] +
+                                           "' (type " + std::to_string(m->geom_type[g1]) + ") vs '" +
+                                           m->geom_names[g2] + "' (type " +
+                                           std::to_string(m->geom_type[g2]) + ")");
+            }
+            double mg = std::max(m->geom_margin[g1], m->geom_margin[g2]);
+            all.push_back({g1, g2, mg, !(moving[w1] || moving[w2])});
+        }
+    }
+    // env-env pairs: constant over waypoints -> evaluated once here (same device math)
+    for (auto& pr : all) {
+        if (!pr.stat) continue;
+        s->n_static_pairs++;
+        const DGeom& A = s->geoms[table_index[pr.g1]];
+        const DGeom& B = s->geoms[table_index[pr.g2]];
+        double dc[3] = {B.pos[0] - A.pos[0], B.pos[1] - A.pos[1], B.pos[2] - A.pos[2]};
+        if (A.rbound > 0.0 && B.rbound > 0.0) {
+            double thr = A.rbound + B.rbound + pr.margin;
+            if (dot3(dc, dc) > thr * thr) continue;
+        }
+        bool afirst = A.type <= B.type;
+        const DGeom& F = afirst ? A : B;
+        const DGeom& S = afirst ? B : A;
+        int nd = 0;
+        int nc = collide<false>(F.type, F.pos, F.mat, F.size, S.type, S.pos, S.mat, S.size, pr.margin, &nd);
+        collide<true>(F.type, F.pos, F.mat, F.size, S.type, S.pos, S.mat, S.size, pr.margin, &nd);
+        s->static_contacts += nc;
+        if (nd > 0) {
+            double term = -1.0 / (sqrt(dot3(dc, dc)) + 1e-4);
+            for (int i = 0; i < nd; ++i) s->static_cost = s->static_cost + term;
+        }
+    }
+    // moving pairs: sspp mode groups by moving geom (pose computed once per group);
+    // tsp mode keeps the oracle's (g1, g2) order so per-waypoint cost sums match bit for bit.
+    std::vector<P2> mov;
+    for (auto& pr : all)
+        if (!pr.stat) mov.push_back(pr);
+    auto moving_geom = [&](const P2& pr) {
+        int w1 = weld[m->geom_body[pr.g1]];
+        return moving[w1] ? pr.g1 : pr.g2;
+    };
+    if (mode == SSPP_MODE_QPOS) {
+        std::stable_sort(mov.begin(), mov.end(), [&](const P2& x, const P2& y) {
+            return moving_geom(x) < moving_geom(y);
+        });
+    }
+    for (auto& pr : mov) {
+        int gm = moving_geom(pr);
+        int go = gm == pr.g1 ? pr.g2 : pr.g1;
+        DPair dp{};
+        dp.gm = table_index[gm];
+        dp.go = table_index[go];
+        dp.margin = pr.margin;
+        s->pairs.push_back(dp);
+    }
+    for (size_t i = 0; i < mover_bodies.size(); ++i) {
+        DMover mv{};
+        mv.qpos_adr = m->body_qpos_adr[mover_bodies[i]];
+        for (int k = 0; k < 7; ++k) mv.qpos0[k] = m->qpos0[mv.qpos_adr + k];
+        s->movers.push_back(mv);
+    }
+    int rc;
+    if ((rc = upload(&s->d_geoms, s->geoms.data(), s->geoms.size())) ||
+        (rc = upload(&s->d_pairs, s->pairs.data(), s->pairs.size())) ||
+        (rc = upload(&s->d_movers, s->movers.data(), s->movers.size()))) {
+        sspp_scene_free(s);
+        return rc;
+    }
+    *out = s;
+    return SSPP_OK;
+}
+
+int sspp_scene_get_info(const sspp_scene* s, sspp_scene_info* out) {
+    if (!s || !out) return sspp::set_error(SSPP_E_INVAL, "null argument");
+    out->n_moving_geoms = s->n_moving_geoms;
+    out->n_static_geoms = s->n_static_geoms;
+    out->n_pairs = (int)s->pairs.size();
+    out->n_static_pairs = s->n_static_pairs;
+    out->static_contacts = s->static_contacts;
+    out->n_movers = (int)s->movers.size();
+    out->static_cost = s->static_cost;
+    return SSPP_OK;
+}
+
+void sspp_scene_free(sspp_scene* s) {
+    if (!s) return;
+    if (s->d_geoms) (void)hipFree(s->d_geoms);
+    if (s->d_pairs) (void)hipFree(s->d_pairs);
+    if (s->d_movers) (void)hipFree(s->d_movers);
+    delete s;
+}
+
+}  // extern "C"
+
+static KScene kscene(const sspp_scene* s, bool tsp) {
+    KScene k{};
+    if (!s) return k;
+    k.geoms = s->d_geoms;
+    k.pairs = s->d_pairs;
+    k.movers = s->d_movers;
+    k.npairs = (int)s->pairs.size();
+    k.static_block = (!tsp && s->count_static && s->static_contacts > 0) ? 1 : 0;
+    k.static_cost = tsp ? s->static_cost : 0.0;
+    return k;
+}
+
+extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_args* a, int64_t max_batch,
+                         sspp_job** out) {
+    sspp::clear_error();
+    if (!a || !out || !a->knots || !a->init_ctrl || !a->limits)
+        return sspp::set_error(SSPP_E_INVAL, "sspp_job_create_sspp: null argument");
+    const int D = a->dof, p = a->degree, n = a->n_ctrl, W = a->check_points;
+    if (!(D == 1 || D == 2 || D == 3 || D == 4 || D == 6 || D == 7 || D == 9))
+        return sspp::set_error(SSPP_E_UNSUPPORTED, "dof must be one of 1,2,3,4,6,7,9");
+    if (p < 1 || p > kMaxP || n < p + 1) return sspp::set_error(SSPP_E_INVAL, "bad degree / control point count");
+    if (W < 2 || W > 1 << 20) return sspp::set_error(SSPP_E_INVAL, "check_points must be >= 2");
+    if (max_batch < 1) return sspp::set_error(SSPP_E_INVAL, "max_batch must be >= 1");
+    if (scene && (scene->mode != SSPP_MODE_QPOS || scene->dof != D))
+        return sspp::set_error(SSPP_E_INVAL, "scene was not bound for this dof");
+    auto* j = new sspp_job();
+    j->kind = 0; j->scene = scene; j->D = D; j->p = p; j->n = n; j->W = W;
+    j->nknots = n + p + 1; j->sigma = a->sigma; j->seed = a->seed; j->max_batch = max_batch;
+    j->nm = scene ? (int)scene->movers.size() : 1;
+    if (j->nm < 1) j->nm = 1;
+    j->lpc = lanes_for(W - 1);
+    j->cpb = kBlock / j->lpc;
+    // endpoints are candidate-independent when the knot vector is clamped (sampled mode)
+    bool clamped = true;
+    for (int i = 0; i <= p; ++i) clamped = clamped && a->knots[i] == a->knots[0] && a->knots[n + i] == a->knots[n + p];
+    j->shared_endpoints = clamped ? 1 : 0;
+    j->lds = sizeof(double) * ((size_t)j->cpb * n * D + (size_t)(2 * W + 1) * (p + 1) + kBlock / 64 + 4) +
+             sizeof(int) * ((size_t)(2 * W + 1) + j->cpb + 1);
+    if (j->lds > 160 * 1024) { delete j; return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS"); }
+    int rc;
+    const int64_t nblk = (max_batch + j->cpb - 1) / j->cpb;
+    if ((rc = upload(&j->d_knots, a->knots, (size_t)j->nknots)) ||
+        (rc = upload(&j->d_init, a->init_ctrl, (size_t)n * D)) ||
+        (rc = upload(&j->d_limits, a->limits, (size_t)D))) {
+        sspp_job_free(j);
+        return rc;
+    }
+    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess) {
+        sspp_job_free(j);
+        return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
+    }
+    *out = j;
+    return SSPP_OK;
+}
+
+template <int D, int NM>
+static hipError_t launch_sspp(const SsppK& k, int nblk, size_t lds, hipStream_t st) {
+    hipLaunchKernelGGL((k_sspp<D, NM>), dim3(nblk), dim3(kBlock), lds, st, k);
+    return hipGetLastError();
+}
+
+static hipError_t dispatch_sspp(int D, int nm, const SsppK& k, int nblk, size_t lds, hipStream_t st) {
+    if (nm == 2) {
+        if (D == 9) return launch_sspp<9, 2>(k, nblk, lds, st);
+        return hipErrorInvalidValue;
+    }
+    switch (D) {
+        case 1: return launch_sspp<1, 1>(k, nblk, lds, st);
+        case 2: return launch_sspp<2, 1>(k, nblk, lds, st);
+        case 3: return launch_sspp<3, 1>(k, nblk, lds, st);
+        case 4: return launch_sspp<4, 1>(k, nblk, lds, st);
+        case 6: return launch_sspp<6, 1>(k, nblk, lds, st);
+        case 7: return launch_sspp<7, 1>(k, nblk, lds, st);
+        case 9: return launch_sspp<9, 1>(k, nblk, lds, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B, double* d_arc,
+                    uint8_t* d_feasible, double* d_ctrl_out, sspp_best* d_best, void* stream) {
+    sspp::clear_error();
+    if (!j || j->kind != 0) return sspp::set_error(SSPP_E_INVAL, "not a SamplingPathPlanner job");
+    if (B < 1 || B > j->max_batch) return sspp::set_error(SSPP_E_INVAL, "batch size out of range");
+    if (!d_arc || !d_feasible) return sspp::set_error(SSPP_E_INVAL, "null output");
+    SsppK k{};
+    k.sc = kscene(j->scene, false);
+    k.has_scene = j->scene != nullptr;
+    k.knots = j->d_knots; k.nknots = j->nknots; k.p = j->p; k.n = j->n; k.W = j->W;
+    k.init_ctrl = j->d_init; k.ctrl_in = d_ctrl; k.ctrl_out = d_ctrl_out;
+    k.sigma = j->sigma; k.limits = j->d_limits; k.seed = j->seed;
+    k.first_id = first_id; k.B = B; k.arc = d_arc; k.feasible = d_feasible; k.part = j->d_part;
+    k.lpc = j->lpc; k.cpb = j->cpb; k.shared_endpoints = (d_ctrl == nullptr) ? j->shared_endpoints : 0;
+    const int nblk = (int)((B + j->cpb - 1) / j->cpb);
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = dispatch_sspp(j->D, j->nm, k, nblk, j->lds, st);
+    if (e != hipSuccess) return hip_fail(e, "k_sspp launch");
+    if (!d_best) return SSPP_OK;  // scoring kernel only (profiling)
+    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kBlock), 0, st, j->d_part, nblk, d_best);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_argmin launch");
+    return SSPP_OK;
+}
+
+extern "C" int sspp_job_sample_score(sspp_job* j, int64_t first_id, int64_t B, double* d_arc,
+                          uint8_t* d_feasible, double* d_ctrl_out, sspp_best* d_best, void* stream) {
+    return run_sspp(j, nullptr, first_id, B, d_arc, d_feasible, d_ctrl_out, d_best, stream);
+}
+
+extern "C" int sspp_job_score_ctrl(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B,
+                        double* d_arc, uint8_t* d_feasible, sspp_best* d_best, void* stream) {
+    if (!d_ctrl) return sspp::set_error(SSPP_E_INVAL, "null control points");
+    return run_sspp(j, d_ctrl, first_id, B, d_arc, d_feasible, nullptr, d_best, stream);
+}
+
+extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args* a, int64_t max_batch,
+                        sspp_job** out) {
+    sspp::clear_error();
+    if (!scene || !a || !out || !a->start || !a->end || !a->lo || !a->hi)
+        return sspp::set_error(SSPP_E_INVAL, "sspp_job_create_tsp: null argument");
+    if (scene->mode != SSPP_MODE_BODY) return sspp::set_error(SSPP_E_INVAL, "scene must be bound to a body");
+    const int K = a->n_vias, cp = a->check_points, n = K + 2;
+    if (K < 0 || K > 60) return sspp::set_error(SSPP_E_INVAL, "n_vias out of range");
+    if (K > 0 && (!a->mean || !a->sigma)) return sspp::set_error(SSPP_E_INVAL, "null mean/sigma");
+    if (cp < 1 || cp > 1 << 20) return sspp::set_error(SSPP_E_INVAL, "check_points must be >= 1");
+    if (max_batch < 1) return sspp::set_error(SSPP_E_INVAL, "max_batch must be >= 1");
+    if (n < 3) return sspp::set_error(SSPP_E_INVAL, "degree-2 interpolation needs >= 3 points");
+    auto* j = new sspp_job();
+    j->kind = 1; j->scene = scene; j->D = 4; j->p = 2; j->n = n; j->K = K; j->cp = cp;
+    j->nknots = n + 3; j->seed = a->seed; j->max_batch = max_batch; j->nm = 1;
+    for (int i = 0; i < 4; ++i) { j->start[i] = a->start[i]; j->end[i] = a->end[i]; j->lo[i] = a->lo[i]; j->hi[i] = a->hi[i]; }
+    j->z_min = a->z_min; j->w_col = a->w_collision;
+    j->floor_z_min = a->floor_z_min; j->floor_margin = a->floor_margin; j->floor_scale = a->floor_scale;
+    j->lpc = lanes_for(cp);
+    j->cpb = kBlock / j->lpc;
+    j->lds = sizeof(double) * ((size_t)2 * j->cpb * n * 4 + (size_t)(cp + 1) * 3 + 3 * (kBlock / 64) + 4) +
+             sizeof(int) * ((size_t)(cp + 1) + j->cpb);
+    if (j->lds > 160 * 1024) { delete j; return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS"); }
+    std::vector<double> u(n), knots(n + 3), Minv((size_t)n * n);
+    for (int i = 0; i < n; ++i) u[i] = (double)i / (n - 1);
+    if (sspp::collocation_inverse(u.data(), n, 2, knots.data(), Minv.data()) != 0) {
+        delete j;
+        return sspp::set_error(SSPP_E_INVAL, "singular collocation matrix");
+    }
+    std::vector<double> zero(4, 0.0);
+    int rc;
+    const int64_t nblk = (max_batch + j->cpb - 1) / j->cpb;
+    if ((rc = upload(&j->d_knots, knots.data(), knots.size())) ||
+        (rc = upload(&j->d_Minv, Minv.data(), Minv.size())) ||
+        (rc = upload(&j->d_mean, K ? a->mean : zero.data(), K ? (size_t)K * 4 : 4)) ||
+        (rc = upload(&j->d_sigma, K ? a->sigma : zero.data(), K ? (size_t)K * 4 : 4))) {
+        sspp_job_free(j);
+        return rc;
+    }
+    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess) {
+        sspp_job_free(j);
+        return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
+    }
+    *out = j;
+    return SSPP_OK;
+}
+
+static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t B, double* d_L,
+                   double* d_Cnf, double* d_Cwf, uint8_t* d_status, double* d_cost,
+                   double* d_vias_out, sspp_best* d_best, void* stream) {
+    sspp::clear_error();
+    if (!j || j->kind != 1) return sspp::set_error(SSPP_E_INVAL, "not a TaskSpacePlanner job");
+    if (B < 1 || B > j->max_batch) return sspp::set_error(SSPP_E_INVAL, "batch size out of range");
+    if (!d_L || !d_Cnf || !d_Cwf || !d_status || !d_cost)
+        return sspp::set_error(SSPP_E_INVAL, "null output");
+    TspK k{};
+    k.sc = kscene(j->scene, true);
+    k.knots = j->d_knots; k.nknots = j->nknots; k.n = j->n; k.K = j->K; k.cp = j->cp;
+    k.Minv = j->d_Minv;
+    for (int i = 0; i < 4; ++i) { k.start[i] = j->start[i]; k.end[i] = j->end[i]; k.lo[i] = j->lo[i]; k.hi[i] = j->hi[i]; }
+    k.mean = j->d_mean; k.sigma = j->d_sigma; k.z_min = j->z_min;
+    k.vias_in = d_vias; k.vias_out = d_vias_out; k.seed = j->seed; k.first_id = first_id; k.B = B;
+    k.w_col = j->w_col; k.floor_z_min = j->floor_z_min; k.floor_margin = j->floor_margin;
+    k.floor_scale = j->floor_scale;
+    k.L = d_L; k.Cnf = d_Cnf; k.Cwf = d_Cwf; k.cost = d_cost; k.status = d_status; k.part = j->d_part;
+    k.lpc = j->lpc; k.cpb = j->cpb;
+    const int nblk = (int)((B + j->cpb - 1) / j->cpb);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL((k_tsp<1>), dim3(nblk), dim3(kBlock), j->lds, st, k);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_tsp launch");
+    if (!d_best) return SSPP_OK;  // scoring kernel only (profiling)
+    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kBlock), 0, st, j->d_part, nblk, d_best);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_argmin launch");
+    return SSPP_OK;
+}
+
+extern "C" int sspp_job_tsp_sample_score(sspp_job* j, int64_t first_id, int64_t B, double* d_L, double* d_Cnf,
+                              double* d_Cwf, uint8_t* d_status, double* d_cost, double* d_vias_out,
+                              sspp_best* d_best, void* stream) {
+    return run_tsp(j, nullptr, first_id, B, d_L, d_Cnf, d_Cwf, d_status, d_cost, d_vias_out, d_best, stream);
+}
+
+extern "C" int sspp_job_tsp_score_vias(sspp_job* j, const double* d_vias, int64_t first_id, int64_t B,
+                            double* d_L, double* d_Cnf, double* d_Cwf, uint8_t* d_status,
+                            double* d_cost, sspp_best* d_best, void* stream) {
+    if (!d_vias && j && j->K > 0) return sspp::set_error(SSPP_E_INVAL, "null via points");
+    return run_tsp(j, d_vias ? d_vias : nullptr, first_id, B, d_L, d_Cnf, d_Cwf, d_status, d_cost,
+                   nullptr, d_best, stream);
+}
+
+extern "C" int sspp_job_info(const sspp_job* j, int* lpc, int* cpb, int* threads, size_t* lds) {
+    if (!j) return sspp::set_error(SSPP_E_INVAL, "null job");
+    if (lpc) *lpc = j->lpc;
+    if (cpb) *cpb = j->cpb;
+    if (threads) *threads = kBlock;
+    if (lds) *lds = j->lds;
+    return SSPP_OK;
+}
+
+extern "C" void sspp_job_free(sspp_job* j) {
+    if (!j) return;
+    for (double* p : {j->d_knots, j->d_init, j->d_limits, j->d_Minv, j->d_mean, j->d_sigma})
+        if (p) (void)hipFree(p);
+    if (j->d_part) (void)hipFree(j->d_part);
+    delete j;
+}
+
+extern "C" int sspp_best_reduce_device(const sspp_best* d_parts, int n, sspp_best* d_out,
+                                       void* stream) {
+    sspp::clear_error();
+    if (!d_parts || !d_out || n < 1) return sspp::set_error(SSPP_E_INVAL, "sspp_best_reduce_device: bad argument");
+    static_assert(sizeof(BlockBest) == sizeof(sspp_best), "layout");
+    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<const BlockBest*>(d_parts), n, d_out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_argmin launch");
+    return SSPP_OK;
+}
+
+extern "C" int sspp_device_count(int* n) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (n) *n = (e == hipSuccess) ? c : 0;
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    return SSPP_OK;
+}
+
+

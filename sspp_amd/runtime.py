@@ -1,0 +1,294 @@
+"""Python host objects over the C ABI: Model, Scene, SsppJob, TspJob.
+
+Device buffers are torch CUDA tensors (torch is plumbing here: HBM allocation, streams and
+torch.distributed); every computation runs in the HIP kernels of libsspp_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import Best, ModelView, SceneInfo, SsppArgs, TspArgs, check, lib
+
+DEFAULT_SEED = 0x5EED
+
+
+def _dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _f64(x, n=None):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1))
+    if n is not None and a.size != n:
+        raise ValueError("expected %d values, got %d" % (n, a.size))
+    return a
+
+
+def _torch():
+    import torch  # noqa: WPS433 (plumbing only)
+    return torch
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    if stream is None:
+        torch = _torch()
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return C.c_void_p(stream)
+    return C.c_void_p(stream.cuda_stream)
+
+
+def best_tensor(device="cuda"):
+    """A device buffer for one sspp_best record (4 x int64; cost is the bits of field 0)."""
+    return _torch().zeros(4, dtype=_torch().int64, device=device)
+
+
+def decode_best(t):
+    """(cost, index, count) from a best buffer (torch tensor or numpy int64[4])."""
+    a = t.detach().cpu().numpy() if hasattr(t, "detach") else np.asarray(t)
+    a = np.ascontiguousarray(a.astype(np.int64))
+    cost = a[:1].view(np.float64)[0]
+    return float(cost), int(a[1]), int(a[2])
+
+
+def reduce_best(parts):
+    """Global argmin over gathered per-rank records: lowest cost, lowest global id on ties."""
+    arr = (Best * len(parts))()
+    for i, (c, idx, cnt) in enumerate(parts):
+        arr[i].cost, arr[i].index, arr[i].count = c, idx, cnt
+    out = Best()
+    check(lib().sspp_best_reduce(arr, len(parts), C.byref(out)), "sspp_best_reduce")
+    return out.cost, out.index, out.count
+
+
+def reduce_best_device(parts, out, stream=None):
+    """Device argmin over gathered records: parts int64 [n, 4] tensor -> out int64 [4]."""
+    n = parts.shape[0]
+    check(lib().sspp_best_reduce_device(_ptr(parts), int(n), _ptr(out), _stream(stream)),
+          "sspp_best_reduce_device")
+
+
+class Model:
+    """Parsed MJCF scene (SamplingPathPlanner(xml_path) semantics: the string is a path)."""
+
+    def __init__(self, xml_path):
+        h = C.c_void_p()
+        check(lib().sspp_model_load_mjcf(str(xml_path).encode(), C.byref(h)), "load MJCF")
+        self._h = h
+        self.path = str(xml_path)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib._lib is not None:
+            _lib._lib.sspp_model_free(self._h)
+            self._h = None
+
+    def arrays(self):
+        v = ModelView()
+        check(lib().sspp_model_view_get(self._h, C.byref(v)), "model view")
+
+        def arr(p, n, dt, shape):
+            if n == 0:
+                return np.zeros(shape, dt)
+            return np.ctypeslib.as_array(p, shape=(n,)).astype(dt).reshape(shape)
+
+        nb, ng, ne, nq = v.nbody, v.ngeom, v.nexclude, v.nq
+        return dict(
+            body_parent=arr(v.body_parent, nb, np.int32, (nb,)),
+            body_jnt_type=arr(v.body_jnt_type, nb, np.int32, (nb,)),
+            body_qpos_adr=arr(v.body_qpos_adr, nb, np.int32, (nb,)),
+            body_pos=arr(v.body_pos, 3 * nb, np.float64, (nb, 3)),
+            body_quat=arr(v.body_quat, 4 * nb, np.float64, (nb, 4)),
+            geom_type=arr(v.geom_type, ng, np.int32, (ng,)),
+            geom_body=arr(v.geom_body, ng, np.int32, (ng,)),
+            geom_contype=arr(v.geom_contype, ng, np.int32, (ng,)),
+            geom_conaffinity=arr(v.geom_conaffinity, ng, np.int32, (ng,)),
+            geom_size=arr(v.geom_size, 3 * ng, np.float64, (ng, 3)),
+            geom_pos=arr(v.geom_pos, 3 * ng, np.float64, (ng, 3)),
+            geom_quat=arr(v.geom_quat, 4 * ng, np.float64, (ng, 4)),
+            geom_margin=arr(v.geom_margin, ng, np.float64, (ng,)),
+            exclude=arr(v.exclude, 2 * ne, np.int32, (ne, 2)),
+            qpos0=arr(v.qpos0, nq, np.float64, (nq,)),
+        )
+
+    def body_id(self, name):
+        return check(lib().sspp_model_body_id(self._h, name.encode()), "body lookup")
+
+    def geom_id(self, name):
+        return check(lib().sspp_model_geom_id(self._h, name.encode()), "geom lookup")
+
+    def body_point(self, name):
+        out = np.zeros(4)
+        check(lib().sspp_model_body_point(self._h, name.encode(), _dptr(out)), "body point")
+        return out
+
+
+class Scene:
+    """Model bound to its moving set, with device-resident geom/pair tables."""
+
+    def __init__(self, model, mode, arg, count_static=False):
+        if isinstance(arg, str):
+            arg = model.body_id(arg)
+        h = C.c_void_p()
+        check(lib().sspp_scene_create(model.handle, int(mode), int(arg), int(bool(count_static)),
+                                      C.byref(h)), "scene create")
+        self._h = h
+        self.model = model  # keep alive
+        self.mode, self.arg = mode, arg
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self):
+        i = SceneInfo()
+        check(lib().sspp_scene_get_info(self._h, C.byref(i)), "scene info")
+        return {k: getattr(i, k) for k, _ in SceneInfo._fields_}
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib._lib is not None:
+            _lib._lib.sspp_scene_free(self._h)
+            self._h = None
+
+
+def interpolate(pts, degree, u):
+    """Eigen SplineFitting::Interpolate (include/sspp.h:95): returns (knots, ctrl [n][D])."""
+    pts = np.ascontiguousarray(np.asarray(pts, dtype=np.float64))
+    n, D = pts.shape
+    u = _f64(u, n)
+    knots = np.zeros(n + degree + 1)
+    ctrl = np.zeros((n, D))
+    check(lib().sspp_interpolate(_dptr(pts), n, D, int(degree), _dptr(u), _dptr(knots),
+                                 _dptr(ctrl)), "interpolate")
+    return knots, ctrl
+
+
+def spline_eval(knots, degree, ctrl, u):
+    knots = _f64(knots)
+    ctrl = np.ascontiguousarray(np.asarray(ctrl, dtype=np.float64))
+    D = ctrl.shape[1]
+    out = np.zeros(D)
+    check(lib().sspp_spline_eval(_dptr(knots), knots.size, int(degree), _dptr(ctrl), D,
+                                 float(u), _dptr(out)), "spline eval")
+    return out
+
+
+class _Job:
+    _h = None
+
+    def info(self):
+        a, b, c, d = C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
+        check(lib().sspp_job_info(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)), "job info")
+        return dict(lanes_per_candidate=a.value, candidates_per_block=b.value,
+                    block_threads=c.value, lds_bytes=d.value)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib._lib is not None:
+            _lib._lib.sspp_job_free(self._h)
+            self._h = None
+
+
+class SsppJob(_Job):
+    """SamplingPathPlanner::plan's candidate loop on the GPU (include/sspp.h:194-225)."""
+
+    def __init__(self, scene, knots, degree, init_ctrl, sigma, limits, check_points,
+                 seed=DEFAULT_SEED, max_batch=4096):
+        init_ctrl = np.ascontiguousarray(np.asarray(init_ctrl, dtype=np.float64))
+        n, D = init_ctrl.shape
+        self.knots = _f64(knots, n + degree + 1)
+        self.init_ctrl = init_ctrl
+        self.limits = _f64(limits, D)
+        self.n, self.D, self.degree, self.W = n, D, int(degree), int(check_points)
+        self.max_batch = int(max_batch)
+        a = SsppArgs(knots=_dptr(self.knots), degree=self.degree, init_ctrl=_dptr(init_ctrl),
+                     n_ctrl=n, dof=D, sigma=float(sigma), limits=_dptr(self.limits),
+                     check_points=self.W, seed=int(seed) & (2 ** 64 - 1))
+        h = C.c_void_p()
+        check(lib().sspp_job_create_sspp(scene.handle if scene is not None else None, C.byref(a),
+                                         self.max_batch, C.byref(h)), "job create (sspp)")
+        self._h = h
+        self.scene = scene
+
+    def alloc(self, B, device="cuda", with_ctrl=False):
+        torch = _torch()
+        out = dict(arc=torch.empty(B, dtype=torch.float64, device=device),
+                   feasible=torch.empty(B, dtype=torch.uint8, device=device),
+                   best=best_tensor(device))
+        if with_ctrl:
+            out["ctrl"] = torch.empty((B, self.n, self.D), dtype=torch.float64, device=device)
+        return out
+
+    def sample_score(self, first_id, B, arc, feasible, best, ctrl_out=None, stream=None):
+        check(lib().sspp_job_sample_score(self._h, int(first_id), int(B), _ptr(arc), _ptr(feasible),
+                                          _ptr(ctrl_out), _ptr(best), _stream(stream)),
+              "sample_score")
+
+    def score_ctrl(self, ctrl, first_id, arc, feasible, best, stream=None):
+        B = ctrl.shape[0]
+        check(lib().sspp_job_score_ctrl(self._h, _ptr(ctrl), int(first_id), int(B), _ptr(arc),
+                                        _ptr(feasible), _ptr(best), _stream(stream)), "score_ctrl")
+
+
+class TspJob(_Job):
+    """tsp::Planner::plan's evaluation loop on the GPU (include/sspp/tsp_planner.h:89-138)."""
+
+    def __init__(self, scene, start, end, n_vias, check_points, mean=None, sigma=None,
+                 lo=(-2, -2, -2, -2), hi=(2, 2, 2, 2), z_min=0.0, w_collision=1.0,
+                 seed=DEFAULT_SEED, max_batch=4096, floor=(0.0, 0.01, 10.0)):
+        K = int(n_vias)
+        self.start, self.end = _f64(start, 4), _f64(end, 4)
+        self.mean = _f64(mean if mean is not None else np.zeros((max(K, 1), 4)))
+        self.sigma = _f64(sigma if sigma is not None else np.zeros((max(K, 1), 4)))
+        self.lo, self.hi = _f64(lo, 4), _f64(hi, 4)
+        self.K, self.cp, self.max_batch = K, int(check_points), int(max_batch)
+        a = TspArgs(start=_dptr(self.start), end=_dptr(self.end), n_vias=K, check_points=self.cp,
+                    w_collision=float(w_collision), mean=_dptr(self.mean), sigma=_dptr(self.sigma),
+                    lo=_dptr(self.lo), hi=_dptr(self.hi), z_min=float(z_min),
+                    seed=int(seed) & (2 ** 64 - 1), floor_z_min=float(floor[0]),
+                    floor_margin=float(floor[1]), floor_scale=float(floor[2]))
+        h = C.c_void_p()
+        check(lib().sspp_job_create_tsp(scene.handle, C.byref(a), self.max_batch, C.byref(h)),
+              "job create (tsp)")
+        self._h = h
+        self.scene = scene
+
+    def alloc(self, B, device="cuda", with_vias=False):
+        torch = _torch()
+        f = lambda: torch.empty(B, dtype=torch.float64, device=device)  # noqa: E731
+        out = dict(L=f(), Cnf=f(), Cwf=f(), cost=f(),
+                   status=torch.empty(B, dtype=torch.uint8, device=device),
+                   best=best_tensor(device))
+        if with_vias:
+            out["vias"] = torch.empty((B, max(self.K, 1), 4), dtype=torch.float64, device=device)
+        return out
+
+    def sample_score(self, first_id, B, L, Cnf, Cwf, status, cost, best, vias_out=None, stream=None):
+        check(lib().sspp_job_tsp_sample_score(self._h, int(first_id), int(B), _ptr(L), _ptr(Cnf),
+                                              _ptr(Cwf), _ptr(status), _ptr(cost), _ptr(vias_out),
+                                              _ptr(best), _stream(stream)), "tsp sample_score")
+
+    def score_vias(self, vias, first_id, L, Cnf, Cwf, status, cost, best, stream=None):
+        B = vias.shape[0]
+        check(lib().sspp_job_tsp_score_vias(self._h, _ptr(vias), int(first_id), int(B), _ptr(L),
+                                            _ptr(Cnf), _ptr(Cwf), _ptr(status), _ptr(cost),
+                                            _ptr(best), _stream(stream)), "tsp score_vias")
+
+
+def device_count():
+    n = C.c_int()
+    rc = lib().sspp_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+__all__ = ["Model", "Scene", "SsppJob", "TspJob", "interpolate", "spline_eval", "best_tensor",
+           "decode_best", "reduce_best", "reduce_best_device", "device_count", "DEFAULT_SEED", "math"]

@@ -1,0 +1,102 @@
+"""The drop-in `from sspp import _sspp` surface (src/sspp_bindings.cpp:14-69) on the GPU."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import mjcf_ref
+from oracle import oracle as O
+from tests.conftest import SCENES
+
+pytestmark = pytest.mark.gpu
+ROBOCRANE = os.path.join(SCENES, "robocrane.xml")
+
+
+@pytest.fixture(scope="module")
+def sp(cuda):
+    from sspp import _sspp
+    assert _sspp.__backend__ == "hip-gfx950"
+    return _sspp
+
+
+def test_plan_matches_oracle(sp, capfd):
+    planner = sp.SamplingPathPlanner7(ROBOCRANE)
+    start = np.array([0.5, 0.15, 0.136, 0.707, 0, 0, 0.707])
+    end = np.array([0.5, -0.05, 0.136, 0.707, 0, 0, 0.707]).reshape(7, 1)  # (N,1) accepted
+    sigma, limits = 0.1, np.ones((7, 1))
+    ok, paths = planner.plan(start, end, sigma, limits, sample_count=512, check_points=64,
+                             init_points=10)
+    out = capfd.readouterr().out
+    assert "Sampled 512 splines. Successful paths found: %d" % len(paths) in out
+    # oracle on the same candidates
+    init = sp.Spline7()
+    assert planner.initializePath(start, end, init, 10)
+    knots = init.knots()
+    ctrl0 = init.ctrls().T.copy()
+    ctrl = O.sample_sspp(ctrl0, 3, sigma, np.ones(7), planner.seed, 0, 512)
+    osc = O.Scene(mjcf_ref.load(ROBOCRANE), 0, 7)
+    arc, feas = O.sspp_score(osc, knots, 3, ctrl, 64)
+    assert len(paths) == int(feas.sum())
+    assert ok == (feas.sum() > 0)
+    feas_idx = np.nonzero(feas)[0]
+    for s, i in zip(paths, feas_idx):
+        np.testing.assert_allclose(s.ctrls().T, ctrl[i], rtol=0, atol=1e-12)
+    if ok:
+        idx, best = O.argmin(arc, feas)
+        assert planner.last_best_index == idx
+        np.testing.assert_allclose(planner.get_ctrl_pts().T, ctrl[idx], atol=1e-12)
+        np.testing.assert_allclose(planner.evaluate(0.0), start, atol=1e-12)
+        np.testing.assert_allclose(planner.evaluate(1.0), end.ravel(), atol=1e-12)
+        # computeArcLength / findBestPath agree with plan's internal argmin
+        assert abs(planner.computeArcLength(paths[0], 64) - arc[feas_idx[0]]) <= 1e-12
+        bs = sp.Spline7()
+        assert planner.findBestPath(paths, bs, 64)
+        np.testing.assert_allclose(bs.ctrls(), planner.get_ctrl_pts(), atol=0)
+
+
+def test_spline_views_and_helpers(sp):
+    planner = sp.SamplingPathPlanner7(ROBOCRANE)
+    s = sp.Spline7()
+    assert s.ctrls().shape == (7, 0)
+    start = np.zeros(7) + [0.3, 0.2, 0.5, 1, 0, 0, 0]
+    end = start + [0.2, 0, 0, 0, 0, 0, 0]
+    planner.initializePath(start, end, s, 7)
+    c = s.ctrls()
+    assert c.shape == (7, 7)
+    c[0, 3] += 0.5  # view semantics (reference_internal)
+    assert s.ctrls()[0, 3] == c[0, 3]
+    noisy = planner.sampleWithNoise(s, 0.1, np.ones(7), 3)
+    assert noisy.ctrls().shape == (7, 7)
+    np.testing.assert_array_equal(noisy.ctrls()[:, :3], s.ctrls()[:, :3])  # j < p fixed
+    assert not planner.checkCollision(s, 20)  # hovering at z=0.5, far from everything
+    low = sp.Spline7()
+    planner.initializePath(start - [0, 0, 0.49, 0, 0, 0, 0], end - [0, 0, 0.49, 0, 0, 0, 0], low, 7)
+    assert planner.checkCollision(low, 20)  # through the floor
+    with pytest.raises(TypeError):
+        planner.sampleWithNoise(s, 0.1, np.ones(7), object())
+    with pytest.raises(ValueError):
+        planner.plan(np.zeros(6), np.zeros(7), 0.1, np.ones(7))
+
+
+def test_bad_path_raises(sp):
+    with pytest.raises(RuntimeError):
+        sp.SamplingPathPlanner7("/nonexistent/scene.xml")
+
+
+def test_other_dofs(sp):
+    """SamplingPathPlanner3/6/9 on the same scene (qpos window semantics, include/sspp.h:139-142)."""
+    for cls, N in ((sp.SamplingPathPlanner3, 3), (sp.SamplingPathPlanner6, 6),
+                   (sp.SamplingPathPlanner9, 9)):
+        planner = cls(ROBOCRANE)
+        q0 = np.array([0.5, 0.15, 0.3, 0.707, 0, 0, 0.707, 0.5, -0.05])[:N]
+        q1 = q0.copy()
+        q1[1] = -0.05
+        ok, paths = planner.plan(q0, q1, 0.02, np.ones(N), sample_count=64, check_points=32,
+                                 init_points=6)
+        osc = O.Scene(mjcf_ref.load(ROBOCRANE), 0, N)
+        init = getattr(sp, "Spline%d" % N)()
+        planner.initializePath(q0, q1, init, 6)
+        ctrl = O.sample_sspp(init.ctrls().T.copy(), 3, 0.02, np.ones(N), planner.seed, 0, 64)
+        arc, feas = O.sspp_score(osc, init.knots(), 3, ctrl, 32)
+        assert len(paths) == int(feas.sum())
+        assert ok == bool(feas.any())

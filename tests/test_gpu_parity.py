@@ -1,0 +1,182 @@
+"""GPU parity: HIP kernels (through the C ABI) vs the CPU oracle on the same inputs.
+
+Bars (BASELINE.json north_star): per-candidate costs within 1e-5 of the oracle — the kernels
+follow the oracle's operation order, so the tests hold them to 1e-12 (SamplingPathPlanner)
+and 1e-9 (TaskSpacePlanner, whose control points come from a precomputed collocation inverse
+instead of a per-candidate QR solve); feasibility flags and the selected index bit-identical.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import mjcf_ref
+from oracle import oracle as O
+from tests.conftest import SCENES
+
+pytestmark = pytest.mark.gpu
+
+ROBOCRANE = os.path.join(SCENES, "robocrane.xml")
+STACKING = os.path.join(SCENES, "stacking.xml")
+PLANNER = os.path.join(SCENES, "planner.xml")
+START7 = np.array([0.5, 0.15, 0.136, 0.707, 0.0, 0.0, 0.707])
+END7 = np.array([0.5, -0.05, 0.136, 0.707, 0.0, 0.0, 0.707])
+COST_TOL = 1e-12
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def linear_init(start, end, n, p=3):
+    import sspp_amd as S
+    u = np.array([i / (n - 1) for i in range(n)])
+    pts = np.array([(1 - t) * start + t * end for t in u])
+    return S.interpolate(pts, p, u)
+
+
+@pytest.fixture(scope="module")
+def robocrane(cuda):
+    import sspp_amd as S
+    model = S.Model(ROBOCRANE)
+    scene = S.Scene(model, 0, 7)
+    oscene = O.Scene(mjcf_ref.load(ROBOCRANE), 0, 7)
+    return model, scene, oscene
+
+
+def run_sspp(job, B, first=0, with_ctrl=True):
+    import sspp_amd as S
+    out = job.alloc(B, with_ctrl=with_ctrl)
+    job.sample_score(first, B, out["arc"], out["feasible"], out["best"], ctrl_out=out.get("ctrl"))
+    import torch
+    torch.cuda.synchronize()
+    res = {k: _np(v) for k, v in out.items() if k != "best"}
+    res["best"] = S.decode_best(out["best"])
+    return res
+
+
+@pytest.mark.parametrize("B,W", [(4096, 128), (257, 128), (1, 128), (300, 50), (100, 256), (64, 2)])
+def test_robocrane_sample_score_matches_oracle(robocrane, B, W):
+    import sspp_amd as S
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=0x5EED, max_batch=B)
+    r = run_sspp(job, B, first=1000)
+    # sampling parity (Philox + Box-Muller restated on the host)
+    ctrl_o = O.sample_sspp(ctrl0, 3, 0.08, np.ones(7), 0x5EED, 1000, B)
+    assert np.abs(r["ctrl"] - ctrl_o).max() <= 1e-12
+    # scoring parity on the exact control points the GPU scored
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], W)
+    np.testing.assert_array_equal(r["feasible"], feas_o)
+    assert np.abs(r["arc"] - arc_o).max() <= COST_TOL
+    idx_o, best_o = O.argmin(arc_o, feas_o)
+    cost, idx, cnt = r["best"]
+    assert cnt == int(feas_o.sum())
+    assert idx == (idx_o + 1000 if idx_o >= 0 else -1)
+    if idx_o >= 0:
+        assert abs(cost - best_o) <= COST_TOL
+
+
+def test_robocrane_config2_is_nontrivial(robocrane):
+    """Config 2 must have both feasible and colliding candidates (else parity is vacuous)."""
+    import sspp_amd as S
+    _, scene, _ = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=4096)
+    r = run_sspp(job, 4096, with_ctrl=False)
+    nfeas = int(r["feasible"].sum())
+    assert 0 < nfeas < 4096, nfeas  # SURVEY config 2 (sigma 0.08): ~0.3% clear the brick stack
+
+
+def test_score_ctrl_mode_matches_oracle(robocrane):
+    """Caller-supplied splines (checkCollision + computeArcLength on arbitrary ctrl)."""
+    import sspp_amd as S
+    import torch
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    rng = np.random.default_rng(7)
+    B = 777
+    ctrl = ctrl0[None] + rng.normal(0, 0.05, size=(B, 10, 7))  # endpoints perturbed too
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=B)
+    out = job.alloc(B)
+    job.score_ctrl(torch.from_numpy(ctrl).cuda(), 0, out["arc"], out["feasible"], out["best"])
+    torch.cuda.synchronize()
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, ctrl, 128)
+    np.testing.assert_array_equal(_np(out["feasible"]), feas_o)
+    assert np.abs(_np(out["arc"]) - arc_o).max() <= COST_TOL
+    assert S.decode_best(out["best"])[1] == O.argmin(arc_o, feas_o)[0]
+
+
+def test_config1_bsplines_golden(cuda, golden):
+    """Config 1: 2-DoF, 64 x 50, no collision, knots/ctrl from the reference's BSplines.py."""
+    import sspp_amd as S
+    import torch
+    knots, ctrl = golden["cfg1_knots"], golden["cfg1_ctrl"]
+    job = S.SsppJob(None, knots, 3, golden["cfg1_ctrl0"], 0.08, np.ones(2), 50, max_batch=64)
+    out = job.alloc(64)
+    job.score_ctrl(torch.from_numpy(np.ascontiguousarray(ctrl)).cuda(), 0, out["arc"],
+                   out["feasible"], out["best"])
+    torch.cuda.synchronize()
+    arc = _np(out["arc"])
+    assert np.abs(arc - golden["cfg1_arc"]).max() <= 1e-12
+    arc_o, _ = O.sspp_score(None, knots, 3, ctrl, 50)
+    assert np.abs(arc - arc_o).max() == 0.0
+    assert S.decode_best(out["best"])[1] == int(golden["cfg1_best"][0])
+    assert _np(out["feasible"]).all()
+
+
+def stacking_problem(B, cp=128, seed=0x5EED, K=1):
+    import sspp_amd as S
+    model = S.Model(STACKING)
+    scene = S.Scene(model, 1, "block1")
+    start = model.body_point("block1") + np.array([0, 0, 0.02, 0])
+    end = model.body_point("block2") + np.array([0, 0, 0.22, 0])
+    mean = np.array([start + (end - start) * (i + 1) / (K + 1) for i in range(K)])
+    sigma = np.full((K, 4), 0.2)
+    lo, hi = np.array([-0.5, -0.5, 0.0, -1.6]), np.array([0.5, 0.5, 0.6, 1.6])
+    job = S.TspJob(scene, start, end, K, cp, mean=mean, sigma=sigma, lo=lo, hi=hi, z_min=0.0,
+                   seed=seed, max_batch=B)
+    oscene = O.Scene(mjcf_ref.load(STACKING), 1, model.body_id("block1"))
+    return model, scene, job, oscene, start, end, mean, sigma, lo, hi
+
+
+@pytest.mark.parametrize("B,cp,K", [(16384, 128, 1), (333, 40, 1), (200, 64, 3), (50, 300, 2)])
+def test_stacking_tsp_matches_oracle(cuda, B, cp, K):
+    import sspp_amd as S
+    import torch
+    model, scene, job, oscene, start, end, mean, sigma, lo, hi = stacking_problem(B, cp, K=K)
+    out = job.alloc(B, with_vias=True)
+    job.sample_score(5, B, out["L"], out["Cnf"], out["Cwf"], out["status"], out["cost"],
+                     out["best"], vias_out=out["vias"])
+    torch.cuda.synchronize()
+    vias = _np(out["vias"])
+    vias_o = O.sample_tsp(mean, sigma, lo, hi, 0.0, 0x5EED, 5, B)
+    assert np.abs(vias - vias_o).max() <= 1e-12
+    L, Cnf, Cwf, st, cost = O.tsp_score(oscene, start, end, vias, cp)
+    np.testing.assert_array_equal(_np(out["status"]), st)
+    for a, b in ((out["L"], L), (out["Cnf"], Cnf), (out["Cwf"], Cwf), (out["cost"], cost)):
+        assert np.abs(_np(a) - b).max() <= 1e-9
+    idx_o, best_o = O.tsp_best(cost, st)
+    c, idx, cnt = S.decode_best(out["best"])
+    assert cnt == int(st.sum())
+    assert idx == (idx_o + 5 if idx_o >= 0 else -1)
+    if B >= 1000:
+        assert 0 < st.sum() < B  # both outcomes present
+
+
+def test_planner_scene_sspp(cuda):
+    """planner.xml: block1 (free) vs static wall/block2, 7-DoF window, path through the wall."""
+    import sspp_amd as S
+    model = S.Model(PLANNER)
+    scene = S.Scene(model, 0, 7)
+    oscene = O.Scene(mjcf_ref.load(PLANNER), 0, 7)
+    start = np.array([0.5, 0.0, 0.15, 1, 0, 0, 0])
+    end = np.array([-0.25, 0.0, 0.15, 1, 0, 0, 0])
+    knots, ctrl0 = linear_init(start, end, 10)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.3, np.array([1, 1, 1, .2, .2, .2, .2]), 100,
+                    seed=3, max_batch=2048)
+    r = run_sspp(job, 2048)
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 100)
+    np.testing.assert_array_equal(r["feasible"], feas_o)
+    assert np.abs(r["arc"] - arc_o).max() <= COST_TOL
+    assert r["best"][1] == O.argmin(arc_o, feas_o)[0]
