@@ -132,8 +132,11 @@ def cpu_baseline(args, ctx, B, device):
         ctrl = out["ctrl"].cpu().numpy()
         arc_g, feas_g = out["arc"].cpu().numpy(), out["feasible"].cpu().numpy()
 
-        def run(lo, hi):
-            return O.sspp_score(osc, ctx["knots"], ctx["p"], ctrl[lo:hi], ctx["W"], nthreads=threads)
+        def run_on(c):
+            return O.sspp_score(osc, ctx["knots"], ctx["p"], c, ctx["W"], nthreads=threads)
+
+        def sample(first, n):
+            return O.sample_sspp(ctx["ctrl0"], ctx["p"], 0.08, np.ones(7), S.DEFAULT_SEED, first, n)
     else:
         job = ctx["job"]
         osc = O.Scene(model, 1, ctx["body"])
@@ -144,28 +147,31 @@ def cpu_baseline(args, ctx, B, device):
         ctrl = out["vias"].cpu().numpy()
         arc_g, feas_g = out["cost"].cpu().numpy(), out["status"].cpu().numpy()
 
-        def run(lo, hi):
-            L, Cnf, Cwf, st, cost = O.tsp_score(osc, ctx["start"], ctx["end"], ctrl[lo:hi], ctx["cp"],
+        def run_on(v):
+            L, Cnf, Cwf, st, cost = O.tsp_score(osc, ctx["start"], ctx["end"], v, ctx["cp"],
                                                 nthreads=threads)
             return cost, st
-    chunk = 256
-    done, t0 = 0, time.perf_counter()
-    arcs, feas = [], []
-    while done < B and time.perf_counter() - t0 < args.cpu_seconds:
-        a, f = run(done, min(B, done + chunk))
-        arcs.append(a)
-        feas.append(f)
-        done = min(B, done + chunk)
+
+        def sample(first, n):
+            return O.sample_tsp(ctx["mean"], ctx["sigma"], ctx["lo"], ctx["hi"], 0.0,
+                                S.DEFAULT_SEED, first, n)
+    # parity on the GPU's own step-0 batch (identical control points / via sets)
+    arc_c, feas_c = run_on(ctrl)
+    fin = np.isfinite(arc_c) & np.isfinite(arc_g)
+    parity = dict(candidates=int(B),
+                  max_abs_cost_diff=float(np.abs(arc_c[fin] - arc_g[fin]).max()) if fin.any() else 0.0,
+                  feasible_identical=bool(np.array_equal(feas_c, feas_g)),
+                  argmin_identical=bool(O.argmin(arc_c, feas_c)[0] == O.argmin(arc_g, feas_g)[0]))
+    # timed: successive batches (sampling included, as in the GPU step) for ~cpu_seconds
+    done, batch, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        run_on(sample((batch + 1) * B, B))
+        done += B
+        batch += 1
     dt = time.perf_counter() - t0
-    arc_c, feas_c = np.concatenate(arcs), np.concatenate(feas)
-    fin = np.isfinite(arc_c) & np.isfinite(arc_g[:done])
-    parity = dict(candidates=int(done),
-                  max_abs_cost_diff=float(np.abs(arc_c[fin] - arc_g[:done][fin]).max()) if fin.any() else 0.0,
-                  feasible_identical=bool(np.array_equal(feas_c, feas_g[:done])),
-                  argmin_identical=bool(O.argmin(arc_c, feas_c)[0] == O.argmin(arc_g[:done], feas_g[:done])[0]))
     return dict(value=done / dt, unit="candidate paths scored/s", cores=threads, kind="port",
-                sample="first %d candidates of the GPU's step-0 batch (same ctrl points), %.1f s, "
-                       "OpenMP schedule(dynamic,1) over candidates" % (done, dt),
+                sample="%d candidates (%d batches of %d, sampling included) in %.1f s; "
+                       "OpenMP schedule(dynamic,1) over candidates" % (done, batch, B, dt),
                 parity=parity)
 
 

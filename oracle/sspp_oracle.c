@@ -57,12 +57,9 @@ static void mulquat(const double* a, const double* b, double* r) {
     double t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
     r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
 }
-/* mju_quat2Mat, row-major */
+/* mju_quat2Mat, row-major (without MuJoCo's identity shortcut: the general formula gives
+   the same matrix for q = (1,0,0,0), and a single code path keeps the GPU off scratch) */
 static void quat2mat(const double* q, double* m) {
-    if (q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0) {
-        m[0] = 1; m[1] = 0; m[2] = 0; m[3] = 0; m[4] = 1; m[5] = 0; m[6] = 0; m[7] = 0; m[8] = 1;
-        return;
-    }
     double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
     double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
     double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
@@ -660,8 +657,9 @@ static int sat_box_box(const double* pa, const double* ma, const double* ea, con
                 double bk[3] = {R[0][k], R[1][k], R[2][k]};
                 rb = fma(eb[k], fabs(dot3(bk, L)), rb);
             }
-            double sep = (pr - (ra + rb)) / sqrt(len2);
-            if (sep >= thr) return 0;
+            /* separation along the unit axis L/|L| >= thr, without the division */
+            double num = pr - (ra + rb);
+            if (num >= thr * sqrt(len2)) return 0;
         }
     }
     return 1;
@@ -692,8 +690,8 @@ static int sat_cyl_box(const double* pa, const double* ma, const double* sz, con
         double rc = fma(sz[1], fabs(aL), sz[0] * sqrt(rr > 0.0 ? rr : 0.0));
         double rb = 0.0;
         for (int k = 0; k < 3; ++k) rb = fma(eb[k], fabs(dot3(Bc[k], L)), rb);
-        double sep = (fabs(dot3(T, L)) - (rc + rb)) / sqrt(len2);
-        if (sep >= thr) return 0;
+        double num = fabs(dot3(T, L)) - (rc + rb);
+        if (num >= thr * sqrt(len2)) return 0;
     }
     return 1;
 }

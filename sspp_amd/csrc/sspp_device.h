@@ -27,16 +27,27 @@ struct DGeom {
     double mat[9];   // row-major, columns = geom axes
     double size[3];
     double rbound;   // bounding-sphere radius (0 = infinite, planes)
+    double reach;    // moving geoms: |pos| (centre offset from the mover root), else 0
     int32_t type;
     int32_t mover;   // -1 static
     int32_t orig;    // model geom index (orders same-type pairs like the oracle)
-    int32_t pad;
+    int32_t relrot;  // moving geoms: 0 when mat is exactly the identity (pose = mover rotation)
 };
 
+// One filter-passing pair with the partner's data inlined, so the wave-uniform pair loop
+// reads one contiguous record per pair (scalar loads, no dependent index chain).
 struct DPair {
     int32_t gm;      // index of the moving geom in the DGeom table
     int32_t go;      // index of the partner geom
+    int32_t otype;   // partner type
+    int32_t oorig;   // partner model index
+    int32_t omover;  // partner mover (-1 static)
+    int32_t pad;
     double margin;   // max(margin1, margin2)
+    double opos[3];  // partner pose: world (static) or relative to its mover
+    double omat[9];
+    double osize[3];
+    double orbound;
 };
 
 struct DMover {
@@ -89,11 +100,8 @@ SSPP_HD void mulquat(const double* a, const double* b, double* r) {
     double t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
     r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
 }
+// mju_quat2Mat without MuJoCo's identity shortcut (same matrix; one code path, no scratch)
 SSPP_HD void quat2mat(const double* q, double* m) {
-    if (q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0) {
-        m[0] = 1; m[1] = 0; m[2] = 0; m[3] = 0; m[4] = 1; m[5] = 0; m[6] = 0; m[7] = 0; m[8] = 1;
-        return;
-    }
     double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
     double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
     double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
@@ -232,25 +240,28 @@ SSPP_HD int col_sphere_cyl(const double* sp, double r, const double* cp, const d
 }
 
 // Separating-axis test, two boxes: true iff every one of the 15 axis separations < thr.
+// Rows of R = A^T B are formed lazily so that an early separating face of A (the common
+// case: the moving box hovering over a static box) skips the rest.  Edge axes compare the
+// unnormalised separation with thr * |L| (no division; the oracle does the same).
 SSPP_HD bool sat_box_box(const double* pa, const double* ma, const double* ea, const double* pb,
                          const double* mb, const double* eb, double thr) {
-    double T[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    const double T[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    double B0[3], B1[3], B2[3];
+    col3(mb, 0, B0);
+    col3(mb, 1, B1);
+    col3(mb, 2, B2);
     double t[3], R[3][3], AR[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         double Ai[3];
         col3(ma, i, Ai);
         t[i] = dot3(Ai, T);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            double Bj[3];
-            col3(mb, j, Bj);
-            R[i][j] = dot3(Ai, Bj);
-            AR[i][j] = fabs(R[i][j]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
+        R[i][0] = dot3(Ai, B0);
+        R[i][1] = dot3(Ai, B1);
+        R[i][2] = dot3(Ai, B2);
+        AR[i][0] = fabs(R[i][0]);
+        AR[i][1] = fabs(R[i][1]);
+        AR[i][2] = fabs(R[i][2]);
         double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
         double sep = fabs(t[i]) - (ea[i] + rb);
         if (sep >= thr) return false;
@@ -280,8 +291,8 @@ SSPP_HD bool sat_box_box(const double* pa, const double* ma, const double* ea, c
                 double bk[3] = {R[0][k], R[1][k], R[2][k]};
                 rb = fma(eb[k], fabs(dot3(bk, L)), rb);
             }
-            double sep = (pr - (ra + rb)) / sqrt(len2);
-            if (sep >= thr) return false;
+            double num = pr - (ra + rb);
+            if (thr == 0.0 ? num >= 0.0 : num >= thr * sqrt(len2)) return false;
         }
     }
     return true;
@@ -314,8 +325,8 @@ SSPP_HD bool sat_cyl_box(const double* pa, const double* ma, const double* sz, c
         double rb = 0.0;
 #pragma unroll
         for (int k = 0; k < 3; ++k) rb = fma(eb[k], fabs(dot3(Bc[k], L)), rb);
-        double sep = (fabs(dot3(T, L)) - (rc + rb)) / sqrt(len2);
-        if (sep >= thr) return false;
+        double num = fabs(dot3(T, L)) - (rc + rb);
+        if (thr == 0.0 ? num >= 0.0 : num >= thr * sqrt(len2)) return false;
     }
     return true;
 }

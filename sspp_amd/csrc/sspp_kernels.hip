@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -30,16 +31,141 @@ using namespace sspd;
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef SSPP_SCORE_WAVES_PER_EU
+#define SSPP_SCORE_WAVES_PER_EU 4  // min waves per SIMD (4 -> <=128 VGPRs; measured best on gfx950)
+#endif
 constexpr int kMaxMovers = 2;
 
 struct KScene {
-    const DGeom* geoms;
-    const DPair* pairs;
-    const DMover* movers;
     int npairs;
+    int onegeom;        // every pair shares one moving geom: its pose is computed once
     int static_block;   // sspp: env-env contacts counted and present -> nothing feasible
     double static_cost; // tsp: Collision.h cost of env-env contacts, added per waypoint
 };
+
+// Scene tables are passed as separate __restrict__ kernel arguments: the pair loop is
+// wave-uniform and the tables are provably not written by the kernel, so the compiler
+// reads them with scalar (s_load) instructions into SGPRs, once per wave.
+struct SceneT {
+    const DGeom* __restrict__ geoms;
+    const DPair* __restrict__ pairs;
+    const DMover* __restrict__ movers;
+};
+
+// Constant address space (4): loads through these are scalar (SMEM) whenever the address
+// is wave-uniform, independent of the alias analysis of the surrounding kernel.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SSPP_CONST __attribute__((address_space(4)))
+#else
+#define SSPP_CONST
+#endif
+typedef const SSPP_CONST DGeom* cgeom_t;
+typedef const SSPP_CONST DPair* cpair_t;
+typedef const SSPP_CONST DMover* cmover_t;
+
+__device__ __forceinline__ DGeom load_geom(cgeom_t p) {
+    DGeom g;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g.pos[k] = p->pos[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) g.mat[k] = p->mat[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g.size[k] = p->size[k];
+    g.rbound = p->rbound;
+    g.reach = p->reach;
+    g.type = p->type;
+    g.mover = p->mover;
+    g.orig = p->orig;
+    g.relrot = p->relrot;
+    return g;
+}
+__device__ __forceinline__ DPair load_pair(cpair_t p) {
+    DPair r;
+    r.gm = p->gm;
+    r.go = p->go;
+    r.otype = p->otype;
+    r.oorig = p->oorig;
+    r.omover = p->omover;
+    r.pad = 0;
+    r.margin = p->margin;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r.opos[k] = p->opos[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.omat[k] = p->omat[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r.osize[k] = p->osize[k];
+    r.orbound = p->orbound;
+    return r;
+}
+
+// ---------------------------------------------------------------- candidate-level broadphase
+// A B-spline lies in the convex hull of its control points (non-negative basis, partition of
+// unity), so every waypoint's mover position lies in the AABB [lo, hi] of the control points'
+// position columns.  A pair whose partner cannot come within rbound + margin of that box
+// (expanded by the moving geom's reach) for ANY waypoint is culled for the whole candidate:
+// exactly the pairs the per-waypoint bounding-sphere test would reject at every waypoint.
+// kHullPad absorbs the rounding of the spline evaluation (|error| ~ 1e-15).
+constexpr double kHullPad = 1e-9;
+
+__device__ __forceinline__ bool pair_may_touch(const DPair& pr, const DGeom& G, const double* lo,
+                                               const double* hi) {
+    if (pr.omover >= 0 || G.rbound <= 0.0) return true;
+    const double slack = G.reach + G.rbound + pr.margin + kHullPad;
+    if (pr.orbound > 0.0) {
+        double d2 = 0.0;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double c = pr.opos[d];
+            const double e = c < lo[d] ? lo[d] - c : (c > hi[d] ? c - hi[d] : 0.0);
+            d2 = fma(e, e, d2);
+        }
+        const double lim = pr.orbound + slack;
+        return d2 <= lim * lim;
+    }
+    if (pr.otype == 0) {  // plane: lowest point of the box over the plane's normal
+        const double n0 = pr.omat[2], n1 = pr.omat[5], n2 = pr.omat[8];
+        const double m = (n0 >= 0 ? n0 * lo[0] : n0 * hi[0]) + (n1 >= 0 ? n1 * lo[1] : n1 * hi[1]) +
+                         (n2 >= 0 ? n2 * lo[2] : n2 * hi[2]) -
+                         (n0 * pr.opos[0] + n1 * pr.opos[1] + n2 * pr.opos[2]);
+        return m - slack < 0.0;
+    }
+    return true;
+}
+
+// Bit k of the result: pair k can touch (pairs >= 64 are always evaluated).  One lane per
+// pair, then a wave ballot -> the mask is wave-uniform (SGPRs).
+template <int D, int NM, int MODE>
+__device__ __forceinline__ unsigned long long hull_mask(const double* ctrl, int n, int npairs,
+                                                        cpair_t pairs, cgeom_t geoms,
+                                                        cmover_t movers) {
+    const int lane = threadIdx.x & 63;
+    bool act = false;
+    if (lane < npairs) {
+        const DPair pr = load_pair(pairs + lane);
+        const DGeom G = load_geom(geoms + pr.gm);
+        const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
+        double lo[3], hi[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int col = MODE == 1 ? d : 7 * m + d;
+            if (col < D) {
+                double a = ctrl[col], b = ctrl[col];
+                for (int j = 1; j < n; ++j) {
+                    const double v = ctrl[j * D + col];
+                    a = v < a ? v : a;
+                    b = v > b ? v : b;
+                }
+                lo[d] = a; hi[d] = b;
+            } else {
+                lo[d] = hi[d] = (double)movers[m].qpos0[d];
+            }
+        }
+        act = pair_may_touch(pr, G, lo, hi);
+    }
+    unsigned long long mask = __ballot(act);
+    if (npairs > 64) mask = ~0ull;
+    return mask;
+}
 
 struct BlockBest {
     double cost;
@@ -51,38 +177,22 @@ struct BlockBest {
 struct SsppK {
     KScene sc;
     int has_scene;
-    const double* knots;
-    int nknots, p, n, W;
-    const double* init_ctrl;
-    const double* ctrl_in;
-    double* ctrl_out;
+    int ablate;  // profiling only (SSPP_ABLATE env): 1 no sampling, 2 no collision, 4 no arc
+    int p, n, W;
     double sigma;
-    const double* limits;
     unsigned long long seed;
     long long first_id, B;
-    double* arc;
-    unsigned char* feasible;
-    BlockBest* part;
     int lpc, cpb, shared_endpoints;
 };
 
 struct TspK {
     KScene sc;
-    const double* knots;
-    int nknots, n, K, cp;
-    const double* Minv;
+    int n, K, cp;
     double start[4], end[4], lo[4], hi[4];
-    const double* mean;
-    const double* sigma;
     double z_min;
-    const double* vias_in;
-    double* vias_out;
     unsigned long long seed;
     long long first_id, B;
     double w_col, floor_z_min, floor_margin, floor_scale;
-    double *L, *Cnf, *Cwf, *cost;
-    unsigned char* status;
-    BlockBest* part;
     int lpc, cpb;
 };
 
@@ -124,15 +234,20 @@ __device__ __forceinline__ double uniform01(unsigned long long seed, unsigned lo
     return (double)b * 1.1102230246251565e-16;
 }
 
-// ---------------------------------------------------------------- spline from LDS tables
-template <int D>
-__device__ __forceinline__ void eval_pt(const double* ctrl, const double* N, int span, int p,
-                                        double* q) {
-    const double* c0 = ctrl + (span - p) * D;
+// ---------------------------------------------------------------- spline from basis rows
+// N: p+1 basis values of one waypoint (host-precomputed table in global memory, L2 resident)
+template <int D, int P>
+__device__ __forceinline__ void eval_pt(const double* ctrl, const double* __restrict__ N,
+                                        int span, double* q) {
+    double Nr[P + 1];
+#pragma unroll
+    for (int r = 0; r <= P; ++r) Nr[r] = N[r];
+    const double* c0 = ctrl + (span - P) * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        double acc = N[0] * c0[d];
-        for (int r = 1; r <= p; ++r) acc = fma(N[r], c0[r * D + d], acc);
+        double acc = Nr[0] * c0[d];
+#pragma unroll
+        for (int r = 1; r <= P; ++r) acc = fma(Nr[r], c0[r * D + d], acc);
         q[d] = acc;
     }
 }
@@ -153,19 +268,18 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // ---------------------------------------------------------------- one waypoint vs the scene
-// MODE 0: q = qpos[0:D] window (SamplingPathPlanner); MODE 1: q = (x, y, z, yaw) body point.
-// DEEP=false: returns 1 at the first contact (checkCollision's ncon > 0).
-// DEEP=true : returns 0, *cost = sum over deep contacts of -1/(center_dist + 1e-4).
-template <int D, int NM, int MODE, bool DEEP>
-__device__ int point_collide(const double* q, const KScene& sc, double* cost) {
-    double mp[NM][3], mR[NM][9];
+// Mover root poses (position + rotation) for MODE 0 (q -> qpos[0:D] window, free joints at
+// qpos[7m:7m+7]) or MODE 1 ((x, y, z, yaw) -> the bound free body, utility.h:149-206).
+template <int D, int NM, int MODE>
+__device__ __forceinline__ void mover_poses(const double* q, cmover_t movers,
+                                            double (&mp)[NM][3], double (&mR)[NM][9]) {
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
         double qp[7];
         if (MODE == 0) {
 #pragma unroll
-            for (int k = 0; k < 7; ++k) qp[k] = (7 * m + k < D) ? q[(7 * m + k < D) ? 7 * m + k : 0]
-                                                                : sc.movers[m].qpos0[k];
+            for (int k = 0; k < 7; ++k)
+                qp[k] = (7 * m + k < D) ? q[(7 * m + k < D) ? 7 * m + k : 0] : (double)movers[m].qpos0[k];
         } else {
             double half = q[3] * 0.5;
             qp[0] = q[0]; qp[1] = q[1]; qp[2] = q[2];
@@ -175,51 +289,86 @@ __device__ int point_collide(const double* q, const KScene& sc, double* cost) {
         quat2mat(qp + 3, mR[m]);
         mp[m][0] = qp[0]; mp[m][1] = qp[1]; mp[m][2] = qp[2];
     }
+}
+
+// Geom pose from its mover's pose.  With an identity relative rotation the geom frame IS the
+// mover frame: copying R reproduces the oracle's quat2mat(mulquat(root, 1)) exactly.
+__device__ __forceinline__ void geom_pose(const double* P, const double* R, const DGeom& G,
+                                          double* gp, double* gm) {
+    double t[3];
+    matvec3(R, G.pos, t);
+    gp[0] = P[0] + t[0]; gp[1] = P[1] + t[1]; gp[2] = P[2] + t[2];
+    if (G.relrot) {
+        matmul3(R, G.mat, gm);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) gm[k] = R[k];
+    }
+}
+
+// DEEP=false: returns 1 at the first contact (checkCollision's ncon > 0).
+// DEEP=true : returns 0, *cost = sum over deep contacts of -1/(center_dist + 1e-4) + static.
+template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM>
+__device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
+                             unsigned long long mask, double* cost) {
+    static_assert(!ONEGEOM || NM == 1, "single moving geom implies a single mover");
+    const cgeom_t geoms = (cgeom_t)T.geoms;
+    const cpair_t pairs = (cpair_t)T.pairs;
+    double mp[NM][3], mR[NM][9];
+    mover_poses<D, NM, MODE>(q, (cmover_t)T.movers, mp, mR);
     double acc = 0.0;
     int cur = -1;
     double gp[3], gmat[9];
-    for (int k = 0; k < sc.npairs; ++k) {
-        const DPair pr = sc.pairs[k];
-        const DGeom& G = sc.geoms[pr.gm];
-        if (pr.gm != cur) {
-            cur = pr.gm;
-            const int m = (NM == 1) ? 0 : G.mover;
-            const double* R = mR[0];
-            const double* P = mp[0];
-            if (NM > 1 && m == 1) { R = mR[NM - 1]; P = mp[NM - 1]; }
-            double t[3];
-            matvec3(R, G.pos, t);
-            gp[0] = P[0] + t[0]; gp[1] = P[1] + t[1]; gp[2] = P[2] + t[2];
-            matmul3(R, G.mat, gmat);
+    DGeom G;
+    if (ONEGEOM) {  // every pair shares one moving geom: pose once, mover pose dies here
+        cur = pairs[0].gm;
+        G = load_geom(geoms + cur);
+        geom_pose(mp[0], mR[0], G, gp, gmat);
+    }
+    const int np = sc.npairs;
+    for (int k = 0; k < np; ++k) {
+        if (k < 64) {
+            // skip culled pairs with a scalar bit scan
+            const unsigned long long rest = mask >> k;
+            if (rest == 0ull) break;
+            k += __builtin_ctzll(rest);
+            if (k >= np) break;
         }
-        const DGeom& O = sc.geoms[pr.go];
+        const DPair pr = load_pair(pairs + k);
+        if (!ONEGEOM && pr.gm != cur) {
+            cur = pr.gm;
+            G = load_geom(geoms + cur);
+            const bool second = NM > 1 && G.mover == 1;
+            geom_pose(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp, gmat);
+        }
         double op_[3], om_[9];
-        const double* op = O.pos;
-        const double* om = O.mat;
-        if (NM > 1 && O.mover >= 0) {
-            const double* R = (O.mover == 0) ? mR[0] : mR[NM - 1];
-            const double* P = (O.mover == 0) ? mp[0] : mp[NM - 1];
+        const double* op = pr.opos;
+        const double* om = pr.omat;
+        if (NM > 1 && pr.omover >= 0) {
+            const bool second = pr.omover == 1;
+            const double* R = second ? mR[NM - 1] : mR[0];
+            const double* P = second ? mp[NM - 1] : mp[0];
             double t[3];
-            matvec3(R, O.pos, t);
+            matvec3(R, pr.opos, t);
             op_[0] = P[0] + t[0]; op_[1] = P[1] + t[1]; op_[2] = P[2] + t[2];
-            matmul3(R, O.mat, om_);
+            matmul3(R, pr.omat, om_);
             op = op_; om = om_;
         }
-        double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
-        const double rg = G.rbound, ro = O.rbound;
+        const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
+        const double rg = G.rbound, ro = pr.orbound;
         if (rg > 0.0 && ro > 0.0) {
-            double thr = rg + ro + pr.margin;
+            const double thr = rg + ro + pr.margin;
             if (dot3(dc, dc) > thr * thr) continue;
         }
         int nd = 0, nc;
-        const bool gfirst = (G.type < O.type) || (G.type == O.type && G.orig < O.orig);
-        if (gfirst) nc = collide<DEEP>(G.type, gp, gmat, G.size, O.type, op, om, O.size, pr.margin, &nd);
-        else nc = collide<DEEP>(O.type, op, om, O.size, G.type, gp, gmat, G.size, pr.margin, &nd);
+        const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
+        if (gfirst) nc = collide<DEEP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+        else nc = collide<DEEP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
         if (!DEEP) {
             if (nc > 0) return 1;
         } else if (nd > 0) {
-            double cd = sqrt(dot3(dc, dc));
-            double term = -1.0 / (cd + 1e-4);
+            const double cd = sqrt(dot3(dc, dc));
+            const double term = -1.0 / (cd + 1e-4);
             for (int i = 0; i < nd; ++i) acc = acc + term;
         }
     }
@@ -227,87 +376,117 @@ __device__ int point_collide(const double* q, const KScene& sc, double* cost) {
     return 0;
 }
 
+// ---------------------------------------------------------------- batch argmin helpers
+__device__ __forceinline__ bool better(double c1, long long i1, double c2, long long i2) {
+    // lexicographic (cost, index); index -1 means "none"
+    if (i2 < 0) return i1 >= 0;
+    if (i1 < 0) return false;
+    return (c1 < c2) || (c1 == c2 && i1 < i2);
+}
+
+// ---------------------------------------------------------------- candidate sampler
+// sampleWithNoise (include/sspp.h:114-130) for candidate ids first_id + [0, B): one thread per
+// (candidate, Box-Muller pair) over the whole chip; writes the perturbed control-point columns
+// j in [p, n-p) as pert[B][npert] with npert = (n-2p)*D, value = init + (sigma * z) * limits[d].
+__global__ __launch_bounds__(kBlock) void k_sample_sspp(
+    unsigned long long seed, long long first_id, long long B, int D, int p, int npert,
+    double sigma, const double* __restrict__ init_ctrl, const double* __restrict__ limits,
+    double* __restrict__ pert) {
+    const int npairs = (npert + 1) >> 1;
+    const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= B * npairs) return;
+    const long long b = t / npairs;
+    const int m = (int)(t - b * npairs);
+    double z0, z1;
+    normal_pair(seed, (unsigned long long)(first_id + b), (unsigned)m, 0u, &z0, &z1);
+    const double* base = init_ctrl + p * D;
+    double* out = pert + b * npert;
+    const int k0 = 2 * m, k1 = 2 * m + 1;
+    {
+        const double noise = (sigma * z0) * limits[k0 % D];
+        out[k0] = base[k0] + noise;
+    }
+    if (k1 < npert) {
+        const double noise = (sigma * z1) * limits[k1 % D];
+        out[k1] = base[k1] + noise;
+    }
+}
+
 // ---------------------------------------------------------------- SamplingPathPlanner kernel
-template <int D, int NM>
-__global__ __launch_bounds__(kBlock) void k_sspp(SsppK a) {
+// tab: host-precomputed basis rows, (W+1) collision rows u = i/W then W arc rows v = i/(W-1),
+// P+1 doubles each; span: matching knot spans.
+template <int D, int NM, int P, bool ONEGEOM>
+__global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
+    SsppK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
+    const double* __restrict__ ctrl_in, const double* __restrict__ pert,
+    double* __restrict__ ctrl_out, double* __restrict__ arc, unsigned char* __restrict__ feasible,
+    BlockBest* __restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, p = a.p, n = a.n, W = a.W;
-    const int P1 = p + 1, ndof = n * D;
+    constexpr int P1 = P + 1;
+    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, W = a.W;
+    const int ndof = n * D;
     const int slot = tid / lpc, lane = tid - slot * lpc;
     const long long cand0 = (long long)blockIdx.x * cpb;
-    double* s_ctrl = smem;
-    double* s_bcol = s_ctrl + cpb * ndof;
-    double* s_barc = s_bcol + (W + 1) * P1;
-    double* s_wsum = s_barc + W * P1;
-    double* s_arc = s_wsum + kBlock / 64;
-    int* s_scol = (int*)(s_arc + 4);
-    int* s_sarc = s_scol + (W + 1);
-    int* s_flag = s_sarc + W;  // [cpb] per-candidate feasibility, [cpb] shared endpoints
+    double* s_ctrl = smem;                        // [cpb][n][D]
+    double* s_wsum = s_ctrl + cpb * ndof;         // [4]
+    double* s_arc = s_wsum + kBlock / 64;         // [4]
+    int* s_flag = (int*)(s_arc + 4);              // [cpb] + shared endpoints
+    const double* tcol = tab;
+    const double* tarc = tab + (W + 1) * P1;
+    const int* scol = span;
+    const int* sarc = span + (W + 1);
 
-    // basis tables: collision grid u = i/W (i = 0..W), arc grid v = i/(W-1) (i = 0..W-1)
-    for (int r = tid; r < 2 * W + 1; r += kBlock) {
-        double u;
-        double* dst;
-        int* sd;
-        if (r <= W) { u = (double)r / W; dst = s_bcol + r * P1; sd = s_scol + r; }
-        else { int i = r - (W + 1); u = (double)i / (W - 1); dst = s_barc + i * P1; sd = s_sarc + i; }
-        int sp = span_of(u, p, a.knots, a.nknots);
-        double N[kMaxP + 1];
-        basis_funcs(u, p, sp, a.knots, N);
-        for (int j = 0; j <= p; ++j) dst[j] = N[j];
-        *sd = sp;
-    }
     if (tid <= cpb) s_flag[tid] = 1;
-
-    // control points
     const long long nvalid = min((long long)cpb, a.B - cand0);
-    if (a.ctrl_in) {
-        const double* src = a.ctrl_in + cand0 * ndof;
+    // prefetch this lane's basis rows (global, L2-resident) while the control points stage
+    double Ncol[P1];
+    int sc0 = P;
+    {
+        const int i = lane + 1 < W ? lane + 1 : W - 1;
+#pragma unroll
+        for (int r = 0; r < P1; ++r) Ncol[r] = tcol[i * P1 + r];
+        sc0 = scol[i];
+    }
+    if (ctrl_in) {
+        const double* src = ctrl_in + cand0 * ndof;
         for (int e = tid; e < nvalid * ndof; e += kBlock) s_ctrl[e] = src[e];
     } else {
-        for (int e = tid; e < cpb * ndof; e += kBlock) s_ctrl[e] = a.init_ctrl[e % ndof];
-        __syncthreads();
-        const int npert = (n - 2 * p) * D;
-        const int npairs = (npert + 1) >> 1;
-        for (int e = tid; e < cpb * npairs; e += kBlock) {
-            const int s = e / npairs, m = e - s * npairs;
-            if (s >= nvalid) continue;
-            const unsigned long long g = (unsigned long long)(a.first_id + cand0 + s);
-            double z0, z1;
-            normal_pair(a.seed, g, (unsigned)m, 0u, &z0, &z1);
-            double* c = s_ctrl + s * ndof + p * D;
-            const int k0 = 2 * m, k1 = 2 * m + 1;
-            {
-                const int d = k0 % D;
-                double noise = (a.sigma * z0) * a.limits[d];
-                c[k0] = c[k0] + noise;
-            }
-            if (k1 < npert) {
-                const int d = k1 % D;
-                double noise = (a.sigma * z1) * a.limits[d];
-                c[k1] = c[k1] + noise;
-            }
+        // init control points + the sampler kernel's perturbed columns j in [p, n-p)
+        const int npert = (n - 2 * P) * D;
+        for (int e = tid; e < cpb * ndof; e += kBlock) {
+            const int sl = e / ndof, r = e - sl * ndof;
+            const int k = r - P * D;
+            s_ctrl[e] = (k >= 0 && k < npert && sl < nvalid && !(a.ablate & 1))
+                            ? pert[(cand0 + sl) * npert + k]
+                            : init_ctrl[r];
         }
     }
     __syncthreads();
-    if (a.ctrl_out) {
-        double* dst = a.ctrl_out + cand0 * ndof;
+    if (ctrl_out) {
+        double* dst = ctrl_out + cand0 * ndof;
         for (int e = tid; e < nvalid * ndof; e += kBlock) dst[e] = s_ctrl[e];
     }
 
     const bool valid = slot < nvalid;
     const double* myc = s_ctrl + slot * ndof;
     double q[D], q2[D];
+    const unsigned long long mask =
+        a.has_scene ? hull_mask<D, NM, 0>(myc, n, a.sc.npairs, (cpair_t)T.pairs, (cgeom_t)T.geoms,
+                                          (cmover_t)T.movers)
+                    : 0ull;
 
     // checkCollision: interior points i = 1..W-1 one per lane; endpoints i = 0, W on a spare lane
-    if (a.has_scene && valid) {
-        volatile int* vflag = s_flag;
+    // Flags are plain LDS stores (every writer stores 0; read after the barrier below):
+    // no volatile/atomic access, so the scene tables stay on the scalar-load path.
+    if (a.has_scene && valid && !(a.ablate & 2)) {
+        int* vflag = s_flag;
         if (a.sc.static_block) vflag[slot] = 0;
         for (int j = lane; j < W - 1; j += lpc) {
-            if (vflag[slot] == 0) break;
             const int i = j + 1;
-            eval_pt<D>(myc, s_bcol + i * P1, s_scol[i], p, q);
-            if (point_collide<D, NM, 0, false>(q, a.sc, nullptr)) { vflag[slot] = 0; break; }
+            if (j == lane) eval_pt<D, P>(myc, Ncol, sc0, q);
+            else eval_pt<D, P>(myc, tcol + i * P1, scol[i], q);
+            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr)) { vflag[slot] = 0; break; }
         }
         const int spare = (W - 1) % lpc == 0 ? 0 : lpc - 1;
         bool duty0 = false, dutyW = false;
@@ -315,29 +494,29 @@ __global__ __launch_bounds__(kBlock) void k_sspp(SsppK a) {
         if (a.shared_endpoints) {
             fidx = cpb;
             if (lane == spare) {
-                if (cpb == 1) { duty0 = dutyW = true; }
+                if (nvalid == 1) { duty0 = dutyW = slot == 0; }
                 else { duty0 = slot == 0; dutyW = slot == 1; }
             }
         } else if (lane == spare) {
             duty0 = dutyW = true;
         }
         if (duty0) {
-            eval_pt<D>(myc, s_bcol, s_scol[0], p, q);
-            if (point_collide<D, NM, 0, false>(q, a.sc, nullptr)) vflag[fidx] = 0;
+            eval_pt<D, P>(myc, tcol, scol[0], q);
+            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr)) vflag[fidx] = 0;
         }
         if (dutyW) {
-            eval_pt<D>(myc, s_bcol + W * P1, s_scol[W], p, q);
-            if (point_collide<D, NM, 0, false>(q, a.sc, nullptr)) vflag[fidx] = 0;
+            eval_pt<D, P>(myc, tcol + W * P1, scol[W], q);
+            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr)) vflag[fidx] = 0;
         }
     }
 
     // computeArcLength: chords between v_{i-1} and v_i, i = 1..W-1
     double acc = 0.0;
-    if (valid) {
+    if (valid && !(a.ablate & 4)) {
         for (int j = lane; j < W - 1; j += lpc) {
             const int i = j + 1;
-            eval_pt<D>(myc, s_barc + (i - 1) * P1, s_sarc[i - 1], p, q);
-            eval_pt<D>(myc, s_barc + i * P1, s_sarc[i], p, q2);
+            eval_pt<D, P>(myc, tarc + (i - 1) * P1, sarc[i - 1], q);
+            eval_pt<D, P>(myc, tarc + i * P1, sarc[i], q2);
             acc = acc + dist_nd<D>(q, q2);
         }
     }
@@ -350,8 +529,8 @@ __global__ __launch_bounds__(kBlock) void k_sspp(SsppK a) {
         for (int w = 1; w < nw; ++w) t = t + s_wsum[w0 + w];
         const long long c = cand0 + slot;
         const int f = s_flag[slot] & s_flag[cpb];
-        a.arc[c] = t;
-        a.feasible[c] = (unsigned char)f;
+        arc[c] = t;
+        feasible[c] = (unsigned char)f;
         s_arc[slot] = f ? t : INFINITY;
     }
     __syncthreads();
@@ -363,13 +542,20 @@ __global__ __launch_bounds__(kBlock) void k_sspp(SsppK a) {
             bb.count++;
             if (s_arc[s] < bb.cost) { bb.cost = s_arc[s]; bb.idx = a.first_id + cand0 + s; }
         }
-        a.part[blockIdx.x] = bb;
+        part[blockIdx.x] = bb;
     }
 }
 
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
-template <int NM>
-__global__ __launch_bounds__(kBlock) void k_tsp(TspK a) {
+// tab: (cp+1) rows of 3 basis values at u = i * (1/cp); Minv: collocation inverse (n x n).
+template <int NM, bool ONEGEOM>
+__global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_tsp(
+    TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ Minv, const double* __restrict__ mean,
+    const double* __restrict__ sigma, const double* __restrict__ vias_in,
+    double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
+    double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
+    BlockBest* __restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int D = 4, P = 2, P1 = 3;
     const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, K = a.K, cp = a.cp;
@@ -378,32 +564,20 @@ __global__ __launch_bounds__(kBlock) void k_tsp(TspK a) {
     const int ndof = n * D;
     double* s_V = smem;                      // [cpb][n][4]
     double* s_ctrl = s_V + cpb * ndof;       // [cpb][n][4]
-    double* s_b = s_ctrl + cpb * ndof;       // [(cp+1)][3]
-    double* s_wsum = s_b + (cp + 1) * P1;    // [3][4]
+    double* s_wsum = s_ctrl + cpb * ndof;    // [3][4]
     double* s_best = s_wsum + 3 * (kBlock / 64);
-    int* s_span = (int*)(s_best + 4);        // [cp+1]
-    int* s_stat = s_span + (cp + 1);         // [cpb]
+    int* s_stat = (int*)(s_best + 4);        // [cpb]
 
-    const double du = 1.0 / cp;
-    for (int r = tid; r <= cp; r += kBlock) {
-        const double u = (double)r * du;
-        int sp = span_of(u, P, a.knots, a.nknots);
-        double N[kMaxP + 1];
-        basis_funcs(u, P, sp, a.knots, N);
-        for (int j = 0; j <= P; ++j) s_b[r * P1 + j] = N[j];
-        s_span[r] = sp;
-    }
     const long long nvalid = min((long long)cpb, a.B - cand0);
-    // via points: V = [start, vias..., end]
     for (int e = tid; e < cpb * 2 * D; e += kBlock) {
         const int s = e / (2 * D), r = e - s * 2 * D;
         if (r < D) s_V[s * ndof + r] = a.start[r];
         else s_V[s * ndof + (n - 1) * D + (r - D)] = a.end[r - D];
     }
-    if (a.vias_in) {
+    if (vias_in) {
         for (int e = tid; e < nvalid * K * D; e += kBlock) {
             const int s = e / (K * D), r = e - s * K * D;
-            s_V[s * ndof + D + r] = a.vias_in[(cand0 + s) * K * D + r];
+            s_V[s * ndof + D + r] = vias_in[(cand0 + s) * K * D + r];
         }
     } else {
         // Sampler::sample_set (tsp_sampler.h:12-51) with Philox streams per (candidate, via, dim)
@@ -412,7 +586,7 @@ __global__ __launch_bounds__(kBlock) void k_tsp(TspK a) {
             if (s >= nvalid) continue;
             const int v = r / D, i = r - v * D;
             const unsigned long long g = (unsigned long long)(a.first_id + cand0 + s);
-            const double m = a.mean[v * D + i], sg = a.sigma[v * D + i];
+            const double m = mean[v * D + i], sg = sigma[v * D + i];
             double val;
             if (i < 3) {
                 bool ok = false;
@@ -445,18 +619,18 @@ __global__ __launch_bounds__(kBlock) void k_tsp(TspK a) {
         }
     }
     __syncthreads();
-    if (a.vias_out) {
+    if (vias_out) {
         for (int e = tid; e < nvalid * K * D; e += kBlock) {
             const int s = e / (K * D), r = e - s * K * D;
-            a.vias_out[(cand0 + s) * K * D + r] = s_V[s * ndof + D + r];
+            vias_out[(cand0 + s) * K * D + r] = s_V[s * ndof + D + r];
         }
     }
     // PathModel::fromVias: ctrl = A^-1 V (collocation inverse precomputed on the host)
     for (int e = tid; e < cpb * ndof; e += kBlock) {
         const int s = e / ndof, r = e - s * ndof, j = r / D, d = r - j * D;
         const double* Vs = s_V + s * ndof;
-        double acc = a.Minv[j * n] * Vs[d];
-        for (int i = 1; i < n; ++i) acc = fma(a.Minv[j * n + i], Vs[i * D + d], acc);
+        double acc = Minv[j * n] * Vs[d];
+        for (int i = 1; i < n; ++i) acc = fma(Minv[j * n + i], Vs[i * D + d], acc);
         s_ctrl[e] = acc;
     }
     __syncthreads();
@@ -464,16 +638,18 @@ __global__ __launch_bounds__(kBlock) void k_tsp(TspK a) {
     // Evaluator::eval_one_pass (tsp_evaluator.h:18-32), waypoint i = 1..cp per lane
     const bool valid = slot < nvalid;
     const double* myc = s_ctrl + slot * ndof;
+    const unsigned long long mask = hull_mask<D, NM, 1>(myc, n, a.sc.npairs, (cpair_t)T.pairs,
+                                                        (cgeom_t)T.geoms, (cmover_t)T.movers);
     double aL = 0.0, aC = 0.0, aW = 0.0;
     if (valid) {
         for (int j = lane; j < cp; j += lpc) {
             const int i = j + 1;
             double pv[4], pc[4];
-            eval_pt<D>(myc, s_b + (i - 1) * P1, s_span[i - 1], P, pv);
-            eval_pt<D>(myc, s_b + i * P1, s_span[i], P, pc);
+            eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
+            eval_pt<D, P>(myc, tab + i * P1, span[i], pc);
             aL = aL + dist_nd<D>(pv, pc);
             double c = 0.0;
-            point_collide<D, NM, 1, true>(pc, a.sc, &c);
+            point_collide<D, NM, 1, true, ONEGEOM>(pc, a.sc, T, mask, &c);
             const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
             const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
             aC = aC + c;
@@ -501,8 +677,8 @@ __global__ __launch_bounds__(kBlock) void k_tsp(TspK a) {
         const long long c = cand0 + slot;
         const int st = Cn == 0.0;
         const double cost = L + a.w_col * Cw;
-        a.L[c] = L; a.Cnf[c] = Cn; a.Cwf[c] = Cw; a.cost[c] = cost;
-        a.status[c] = (unsigned char)st;
+        oL[c] = L; oCnf[c] = Cn; oCwf[c] = Cw; ocost[c] = cost;
+        ostatus[c] = (unsigned char)st;
         s_stat[slot] = st;
         s_best[slot] = cost;
     }
@@ -515,45 +691,44 @@ __global__ __launch_bounds__(kBlock) void k_tsp(TspK a) {
             bb.count++;
             if (s_best[s] < bb.cost) { bb.cost = s_best[s]; bb.idx = a.first_id + cand0 + s; }
         }
-        a.part[blockIdx.x] = bb;
+        part[blockIdx.x] = bb;
     }
 }
 
 // ---------------------------------------------------------------- argmin over block results
-__device__ __forceinline__ bool better(double c1, long long i1, double c2, long long i2) {
-    // lexicographic (cost, index); index -1 means "none"
-    if (i2 < 0) return i1 >= 0;
-    if (i1 < 0) return false;
-    return (c1 < c2) || (c1 == c2 && i1 < i2);
-}
 
-__global__ __launch_bounds__(kBlock) void k_argmin(const BlockBest* part, int nparts,
-                                                   sspp_best* out) {
-    __shared__ double sc[kBlock];
-    __shared__ long long si[kBlock], sn[kBlock];
+constexpr int kArgminThreads = 1024;
+__global__ __launch_bounds__(kArgminThreads) void k_argmin(const BlockBest* __restrict__ part,
+                                                           int nparts, sspp_best* out) {
+    __shared__ double sc[kArgminThreads / 64];
+    __shared__ long long si[kArgminThreads / 64], sn[kArgminThreads / 64];
     double bc = INFINITY;
     long long bi = -1, cnt = 0;
-    for (int i = threadIdx.x; i < nparts; i += kBlock) {
+    for (int i = threadIdx.x; i < nparts; i += kArgminThreads) {
         const BlockBest b = part[i];
         cnt += b.count;
         if (better(b.cost, b.idx, bc, bi)) { bc = b.cost; bi = b.idx; }
     }
-    sc[threadIdx.x] = bc; si[threadIdx.x] = bi; sn[threadIdx.x] = cnt;
-    __syncthreads();
-    for (int s = kBlock / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            const int o = threadIdx.x + s;
-            if (better(sc[o], si[o], sc[threadIdx.x], si[threadIdx.x])) {
-                sc[threadIdx.x] = sc[o]; si[threadIdx.x] = si[o];
-            }
-            sn[threadIdx.x] += sn[o];
-        }
-        __syncthreads();
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double oc = __shfl_xor(bc, off, 64);
+        const long long oi = __shfl_xor(bi, off, 64);
+        cnt += __shfl_xor(cnt, off, 64);
+        if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
     }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sc[w] = bc; si[w] = bi; sn[w] = cnt; }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        out->cost = si[0] < 0 ? INFINITY : sc[0];
-        out->index = si[0];
-        out->count = sn[0];
+        double c = sc[0];
+        long long i = si[0], n = sn[0];
+        for (int k = 1; k < kArgminThreads / 64; ++k) {
+            n += sn[k];
+            if (better(sc[k], si[k], c, i)) { c = sc[k]; i = si[k]; }
+        }
+        out->cost = i < 0 ? INFINITY : c;
+        out->index = i;
+        out->count = n;
         out->reserved = 0;
     }
 }
@@ -590,12 +765,16 @@ struct sspp_job {
     double sigma = 0.0;
     uint64_t seed = 0;
     double* d_knots = nullptr;
+    double* d_tab = nullptr;   // basis rows (host-precomputed, P+1 doubles per waypoint)
+    int* d_span = nullptr;     // knot span per waypoint
     double* d_init = nullptr;
     double* d_limits = nullptr;
     double* d_Minv = nullptr;
     double* d_mean = nullptr;
     double* d_sigma = nullptr;
     BlockBest* d_part = nullptr;
+    double* d_pert = nullptr;  // sampler output: perturbed columns [max_batch][(n-2p)*D]
+    int npert = 0;
     double start[4], end[4], lo[4], hi[4];
     double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
 };
@@ -730,6 +909,10 @@ int sspp_scene_create(const sspp_model* m, int mode, int arg, int count_static, 
         for (int k = 0; k < 9; ++k) dg.mat[k] = M[9 * g + k];
         for (int k = 0; k < 3; ++k) dg.size[k] = m->geom_size[3 * g + k];
         dg.rbound = geom_rbound(dg.type, dg.size);
+        dg.relrot = 0;
+        for (int k = 0; k < 9; ++k) dg.relrot |= dg.mat[k] != ((k % 4 == 0) ? 1.0 : 0.0);
+        dg.reach = mv ? std::sqrt(dg.pos[0] * dg.pos[0] + dg.pos[1] * dg.pos[1] + dg.pos[2] * dg.pos[2]) * (1.0 + 1e-12)
+                      : 0.0;
         table_index[g] = (int)s->geoms.size();
         s->geoms.push_back(dg);
         if (m->geom_contype[g] || m->geom_conaffinity[g]) {
@@ -811,7 +994,15 @@ int sspp_scene_create(const sspp_model* m, int mode, int arg, int count_static, 
         DPair dp{};
         dp.gm = table_index[gm];
         dp.go = table_index[go];
+        const DGeom& O = s->geoms[dp.go];
+        dp.otype = O.type;
+        dp.oorig = O.orig;
+        dp.omover = O.mover;
         dp.margin = pr.margin;
+        for (int k = 0; k < 3; ++k) dp.opos[k] = O.pos[k];
+        for (int k = 0; k < 9; ++k) dp.omat[k] = O.mat[k];
+        for (int k = 0; k < 3; ++k) dp.osize[k] = O.size[k];
+        dp.orbound = O.rbound;
         s->pairs.push_back(dp);
     }
     for (size_t i = 0; i < mover_bodies.size(); ++i) {
@@ -856,13 +1047,35 @@ void sspp_scene_free(sspp_scene* s) {
 static KScene kscene(const sspp_scene* s, bool tsp) {
     KScene k{};
     if (!s) return k;
-    k.geoms = s->d_geoms;
-    k.pairs = s->d_pairs;
-    k.movers = s->d_movers;
     k.npairs = (int)s->pairs.size();
+    k.onegeom = 1;
+    for (const DPair& p : s->pairs) k.onegeom &= (p.gm == s->pairs[0].gm);
     k.static_block = (!tsp && s->count_static && s->static_contacts > 0) ? 1 : 0;
     k.static_cost = tsp ? s->static_cost : 0.0;
     return k;
+}
+
+static SceneT scene_t(const sspp_scene* s) {
+    SceneT t{};
+    if (!s) return t;
+    t.geoms = s->d_geoms;
+    t.pairs = s->d_pairs;
+    t.movers = s->d_movers;
+    return t;
+}
+
+// Basis rows for a list of parameters (same A2.1/A2.2 code as the device header).
+static int upload_basis(const std::vector<double>& us, int p, const double* knots, int nknots,
+                        double** d_tab, int** d_span) {
+    std::vector<double> tab(us.size() * (p + 1));
+    std::vector<int> sp(us.size());
+    for (size_t i = 0; i < us.size(); ++i) {
+        sp[i] = span_of(us[i], p, knots, nknots);
+        basis_funcs(us[i], p, sp[i], knots, &tab[i * (p + 1)]);
+    }
+    int rc = upload(d_tab, tab.data(), tab.size());
+    if (rc) return rc;
+    return upload(d_span, sp.data(), sp.size());
 }
 
 extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_args* a, int64_t max_batch,
@@ -873,7 +1086,8 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     const int D = a->dof, p = a->degree, n = a->n_ctrl, W = a->check_points;
     if (!(D == 1 || D == 2 || D == 3 || D == 4 || D == 6 || D == 7 || D == 9))
         return sspp::set_error(SSPP_E_UNSUPPORTED, "dof must be one of 1,2,3,4,6,7,9");
-    if (p < 1 || p > kMaxP || n < p + 1) return sspp::set_error(SSPP_E_INVAL, "bad degree / control point count");
+    if (p < 2 || p > 3) return sspp::set_error(SSPP_E_UNSUPPORTED, "GPU scorer supports spline degree 2 or 3");
+    if (n < p + 1) return sspp::set_error(SSPP_E_INVAL, "need at least degree + 1 control points");
     if (W < 2 || W > 1 << 20) return sspp::set_error(SSPP_E_INVAL, "check_points must be >= 2");
     if (max_batch < 1) return sspp::set_error(SSPP_E_INVAL, "max_batch must be >= 1");
     if (scene && (scene->mode != SSPP_MODE_QPOS || scene->dof != D))
@@ -889,16 +1103,25 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     bool clamped = true;
     for (int i = 0; i <= p; ++i) clamped = clamped && a->knots[i] == a->knots[0] && a->knots[n + i] == a->knots[n + p];
     j->shared_endpoints = clamped ? 1 : 0;
-    j->lds = sizeof(double) * ((size_t)j->cpb * n * D + (size_t)(2 * W + 1) * (p + 1) + kBlock / 64 + 4) +
-             sizeof(int) * ((size_t)(2 * W + 1) + j->cpb + 1);
+    j->lds = sizeof(double) * ((size_t)j->cpb * n * D + kBlock / 64 + 4) + sizeof(int) * (j->cpb + 1);
     if (j->lds > 160 * 1024) { delete j; return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS"); }
     int rc;
     const int64_t nblk = (max_batch + j->cpb - 1) / j->cpb;
+    std::vector<double> us;
+    for (int i = 0; i <= W; ++i) us.push_back((double)i / W);            // collision grid
+    for (int i = 0; i < W; ++i) us.push_back((double)i / (W - 1));       // arc-length grid
     if ((rc = upload(&j->d_knots, a->knots, (size_t)j->nknots)) ||
+        (rc = upload_basis(us, p, a->knots, j->nknots, &j->d_tab, &j->d_span)) ||
         (rc = upload(&j->d_init, a->init_ctrl, (size_t)n * D)) ||
         (rc = upload(&j->d_limits, a->limits, (size_t)D))) {
         sspp_job_free(j);
         return rc;
+    }
+    j->npert = (n - 2 * p) * D;
+    if (j->npert < 0) j->npert = 0;
+    if (j->npert > 0 && hipMalloc((void**)&j->d_pert, sizeof(double) * (size_t)max_batch * j->npert) != hipSuccess) {
+        sspp_job_free(j);
+        return sspp::set_error(SSPP_E_NOMEM, "hipMalloc sampler buffer");
     }
     if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess) {
         sspp_job_free(j);
@@ -908,25 +1131,43 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     return SSPP_OK;
 }
 
-template <int D, int NM>
-static hipError_t launch_sspp(const SsppK& k, int nblk, size_t lds, hipStream_t st) {
-    hipLaunchKernelGGL((k_sspp<D, NM>), dim3(nblk), dim3(kBlock), lds, st, k);
+struct SsppPtrs {
+    const double* ctrl_in;
+    double* ctrl_out;
+    double* arc;
+    unsigned char* feasible;
+};
+
+template <int D, int NM, int P>
+static hipError_t launch_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                              hipStream_t st) {
+    if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
+        hipLaunchKernelGGL((k_sspp<D, 1, P, true>), dim3(nblk), dim3(kBlock), j->lds, st, k,
+                           scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
+                           j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((k_sspp<D, NM, P, false>), dim3(nblk), dim3(kBlock), j->lds, st, k,
+                       scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
+                       j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part);
     return hipGetLastError();
 }
 
-static hipError_t dispatch_sspp(int D, int nm, const SsppK& k, int nblk, size_t lds, hipStream_t st) {
-    if (nm == 2) {
-        if (D == 9) return launch_sspp<9, 2>(k, nblk, lds, st);
+template <int P>
+static hipError_t dispatch_sspp_p(const SsppK& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                                  hipStream_t st) {
+    if (j->nm == 2) {
+        if (j->D == 9) return launch_sspp<9, 2, P>(k, j, o, nblk, st);
         return hipErrorInvalidValue;
     }
-    switch (D) {
-        case 1: return launch_sspp<1, 1>(k, nblk, lds, st);
-        case 2: return launch_sspp<2, 1>(k, nblk, lds, st);
-        case 3: return launch_sspp<3, 1>(k, nblk, lds, st);
-        case 4: return launch_sspp<4, 1>(k, nblk, lds, st);
-        case 6: return launch_sspp<6, 1>(k, nblk, lds, st);
-        case 7: return launch_sspp<7, 1>(k, nblk, lds, st);
-        case 9: return launch_sspp<9, 1>(k, nblk, lds, st);
+    switch (j->D) {
+        case 1: return launch_sspp<1, 1, P>(k, j, o, nblk, st);
+        case 2: return launch_sspp<2, 1, P>(k, j, o, nblk, st);
+        case 3: return launch_sspp<3, 1, P>(k, j, o, nblk, st);
+        case 4: return launch_sspp<4, 1, P>(k, j, o, nblk, st);
+        case 6: return launch_sspp<6, 1, P>(k, j, o, nblk, st);
+        case 7: return launch_sspp<7, 1, P>(k, j, o, nblk, st);
+        case 9: return launch_sspp<9, 1, P>(k, j, o, nblk, st);
     }
     return hipErrorInvalidValue;
 }
@@ -940,17 +1181,27 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     SsppK k{};
     k.sc = kscene(j->scene, false);
     k.has_scene = j->scene != nullptr;
-    k.knots = j->d_knots; k.nknots = j->nknots; k.p = j->p; k.n = j->n; k.W = j->W;
-    k.init_ctrl = j->d_init; k.ctrl_in = d_ctrl; k.ctrl_out = d_ctrl_out;
-    k.sigma = j->sigma; k.limits = j->d_limits; k.seed = j->seed;
-    k.first_id = first_id; k.B = B; k.arc = d_arc; k.feasible = d_feasible; k.part = j->d_part;
+    k.p = j->p; k.n = j->n; k.W = j->W;
+    k.sigma = j->sigma; k.seed = j->seed;
+    k.first_id = first_id; k.B = B;
     k.lpc = j->lpc; k.cpb = j->cpb; k.shared_endpoints = (d_ctrl == nullptr) ? j->shared_endpoints : 0;
+    static const int ablate = [] { const char* e = getenv("SSPP_ABLATE"); return e ? atoi(e) : 0; }();
+    k.ablate = ablate;
+    SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible};
     const int nblk = (int)((B + j->cpb - 1) / j->cpb);
     hipStream_t st = (hipStream_t)stream;
-    hipError_t e = dispatch_sspp(j->D, j->nm, k, nblk, j->lds, st);
+    if (!d_ctrl && j->npert > 0) {  // sampleWithNoise over the whole chip
+        const long long work = B * (long long)((j->npert + 1) / 2);
+        hipLaunchKernelGGL(k_sample_sspp, dim3((unsigned)((work + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                           (unsigned long long)j->seed, (long long)first_id, (long long)B, j->D, j->p,
+                           j->npert, j->sigma, j->d_init, j->d_limits, j->d_pert);
+        hipError_t es = hipGetLastError();
+        if (es != hipSuccess) return hip_fail(es, "k_sample_sspp launch");
+    }
+    hipError_t e = j->p == 3 ? dispatch_sspp_p<3>(k, j, o, nblk, st) : dispatch_sspp_p<2>(k, j, o, nblk, st);
     if (e != hipSuccess) return hip_fail(e, "k_sspp launch");
-    if (!d_best) return SSPP_OK;  // scoring kernel only (profiling)
-    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kBlock), 0, st, j->d_part, nblk, d_best);
+    if (!d_best) return SSPP_OK;  // scoring kernels only (profiling)
+    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kArgminThreads), 0, st, j->d_part, nblk, d_best);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_argmin launch");
     return SSPP_OK;
@@ -987,8 +1238,7 @@ extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args*
     j->floor_z_min = a->floor_z_min; j->floor_margin = a->floor_margin; j->floor_scale = a->floor_scale;
     j->lpc = lanes_for(cp);
     j->cpb = kBlock / j->lpc;
-    j->lds = sizeof(double) * ((size_t)2 * j->cpb * n * 4 + (size_t)(cp + 1) * 3 + 3 * (kBlock / 64) + 4) +
-             sizeof(int) * ((size_t)(cp + 1) + j->cpb);
+    j->lds = sizeof(double) * ((size_t)2 * j->cpb * n * 4 + 3 * (kBlock / 64) + 4) + sizeof(int) * j->cpb;
     if (j->lds > 160 * 1024) { delete j; return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS"); }
     std::vector<double> u(n), knots(n + 3), Minv((size_t)n * n);
     for (int i = 0; i < n; ++i) u[i] = (double)i / (n - 1);
@@ -999,7 +1249,11 @@ extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args*
     std::vector<double> zero(4, 0.0);
     int rc;
     const int64_t nblk = (max_batch + j->cpb - 1) / j->cpb;
+    std::vector<double> us;
+    const double du = 1.0 / cp;
+    for (int i = 0; i <= cp; ++i) us.push_back((double)i * du);  // eval_one_pass: s(i * du)
     if ((rc = upload(&j->d_knots, knots.data(), knots.size())) ||
+        (rc = upload_basis(us, 2, knots.data(), (int)knots.size(), &j->d_tab, &j->d_span)) ||
         (rc = upload(&j->d_Minv, Minv.data(), Minv.size())) ||
         (rc = upload(&j->d_mean, K ? a->mean : zero.data(), K ? (size_t)K * 4 : 4)) ||
         (rc = upload(&j->d_sigma, K ? a->sigma : zero.data(), K ? (size_t)K * 4 : 4))) {
@@ -1024,22 +1278,26 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
         return sspp::set_error(SSPP_E_INVAL, "null output");
     TspK k{};
     k.sc = kscene(j->scene, true);
-    k.knots = j->d_knots; k.nknots = j->nknots; k.n = j->n; k.K = j->K; k.cp = j->cp;
-    k.Minv = j->d_Minv;
+    k.n = j->n; k.K = j->K; k.cp = j->cp;
     for (int i = 0; i < 4; ++i) { k.start[i] = j->start[i]; k.end[i] = j->end[i]; k.lo[i] = j->lo[i]; k.hi[i] = j->hi[i]; }
-    k.mean = j->d_mean; k.sigma = j->d_sigma; k.z_min = j->z_min;
-    k.vias_in = d_vias; k.vias_out = d_vias_out; k.seed = j->seed; k.first_id = first_id; k.B = B;
+    k.z_min = j->z_min; k.seed = j->seed; k.first_id = first_id; k.B = B;
     k.w_col = j->w_col; k.floor_z_min = j->floor_z_min; k.floor_margin = j->floor_margin;
     k.floor_scale = j->floor_scale;
-    k.L = d_L; k.Cnf = d_Cnf; k.Cwf = d_Cwf; k.cost = d_cost; k.status = d_status; k.part = j->d_part;
     k.lpc = j->lpc; k.cpb = j->cpb;
     const int nblk = (int)((B + j->cpb - 1) / j->cpb);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL((k_tsp<1>), dim3(nblk), dim3(kBlock), j->lds, st, k);
+    if (k.sc.onegeom && k.sc.npairs > 0)
+        hipLaunchKernelGGL((k_tsp<1, true>), dim3(nblk), dim3(kBlock), j->lds, st, k, scene_t(j->scene),
+                           j->d_tab, j->d_span, j->d_Minv, j->d_mean, j->d_sigma, d_vias, d_vias_out,
+                           d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part);
+    else
+        hipLaunchKernelGGL((k_tsp<1, false>), dim3(nblk), dim3(kBlock), j->lds, st, k, scene_t(j->scene),
+                           j->d_tab, j->d_span, j->d_Minv, j->d_mean, j->d_sigma, d_vias, d_vias_out,
+                           d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_tsp launch");
     if (!d_best) return SSPP_OK;  // scoring kernel only (profiling)
-    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kBlock), 0, st, j->d_part, nblk, d_best);
+    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kArgminThreads), 0, st, j->d_part, nblk, d_best);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_argmin launch");
     return SSPP_OK;
@@ -1070,9 +1328,11 @@ extern "C" int sspp_job_info(const sspp_job* j, int* lpc, int* cpb, int* threads
 
 extern "C" void sspp_job_free(sspp_job* j) {
     if (!j) return;
-    for (double* p : {j->d_knots, j->d_init, j->d_limits, j->d_Minv, j->d_mean, j->d_sigma})
+    for (double* p : {j->d_knots, j->d_tab, j->d_init, j->d_limits, j->d_Minv, j->d_mean, j->d_sigma})
         if (p) (void)hipFree(p);
+    if (j->d_span) (void)hipFree(j->d_span);
     if (j->d_part) (void)hipFree(j->d_part);
+    if (j->d_pert) (void)hipFree(j->d_pert);
     delete j;
 }
 
@@ -1081,7 +1341,7 @@ extern "C" int sspp_best_reduce_device(const sspp_best* d_parts, int n, sspp_bes
     sspp::clear_error();
     if (!d_parts || !d_out || n < 1) return sspp::set_error(SSPP_E_INVAL, "sspp_best_reduce_device: bad argument");
     static_assert(sizeof(BlockBest) == sizeof(sspp_best), "layout");
-    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kBlock), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kArgminThreads), 0, (hipStream_t)stream,
                        reinterpret_cast<const BlockBest*>(d_parts), n, d_out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_argmin launch");

@@ -1,0 +1,56 @@
+"""Profiling helper: per-batch kernel time for the scoring path (robocrane sspp / stacking tsp).
+
+    SSPP_ABLATE=<mask> SSPP_LIB_PATH=<variant .so> CONFIG=robocrane|stacking python tools/ablate.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import sspp_amd as S  # noqa: E402
+
+cfg = os.environ.get("CONFIG", "robocrane")
+B = int(os.environ.get("B", "4096" if cfg == "robocrane" else "16384"))
+if cfg == "robocrane":
+    model = S.Model(os.path.join(S.SCENE_DIR, "robocrane.xml"))
+    scene = S.Scene(model, 0, 7)
+    start = np.array([0.5, 0.15, 0.136, 0.707, 0, 0, 0.707])
+    end = np.array([0.5, -0.05, 0.136, 0.707, 0, 0, 0.707])
+    u = np.array([i / 9 for i in range(10)])
+    knots, ctrl0 = S.interpolate(np.array([(1 - t) * start + t * end for t in u]), 3, u)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=B)
+    o = job.alloc(B)
+
+    def run(i, best):
+        job.sample_score(i * B, B, o["arc"], o["feasible"], best)
+    feas = lambda: int(o["feasible"].sum().item())  # noqa: E731
+else:
+    model = S.Model(os.path.join(S.SCENE_DIR, "stacking.xml"))
+    scene = S.Scene(model, 1, "block1")
+    start = model.body_point("block1") + np.array([0, 0, 0.02, 0])
+    end = model.body_point("block2") + np.array([0, 0, 0.22, 0])
+    job = S.TspJob(scene, start, end, 1, 128, mean=(start + 0.5 * (end - start)).reshape(1, 4),
+                   sigma=np.full((1, 4), 0.2), lo=np.array([-0.5, -0.5, 0.0, -1.6]),
+                   hi=np.array([0.5, 0.5, 0.6, 1.6]), max_batch=B)
+    o = job.alloc(B)
+
+    def run(i, best):
+        job.sample_score(i * B, B, o["L"], o["Cnf"], o["Cwf"], o["status"], o["cost"], best)
+    feas = lambda: int(o["status"].sum().item())  # noqa: E731
+for i in range(20):
+    run(i, o["best"])
+torch.cuda.synchronize()
+res = {}
+for name, best in (("kernel_only", None), ("full_step", o["best"])):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(200):
+        run(i, best)
+    e1.record()
+    torch.cuda.synchronize()
+    res[name] = e0.elapsed_time(e1) / 200 * 1e3
+print(json.dumps(dict(config=cfg, lib=os.path.basename(os.environ.get("SSPP_LIB_PATH", "default")),
+                      ablate=int(os.environ.get("SSPP_ABLATE", "0")), B=B, us=res, feasible=feas())))
