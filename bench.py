@@ -10,7 +10,9 @@ the scene, arc-length cost and the argmin over feasible candidates (include/sspp
 Default workload = BASELINE.json configs[1]: SamplingPathPlanner7 on the robocrane scene,
 4096 candidates x 128 waypoints per GPU (weak scaling: every rank scores its own 4096
 candidates with globally unique Philox ids; the per-step global argmin is one RCCL all-gather
-of a 32-byte record per rank, reduced on the device).
+of a 32-byte record per rank, reduced on the device). Consecutive steps are independent
+batches and alternate over --streams (default 2) HIP streams, each with its own job, so one
+batch's argmin tail and launch gap hide under the next batch's scoring.
 
 Printed (rank 0): one JSON line with value = candidates scored per second over all ranks,
 a `roofline` object for the dominant kernel (k_sspp), a `roofline_fp64` object, and a
@@ -46,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-launches", type=int, default=200)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="independent batches in flight (one job + stream each, steps alternate)")
     return ap.parse_args()
 
 
@@ -59,16 +63,17 @@ def setup_robocrane(args, device):
     u = np.array([i / (n - 1) for i in range(n)])
     knots, ctrl0 = S.interpolate(np.array([(1 - t) * start + t * end for t in u]), 3, u)
     B = args.batch or 4096
-    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=S.DEFAULT_SEED, max_batch=B)
-    bufs = job.alloc(B, device=device)
-    bufs["ctrl"] = None
+    jobs = [S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=S.DEFAULT_SEED, max_batch=B)
+            for _ in range(args.streams)]
+    bufs = [j.alloc(B, device=device) for j in jobs]
+    job = jobs[0]
 
-    def step(first_id, best=None, ctrl_out=None):
-        job.sample_score(first_id, B, bufs["arc"], bufs["feasible"],
-                         bufs["best"] if best is None else best, ctrl_out=ctrl_out)
+    def step(first_id, best, lane=0, stream=None):
+        jobs[lane].sample_score(first_id, B, bufs[lane]["arc"], bufs[lane]["feasible"], best,
+                                stream=stream)
 
     def kernel_only(first_id):
-        job.sample_score(first_id, B, bufs["arc"], bufs["feasible"], None)
+        job.sample_score(first_id, B, bufs[0]["arc"], bufs[0]["feasible"], None)
 
     n_, D, p = 10, 7, 3
     # SURVEY §8(d) algorithmic work per candidate
@@ -92,17 +97,19 @@ def setup_stacking(args, device):
     sigma = np.full((1, 4), 0.2)
     lo, hi = np.array([-0.5, -0.5, 0.0, -1.6]), np.array([0.5, 0.5, 0.6, 1.6])
     B = args.batch or 16384
-    job = S.TspJob(scene, start, end, K, cp, mean=mean, sigma=sigma, lo=lo, hi=hi, z_min=0.0,
-                   max_batch=B)
-    bufs = job.alloc(B, device=device)
+    jobs = [S.TspJob(scene, start, end, K, cp, mean=mean, sigma=sigma, lo=lo, hi=hi, z_min=0.0,
+                     max_batch=B) for _ in range(args.streams)]
+    bufs = [j.alloc(B, device=device) for j in jobs]
+    job = jobs[0]
 
-    def step(first_id, best=None, ctrl_out=None):
-        job.sample_score(first_id, B, bufs["L"], bufs["Cnf"], bufs["Cwf"], bufs["status"],
-                         bufs["cost"], bufs["best"] if best is None else best, vias_out=ctrl_out)
+    def step(first_id, best, lane=0, stream=None):
+        q = bufs[lane]
+        jobs[lane].sample_score(first_id, B, q["L"], q["Cnf"], q["Cwf"], q["status"], q["cost"],
+                                best, stream=stream)
 
     def kernel_only(first_id):
-        job.sample_score(first_id, B, bufs["L"], bufs["Cnf"], bufs["Cwf"], bufs["status"],
-                         bufs["cost"], None)
+        q = bufs[0]
+        job.sample_score(first_id, B, q["L"], q["Cnf"], q["Cwf"], q["status"], q["cost"], None)
 
     n_, D = K + 2, 4
     bytes_per = n_ * D * 8 + 8 + 1
@@ -191,16 +198,22 @@ def main():
     setup = setup_robocrane if args.config == "robocrane" else setup_stacking
     B, step, kernel_only, bytes_per, flops_per, meta, ctx = setup(args, device)
 
-    gathered = torch.zeros((world, 4), dtype=torch.int64, device=device)
-    gbest = S.best_tensor(device)
-    local_best = S.best_tensor(device)
+    ns = args.streams
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device) for _ in range(ns - 1)]
+    gathered = [torch.zeros((world, 4), dtype=torch.int64, device=device) for _ in range(ns)]
+    gbest = [S.best_tensor(device) for _ in range(ns)]
+    local_best = [S.best_tensor(device) for _ in range(ns)]
 
     def full_step(i):
+        # step i runs on stream i % ns: consecutive batches overlap, so one batch's argmin tail
+        # and launch gap hide under the next batch's scoring (the steps are independent)
+        lane = i % ns
         first = (i * world + rank) * B  # globally unique candidate ids
-        step(first, best=local_best)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, local_best)
-            S.reduce_best_device(gathered, gbest)
+        with torch.cuda.stream(streams[lane]):
+            step(first, local_best[lane], lane, streams[lane])
+            if world > 1:
+                dist.all_gather_into_tensor(gathered[lane], local_best[lane])
+                S.reduce_best_device(gathered[lane], gbest[lane], stream=streams[lane])
 
     for i in range(args.warmup):
         full_step(i)
@@ -254,7 +267,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (on-device Philox candidates around a linear init spline)",
-            "config": dict(meta, parallelism="dp%d (candidate shards, RCCL all-gather argmin)" % world),
+            "config": dict(meta, streams=ns,
+                           parallelism="dp%d (candidate shards, RCCL all-gather argmin)" % world),
             "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach_gbs / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "k_sspp" if ctx["kind"] == "sspp" else "k_tsp",

@@ -177,7 +177,8 @@ struct BlockBest {
 struct SsppK {
     KScene sc;
     int has_scene;
-    int ablate;  // profiling only (SSPP_ABLATE env): 1 no sampling, 2 no collision, 4 no arc
+    int ablate;    // profiling only (SSPP_ABLATE env): 1 no sampling, 2 no collision, 4 no arc
+    int insample;  // draw the candidates inside the scoring kernel (else k_sample_sspp)
     int p, n, W;
     double sigma;
     unsigned long long seed;
@@ -306,11 +307,15 @@ __device__ __forceinline__ void geom_pose(const double* P, const double* R, cons
     }
 }
 
-// DEEP=false: returns 1 at the first contact (checkCollision's ncon > 0).
+// DEEP=false: checkCollision's ncon > 0 for one candidate.  Every active lane of the wave
+//   must belong to that candidate: the scan stops for the whole wave at the first pair where
+//   any lane finds a contact (returns 1 on every lane — the candidate is infeasible whatever
+//   the other waypoints give), or when *stop (the candidate's LDS flag, cleared by another
+//   wave of the same candidate) reads 0.  Returns 0 when no lane has a contact.
 // DEEP=true : returns 0, *cost = sum over deep contacts of -1/(center_dist + 1e-4) + static.
 template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
-                             unsigned long long mask, double* cost) {
+                             unsigned long long mask, double* cost, int* stop = nullptr) {
     static_assert(!ONEGEOM || NM == 1, "single moving geom implies a single mover");
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
@@ -356,16 +361,22 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
         }
         const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
         const double rg = G.rbound, ro = pr.orbound;
+        bool near = true;
         if (rg > 0.0 && ro > 0.0) {
             const double thr = rg + ro + pr.margin;
-            if (dot3(dc, dc) > thr * thr) continue;
+            near = !(dot3(dc, dc) > thr * thr);
         }
-        int nd = 0, nc;
-        const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
-        if (gfirst) nc = collide<DEEP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
-        else nc = collide<DEEP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+        int nd = 0, nc = 0;
+        if (near) {
+            const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
+            if (gfirst) nc = collide<DEEP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+            else nc = collide<DEEP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+        }
         if (!DEEP) {
-            if (nc > 0) return 1;
+            // the loop trip is wave-uniform, so every active lane reaches this vote
+            if (__ballot(nc > 0) != 0ull) return 1;
+            if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                return 1;
         } else if (nd > 0) {
             const double cd = sqrt(dot3(dc, dc));
             const double term = -1.0 / (cd + 1e-4);
@@ -382,6 +393,116 @@ __device__ __forceinline__ bool better(double c1, long long i1, double c2, long 
     if (i2 < 0) return i1 >= 0;
     if (i1 < 0) return false;
     return (c1 < c2) || (c1 == c2 && i1 < i2);
+}
+
+// ---------------------------------------------------------------- fused batch argmin
+// Each workgroup publishes one BlockBest; arrivals are counted on 8 sharded counters (one
+// 64-byte line each, shard = block % 8) so no single word sees more than ~B/16 atomics.
+// The last arriver of a shard reduces that shard and publishes a shard record; the last of
+// the shards reduces the 8 shard records into *out and re-arms every counter.
+// Hand-off (cdna_hip_programming.md Guideline 16, R1 with sc1 on both sides): records are
+// written with 8-byte agent-scope relaxed atomic stores (global_store ... sc1, write-through),
+// every storing lane drains with s_waitcnt vmcnt(0) before its relaxed agent atomic add, and
+// consumers read records only with agent-scope relaxed atomic loads (sc1, bypass L1) after
+// their add returned "last" and a workgroup barrier.  No release/acquire fences needed.
+struct ArgminSync {
+    unsigned int shard[8][16];  // arrival counters, one cache line each
+    unsigned int top[16];
+    BlockBest rec[8];           // shard results
+};
+
+__device__ __forceinline__ void st_rec(BlockBest* p, const BlockBest& b) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q + 0, (unsigned long long)__double_as_longlong(b.cost), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (unsigned long long)b.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 2, (unsigned long long)b.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ BlockBest ld_rec(BlockBest* p) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    BlockBest b;
+    b.cost = __longlong_as_double((long long)__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    b.idx = (long long)__hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b.count = (long long)__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b.pad = 0;
+    return b;
+}
+
+// block-wide lexicographic reduction of records idx0 + stride*i, i < n (all threads call)
+__device__ BlockBest reduce_recs(BlockBest* recs, int idx0, int stride, int n, double* scratch) {
+    double bc = INFINITY;
+    long long bi = -1, cnt = 0;
+    for (int i = threadIdx.x; i < n; i += kBlock) {
+        const BlockBest b = ld_rec(recs + idx0 + (long long)stride * i);
+        cnt += b.count;
+        if (better(b.cost, b.idx, bc, bi)) { bc = b.cost; bi = b.idx; }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double oc = __shfl_xor(bc, off, 64);
+        const long long oi = __shfl_xor(bi, off, 64);
+        cnt += __shfl_xor(cnt, off, 64);
+        if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        scratch[3 * w] = bc;
+        scratch[3 * w + 1] = __longlong_as_double(bi);
+        scratch[3 * w + 2] = __longlong_as_double(cnt);
+    }
+    __syncthreads();
+    BlockBest r;
+    r.cost = scratch[0];
+    r.idx = __double_as_longlong(scratch[1]);
+    r.count = __double_as_longlong(scratch[2]);
+    r.pad = 0;
+    for (int k = 1; k < kBlock / 64; ++k) {
+        const double oc = scratch[3 * k];
+        const long long oi = __double_as_longlong(scratch[3 * k + 1]);
+        r.count += __double_as_longlong(scratch[3 * k + 2]);
+        if (better(oc, oi, r.cost, r.idx)) { r.cost = oc; r.idx = oi; }
+    }
+    return r;
+}
+
+// All threads of the workgroup call this after thread 0 filled `bb`.
+__device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, ArgminSync* sync,
+                             sspp_best* out) {
+    __shared__ double scratch[16];
+    const int nblk = gridDim.x, b = blockIdx.x, sh = b & 7;
+    const int nsh = nblk < 8 ? nblk : 8;
+    int* flag = reinterpret_cast<int*>(scratch + 14);
+    if (!out) {
+        if (threadIdx.x == 0) part[b] = bb;
+        return;
+    }
+    if (threadIdx.x == 0) {
+        st_rec(part + b, bb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned shard_n = (unsigned)((nblk - sh + 7) >> 3);
+        const unsigned prev = __hip_atomic_fetch_add(&sync->shard[sh][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = prev == shard_n - 1;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const BlockBest shard_best = reduce_recs(part, sh, 8, (nblk - sh + 7) >> 3, scratch);
+    if (threadIdx.x == 0) {
+        st_rec(sync->rec + sh, shard_best);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(&sync->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = prev == (unsigned)nsh - 1;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const BlockBest r = reduce_recs(sync->rec, 0, 1, nsh, scratch);
+    if (threadIdx.x == 0) {
+        out->cost = r.idx < 0 ? INFINITY : r.cost;
+        out->index = r.idx;
+        out->count = r.count;
+        out->reserved = 0;
+        for (int k = 0; k < 8; ++k) __hip_atomic_store(&sync->shard[k][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sync->top[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // ---------------------------------------------------------------- candidate sampler
@@ -421,7 +542,7 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
     const double* __restrict__ init_ctrl, const double* __restrict__ limits,
     const double* __restrict__ ctrl_in, const double* __restrict__ pert,
     double* __restrict__ ctrl_out, double* __restrict__ arc, unsigned char* __restrict__ feasible,
-    BlockBest* __restrict__ part) {
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int P1 = P + 1;
     const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, W = a.W;
@@ -452,14 +573,36 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
         const double* src = ctrl_in + cand0 * ndof;
         for (int e = tid; e < nvalid * ndof; e += kBlock) s_ctrl[e] = src[e];
     } else {
-        // init control points + the sampler kernel's perturbed columns j in [p, n-p)
+        // init control points + perturbed columns j in [p, n-p): from the sampler kernel, or
+        // (insample) drawn here by the workgroup itself
         const int npert = (n - 2 * P) * D;
+        const bool from_pert = !a.insample && !(a.ablate & 1);
         for (int e = tid; e < cpb * ndof; e += kBlock) {
             const int sl = e / ndof, r = e - sl * ndof;
             const int k = r - P * D;
-            s_ctrl[e] = (k >= 0 && k < npert && sl < nvalid && !(a.ablate & 1))
+            s_ctrl[e] = (from_pert && k >= 0 && k < npert && sl < nvalid)
                             ? pert[(cand0 + sl) * npert + k]
                             : init_ctrl[r];
+        }
+        if (a.insample) {
+            __syncthreads();
+            const int npairs = (npert + 1) >> 1;
+            for (int e = tid; e < cpb * npairs; e += kBlock) {
+                const int sl = e / npairs, m = e - sl * npairs;
+                if (sl >= nvalid) continue;
+                double z0, z1;
+                normal_pair(a.seed, (unsigned long long)(a.first_id + cand0 + sl), (unsigned)m, 0u, &z0, &z1);
+                double* c = s_ctrl + sl * ndof + P * D;
+                const int k0 = 2 * m, k1 = 2 * m + 1;
+                {
+                    const double noise = (a.sigma * z0) * limits[k0 % D];
+                    c[k0] = c[k0] + noise;
+                }
+                if (k1 < npert) {
+                    const double noise = (a.sigma * z1) * limits[k1 % D];
+                    c[k1] = c[k1] + noise;
+                }
+            }
         }
     }
     __syncthreads();
@@ -486,7 +629,10 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
             const int i = j + 1;
             if (j == lane) eval_pt<D, P>(myc, Ncol, sc0, q);
             else eval_pt<D, P>(myc, tcol + i * P1, scol[i], q);
-            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr)) { vflag[slot] = 0; break; }
+            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr, vflag + slot)) {
+                __hip_atomic_store(vflag + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
+            }
         }
         const int spare = (W - 1) % lpc == 0 ? 0 : lpc - 1;
         bool duty0 = false, dutyW = false;
@@ -534,16 +680,16 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
         s_arc[slot] = f ? t : INFINITY;
     }
     __syncthreads();
+    BlockBest bb;
     if (tid == 0) {
-        BlockBest bb;
         bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
         for (int s = 0; s < nvalid; ++s) {
             if (!(s_flag[s] & s_flag[cpb])) continue;
             bb.count++;
             if (s_arc[s] < bb.cost) { bb.cost = s_arc[s]; bb.idx = a.first_id + cand0 + s; }
         }
-        part[blockIdx.x] = bb;
     }
+    finish_batch(bb, part, sync, best);
 }
 
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
@@ -555,7 +701,7 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_tsp(
     const double* __restrict__ sigma, const double* __restrict__ vias_in,
     double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
     double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
-    BlockBest* __restrict__ part) {
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int D = 4, P = 2, P1 = 3;
     const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, K = a.K, cp = a.cp;
@@ -683,16 +829,16 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_tsp(
         s_best[slot] = cost;
     }
     __syncthreads();
+    BlockBest bb;
     if (tid == 0) {
-        BlockBest bb;
         bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
         for (int s = 0; s < nvalid; ++s) {
             if (!s_stat[s]) continue;
             bb.count++;
             if (s_best[s] < bb.cost) { bb.cost = s_best[s]; bb.idx = a.first_id + cand0 + s; }
         }
-        part[blockIdx.x] = bb;
     }
+    finish_batch(bb, part, sync, best);
 }
 
 // ---------------------------------------------------------------- argmin over block results
@@ -775,6 +921,8 @@ struct sspp_job {
     BlockBest* d_part = nullptr;
     double* d_pert = nullptr;  // sampler output: perturbed columns [max_batch][(n-2p)*D]
     int npert = 0;
+    int insample = 0;          // sample inside the scoring kernel (SSPP_INSAMPLE=1)
+    ArgminSync* d_sync = nullptr;  // sharded arrival counters of the fused argmin
     double start[4], end[4], lo[4], hi[4];
     double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
 };
@@ -1119,11 +1267,14 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     }
     j->npert = (n - 2 * p) * D;
     if (j->npert < 0) j->npert = 0;
+    { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : 0; }
     if (j->npert > 0 && hipMalloc((void**)&j->d_pert, sizeof(double) * (size_t)max_batch * j->npert) != hipSuccess) {
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc sampler buffer");
     }
-    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess) {
+    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess ||
+        hipMalloc((void**)&j->d_sync, sizeof(ArgminSync)) != hipSuccess ||
+        hipMemset(j->d_sync, 0, sizeof(ArgminSync)) != hipSuccess) {
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
     }
@@ -1136,6 +1287,7 @@ struct SsppPtrs {
     double* ctrl_out;
     double* arc;
     unsigned char* feasible;
+    sspp_best* best;
 };
 
 template <int D, int NM, int P>
@@ -1144,12 +1296,12 @@ static hipError_t launch_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs&
     if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
         hipLaunchKernelGGL((k_sspp<D, 1, P, true>), dim3(nblk), dim3(kBlock), j->lds, st, k,
                            scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
-                           j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part);
+                           j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((k_sspp<D, NM, P, false>), dim3(nblk), dim3(kBlock), j->lds, st, k,
                        scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
-                       j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part);
+                       j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
     return hipGetLastError();
 }
 
@@ -1187,10 +1339,11 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     k.lpc = j->lpc; k.cpb = j->cpb; k.shared_endpoints = (d_ctrl == nullptr) ? j->shared_endpoints : 0;
     static const int ablate = [] { const char* e = getenv("SSPP_ABLATE"); return e ? atoi(e) : 0; }();
     k.ablate = ablate;
-    SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible};
+    k.insample = j->insample;
+    SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
     const int nblk = (int)((B + j->cpb - 1) / j->cpb);
     hipStream_t st = (hipStream_t)stream;
-    if (!d_ctrl && j->npert > 0) {  // sampleWithNoise over the whole chip
+    if (!d_ctrl && j->npert > 0 && !j->insample) {  // sampleWithNoise over the whole chip
         const long long work = B * (long long)((j->npert + 1) / 2);
         hipLaunchKernelGGL(k_sample_sspp, dim3((unsigned)((work + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                            (unsigned long long)j->seed, (long long)first_id, (long long)B, j->D, j->p,
@@ -1200,10 +1353,6 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     }
     hipError_t e = j->p == 3 ? dispatch_sspp_p<3>(k, j, o, nblk, st) : dispatch_sspp_p<2>(k, j, o, nblk, st);
     if (e != hipSuccess) return hip_fail(e, "k_sspp launch");
-    if (!d_best) return SSPP_OK;  // scoring kernels only (profiling)
-    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kArgminThreads), 0, st, j->d_part, nblk, d_best);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "k_argmin launch");
     return SSPP_OK;
 }
 
@@ -1260,7 +1409,9 @@ extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args*
         sspp_job_free(j);
         return rc;
     }
-    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess) {
+    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess ||
+        hipMalloc((void**)&j->d_sync, sizeof(ArgminSync)) != hipSuccess ||
+        hipMemset(j->d_sync, 0, sizeof(ArgminSync)) != hipSuccess) {
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
     }
@@ -1289,17 +1440,13 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     if (k.sc.onegeom && k.sc.npairs > 0)
         hipLaunchKernelGGL((k_tsp<1, true>), dim3(nblk), dim3(kBlock), j->lds, st, k, scene_t(j->scene),
                            j->d_tab, j->d_span, j->d_Minv, j->d_mean, j->d_sigma, d_vias, d_vias_out,
-                           d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part);
+                           d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part, j->d_sync, d_best);
     else
         hipLaunchKernelGGL((k_tsp<1, false>), dim3(nblk), dim3(kBlock), j->lds, st, k, scene_t(j->scene),
                            j->d_tab, j->d_span, j->d_Minv, j->d_mean, j->d_sigma, d_vias, d_vias_out,
-                           d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part);
+                           d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part, j->d_sync, d_best);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_tsp launch");
-    if (!d_best) return SSPP_OK;  // scoring kernel only (profiling)
-    hipLaunchKernelGGL(k_argmin, dim3(1), dim3(kArgminThreads), 0, st, j->d_part, nblk, d_best);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "k_argmin launch");
     return SSPP_OK;
 }
 
@@ -1333,6 +1480,7 @@ extern "C" void sspp_job_free(sspp_job* j) {
     if (j->d_span) (void)hipFree(j->d_span);
     if (j->d_part) (void)hipFree(j->d_part);
     if (j->d_pert) (void)hipFree(j->d_pert);
+    if (j->d_sync) (void)hipFree(j->d_sync);
     delete j;
 }
 
