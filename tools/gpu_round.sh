@@ -1,5 +1,18 @@
+# Round evidence: gpu tests, smoke, bench (N=1), rocprofv3 kernel-trace stats, PMC HBM passes.
+#   gpurun --timeout 1100 -- bash tools/gpu_round.sh [tag]
 set -o pipefail
-cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/gpu_tests.log 2>&1; echo "EXIT $?" >> gpurun_out/gpu_tests.log
-timeout -k 10 300 python bench.py --steps 200 --warmup 20 > gpurun_out/bench4.json 2> gpurun_out/bench4.err || exit 1
-cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof4 -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof4.log 2>&1
+TAG=${1:-r01}
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out/$TAG
+O=$R/gpurun_out/$TAG
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > $O/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "SMOKE FAILED"; tail -20 $O/smoke.log; exit 1; }
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 300 python bench.py --config stacking > $O/bench_stacking.json 2> $O/bench_stacking.err || { echo "BENCH2 FAILED"; tail -20 $O/bench_stacking.err; exit 1; }
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 200 --warmup 20 --no-cpu-baseline > $O/prof.log 2>&1 || { echo "PROF FAILED"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --roofline-launches 20 > $O/pmc_fetch.log 2>&1 || { echo "PMC1 FAILED"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --roofline-launches 20 > $O/pmc_write.log 2>&1 || { echo "PMC2 FAILED"; exit 1; }
+echo DONE
