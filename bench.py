@@ -48,8 +48,12 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-launches", type=int, default=200)
-    ap.add_argument("--streams", type=int, default=2,
-                    help="independent batches in flight (one job + stream each, steps alternate)")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="independent batches in flight (one job + stream/graph branch each)")
+    ap.add_argument("--mode", default="native", choices=["native", "eager"],
+                    help="native: the C++ step executor enqueues --chunk steps per call "
+                         "(robocrane); eager: one Python-level launch per step")
+    ap.add_argument("--chunk", type=int, default=50)
     return ap.parse_args()
 
 
@@ -75,6 +79,9 @@ def setup_robocrane(args, device):
     def kernel_only(first_id):
         job.sample_score(first_id, B, bufs[0]["arc"], bufs[0]["feasible"], None)
 
+    def make_executor(streams):
+        return S.SsppSteps(jobs, streams, B, [b["arc"] for b in bufs], [b["feasible"] for b in bufs])
+
     n_, D, p = 10, 7, 3
     # SURVEY §8(d) algorithmic work per candidate
     bytes_per = n_ * D * 8 + 8 + 1
@@ -82,7 +89,8 @@ def setup_robocrane(args, device):
         (W + 1) * (40 + 42 + 48 + 8 * 450 + 300)
     meta = dict(workload="robocrane SamplingPathPlanner7 (block_green free joint), sigma 0.08",
                 candidates_per_gpu=B, waypoints=W, init_points=n_, degree=p, dof=D)
-    ctx = dict(kind="sspp", job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p)
+    ctx = dict(kind="sspp", job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p,
+               make_executor=make_executor)
     return B, step, kernel_only, bytes_per, flops_per, meta, ctx
 
 
@@ -199,31 +207,71 @@ def main():
     B, step, kernel_only, bytes_per, flops_per, meta, ctx = setup(args, device)
 
     ns = args.streams
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device) for _ in range(ns - 1)]
-    gathered = [torch.zeros((world, 4), dtype=torch.int64, device=device) for _ in range(ns)]
-    gbest = [S.best_tensor(device) for _ in range(ns)]
-    local_best = [S.best_tensor(device) for _ in range(ns)]
+    native = args.mode == "native" and "make_executor" in ctx
+    if native:
+        # The C++ step executor enqueues G steps per call, round robin over ns streams (one job
+        # each): step t scores global ids (t * world + rank) * B + [0, B), so the candidate set
+        # does not depend on the rank count.  With several ranks each chunk's G per-step argmin
+        # records go through ONE all-gather (bucketed) and are reduced per step on the device.
+        G = max(1, args.chunk)
+        main = torch.cuda.current_stream()
+        streams = [main] + [torch.cuda.Stream(device) for _ in range(ns - 1)]
+        ex = ctx["make_executor"](streams)
+        best = torch.zeros((G, 4), dtype=torch.int64, device=device)
+        gbufs = {}
+        counter = [0]
 
-    def full_step(i):
-        # step i runs on stream i % ns: consecutive batches overlap, so one batch's argmin tail
-        # and launch gap hide under the next batch's scoring (the steps are independent)
-        lane = i % ns
-        first = (i * world + rank) * B  # globally unique candidate ids
-        with torch.cuda.stream(streams[lane]):
-            step(first, local_best[lane], lane, streams[lane])
-            if world > 1:
-                dist.all_gather_into_tensor(gathered[lane], local_best[lane])
-                S.reduce_best_device(gathered[lane], gbest[lane], stream=streams[lane])
+        def gbuf(g):
+            if g not in gbufs:
+                gbufs[g] = (torch.zeros((world, g, 4), dtype=torch.int64, device=device),
+                            torch.zeros((g, 4), dtype=torch.int64, device=device))
+            return gbufs[g]
 
-    for i in range(args.warmup):
-        full_step(i)
+        def run_steps(k):
+            while k > 0:
+                g = min(G, k)
+                if world > 1:
+                    for st in streams[1:]:
+                        st.wait_stream(main)
+                ex.enqueue(g, (counter[0] * world + rank) * B, world * B, best[:g])
+                if world > 1:
+                    for st in streams[1:]:
+                        main.wait_stream(st)
+                    gat, gout = gbuf(g)
+                    dist.all_gather_into_tensor(gat, best[:g])
+                    S.reduce_best_steps(gat, gout)
+                counter[0] += g
+                k -= g
+    else:
+        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device) for _ in range(ns - 1)]
+        gathered = [torch.zeros((world, 4), dtype=torch.int64, device=device) for _ in range(ns)]
+        gbest = [S.best_tensor(device) for _ in range(ns)]
+        local_best = [S.best_tensor(device) for _ in range(ns)]
+        counter = [0]
+
+        def full_step(i):
+            # step i runs on stream i % ns: consecutive batches overlap, so one batch's argmin
+            # tail and launch gap hide under the next batch's scoring (the steps are independent)
+            lane = i % ns
+            first = (i * world + rank) * B  # globally unique candidate ids
+            with torch.cuda.stream(streams[lane]):
+                step(first, local_best[lane], lane, streams[lane])
+                if world > 1:
+                    dist.all_gather_into_tensor(gathered[lane], local_best[lane])
+                    S.reduce_best_device(gathered[lane], gbest[lane], stream=streams[lane])
+
+        def run_steps(k):
+            for _ in range(k):
+                full_step(counter[0])
+                counter[0] += 1
+
+    run_steps(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        full_step(args.warmup + i)
+    run_steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -267,7 +315,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (on-device Philox candidates around a linear init spline)",
-            "config": dict(meta, streams=ns,
+            "config": dict(meta, streams=ns, launch=("native executor, %d steps/call" % args.chunk)
+                           if native else "eager",
                            parallelism="dp%d (candidate shards, RCCL all-gather argmin)" % world),
             "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach_gbs / HBM_PEAK_GBS, "traffic": None,

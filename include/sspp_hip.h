@@ -185,10 +185,23 @@ int sspp_job_info(const sspp_job* job, int* lanes_per_candidate, int* candidates
                   int* block_threads, size_t* lds_bytes);
 void sspp_job_free(sspp_job* job);
 
+/* ---- step executor: a planning loop's back-to-back batches in one call ----
+ * Enqueues nsteps independent SamplingPathPlanner batches (sampleWithNoise + checkCollision +
+ * computeArcLength + findBestPath each, include/sspp.h:194-225), step i on branch i % nbranch:
+ * jobs[b] (distinct jobs: each owns its argmin counters), streams[b], scratch outputs
+ * d_arc[b] [B] / d_feasible[b] [B]; candidate ids [first_id + i * step_stride, ... + B);
+ * step i's argmin record to d_best[i] (nullable).  Asynchronous.                          */
+int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void* const* streams, int64_t B,
+                            int nsteps, int64_t first_id, int64_t step_stride,
+                            double* const* d_arc, uint8_t* const* d_feasible, sspp_best* d_best);
+
 /* ---- multi-GPU helpers: reduce gathered per-rank results (lowest cost, lowest id) ---- */
 int sspp_best_reduce(const sspp_best* parts, int n, sspp_best* out);          /* host */
 int sspp_best_reduce_device(const sspp_best* d_parts, int n, sspp_best* d_out,
                             void* stream);                                    /* device, async */
+/* G steps gathered from R ranks: d_parts [R][G] -> d_out [G] (device, async)              */
+int sspp_best_reduce_steps(const sspp_best* d_parts, int R, int G, sspp_best* d_out,
+                           void* stream);
 
 /* ---- host-synchronous conveniences (host buffers in/out; used by the _sspp drop-in) ----
  * sspp_plan_sspp  <- SamplingPathPlanner::plan (include/sspp.h:194-225) in one call:

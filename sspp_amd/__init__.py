@@ -4,7 +4,6 @@ Product layout:
   csrc/              HIP kernels (gfx950) + C ABI (include/sspp_hip.h) + MJCF loader
   lib/               built libsspp_hip.so (in-tree)
   runtime.py         Model / Scene / SsppJob / TspJob over the C ABI
-  planner.py         SamplingPathPlanner{3,6,7,9} / TaskSpacePlanner host mirrors
   BSplines.py, CubicPath.py   reference operator API (sspp/BSplines.py, sspp/CubicPath.py)
   scenes/            collision-only MJCF scenes derived from the reference's mjcf/
 """
@@ -13,9 +12,10 @@ import os
 SCENE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
 
 from ._lib import SsppError  # noqa: E402
-from .runtime import (DEFAULT_SEED, Model, Scene, SsppJob, TspJob, best_tensor,  # noqa: E402
-                      decode_best, device_count, interpolate, reduce_best,
-                      reduce_best_device, spline_eval)
+from .runtime import (DEFAULT_SEED, Model, Scene, SsppJob, SsppSteps, TspJob,  # noqa: E402
+                      best_tensor, decode_best, device_count, interpolate, reduce_best,
+                      reduce_best_device, reduce_best_steps, spline_eval)
 
 __all__ = ["SsppError", "Model", "Scene", "SsppJob", "TspJob", "interpolate", "spline_eval",
-           "best_tensor", "decode_best", "reduce_best", "reduce_best_device", "device_count", "DEFAULT_SEED", "SCENE_DIR"]
+           "best_tensor", "decode_best", "reduce_best", "reduce_best_device", "reduce_best_steps",
+           "SsppSteps", "device_count", "DEFAULT_SEED", "SCENE_DIR"]

@@ -692,6 +692,320 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
     finish_batch(bb, part, sync, best);
 }
 
+// ================================================================ coarse-to-fine feasibility
+// k_sspp_c2f: SamplingPathPlanner scoring, workgroup = CPB candidates (CPB = 256 / G1).
+//
+// checkCollision (include/sspp.h:132-150) stops at the first waypoint in contact, so the result
+// is an OR over waypoints and pairs; the order in which they are examined cannot change it.
+// An infeasible candidate is typically in contact over a long stretch of its path (robocrane,
+// config 2: ~55 of 129 waypoints), so a handful of well-spread waypoints finds almost all of
+// them.  The host orders the W+1 collision waypoints breadth-first by interval bisection
+// (ord table); then per workgroup:
+//   phase 1  G1 lanes per candidate test the first G1 waypoints of that order; a candidate's
+//            lanes leave the pair loop together at the first pair any of them touches
+//            (ballot over the candidate's lane group);
+//   phase 2  the survivors (few: the feasible ones plus the rare misses) are compacted in LDS
+//            and their remaining waypoints spread over all 256 lanes; a lane group that finds
+//            a contact clears the candidate's LDS flag, which stops its other lanes;
+//   phase 3  arc length for every candidate, in passes of 256/LPC candidates that keep the
+//            canonical reduction order of oracle/sspp_oracle.c::or_canon_sum;
+//   phase 4  block argmin + the fused batch argmin (finish_batch).
+// Sampling (sampleWithNoise, include/sspp.h:114-130) runs in the prologue: one Box-Muller pair
+// per thread.
+struct SsppC2F {
+    KScene sc;
+    int has_scene;
+    int ablate;
+    int insample;
+    int p, n, W;
+    double sigma;
+    unsigned long long seed;
+    long long first_id, B;
+    int g1, cpb;   // phase-1 lanes per candidate (divides 64), candidates per workgroup
+    int npts, n1;  // collision waypoints per candidate (W+1), phase-1 waypoints (<= g1)
+    int lpc;       // canonical lanes of the arc-length sum (or_lanes_for(W-1))
+};
+
+// Hull mask of one candidate for a lane group of G1 lanes (lane l of group wg in its wave):
+// pairs k = l, l+G1, ... tested one per lane, then a ballot; every lane of the group gets the
+// group's mask.
+template <int D, int NM>
+__device__ __forceinline__ unsigned long long group_hull_mask(const double* ctrl, int n, int npairs,
+                                                              cpair_t pairs, cgeom_t geoms,
+                                                              cmover_t movers, int g1, int l,
+                                                              int wg) {
+    double lo[NM][3], hi[NM][3];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int col = 7 * m + d;
+            if (col < D) {
+                double a = ctrl[col], b = ctrl[col];
+                for (int j = 1; j < n; ++j) {
+                    const double v = ctrl[j * D + col];
+                    a = v < a ? v : a;
+                    b = v > b ? v : b;
+                }
+                lo[m][d] = a; hi[m][d] = b;
+            } else {
+                lo[m][d] = hi[m][d] = (double)movers[m].qpos0[d];
+            }
+        }
+    }
+    const unsigned long long low = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
+    unsigned long long mask = 0ull;
+    const int lim = npairs < 64 ? npairs : 64;
+    for (int base = 0; base < lim; base += g1) {
+        const int k = base + l;
+        bool act = false;
+        if (k < lim) {
+            const DPair pr = load_pair(pairs + k);
+            const DGeom G = load_geom(geoms + pr.gm);
+            const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
+            act = pair_may_touch(pr, G, lo[m], hi[m]);
+        }
+        const unsigned long long b = __ballot(act);
+        mask |= ((b >> (wg * g1)) & low) << base;
+    }
+    if (npairs > 64) mask = ~0ull;
+    return mask;
+}
+
+// Pair loop of one waypoint per lane.  All 64 lanes run the (wave-uniform) loop; `live` lanes
+// test the pairs of their own mask.  gbits = the lanes of this lane's candidate within the
+// wave: when any of them touches, all of them stop (returns true for the group).  flag: the
+// candidate's LDS feasibility flag (phase 2), polled so lanes in other waves stop too.
+template <int D, int NM, bool ONEGEOM>
+__device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned long long mymask,
+                                           unsigned long long umask, unsigned long long gbits,
+                                           int* flag, const KScene& sc, const SceneT& T) {
+    const cgeom_t geoms = (cgeom_t)T.geoms;
+    const cpair_t pairs = (cpair_t)T.pairs;
+    double mp[NM][3], mR[NM][9];
+    mover_poses<D, NM, 0>(q, (cmover_t)T.movers, mp, mR);
+    int cur = -1;
+    double gp[3], gmat[9];
+    DGeom G;
+    if (ONEGEOM) {
+        cur = pairs[0].gm;
+        G = load_geom(geoms + cur);
+        geom_pose(mp[0], mR[0], G, gp, gmat);
+    }
+    bool ghit = false;
+    const int np = sc.npairs;
+    for (int k = 0; k < np; ++k) {
+        if (k < 64) {
+            const unsigned long long rest = umask >> k;
+            if (rest == 0ull) break;
+            k += __builtin_ctzll(rest);
+            if (k >= np) break;
+        }
+        const DPair pr = load_pair(pairs + k);
+        if (!ONEGEOM && pr.gm != cur) {
+            cur = pr.gm;
+            G = load_geom(geoms + cur);
+            const bool second = NM > 1 && G.mover == 1;
+            geom_pose(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp, gmat);
+        }
+        int nc = 0;
+        if (live && (k >= 64 || ((mymask >> k) & 1ull))) {
+            double op_[3], om_[9];
+            const double* op = pr.opos;
+            const double* om = pr.omat;
+            if (NM > 1 && pr.omover >= 0) {
+                const bool second = pr.omover == 1;
+                const double* R = second ? mR[NM - 1] : mR[0];
+                const double* P = second ? mp[NM - 1] : mp[0];
+                double t[3];
+                matvec3(R, pr.opos, t);
+                op_[0] = P[0] + t[0]; op_[1] = P[1] + t[1]; op_[2] = P[2] + t[2];
+                matmul3(R, pr.omat, om_);
+                op = op_; om = om_;
+            }
+            const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
+            const double rg = G.rbound, ro = pr.orbound;
+            bool near = true;
+            if (rg > 0.0 && ro > 0.0) {
+                const double thr = rg + ro + pr.margin;
+                near = !(dot3(dc, dc) > thr * thr);
+            }
+            if (near) {
+                int nd = 0;
+                const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
+                if (gfirst) nc = collide<false>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+                else nc = collide<false>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+            }
+        }
+        if (__ballot(nc > 0) & gbits) { ghit = true; live = false; }
+        if (flag && live && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+            live = false;
+        if (__ballot(live) == 0ull) break;
+    }
+    return ghit;
+}
+
+template <int D, int NM, int P, bool ONEGEOM>
+__global__ __launch_bounds__(kBlock) void k_sspp_c2f(
+    SsppC2F a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
+    const double* __restrict__ atab, const int* __restrict__ aspan,
+    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
+    const double* __restrict__ ctrl_in, const double* __restrict__ pert,
+    double* __restrict__ ctrl_out, double* __restrict__ arc, unsigned char* __restrict__ feasible,
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int P1 = P + 1;
+    const int tid = threadIdx.x, cpb = a.cpb, n = a.n, W = a.W, g1 = a.g1;
+    const int ndof = n * D;
+    const long long cand0 = (long long)blockIdx.x * cpb;
+    const int nvalid = (int)min((long long)cpb, a.B - cand0);
+    const long long first_id = a.first_id;
+    double* s_ctrl = smem;                                    // [cpb][n][D]
+    double* s_wsum = s_ctrl + cpb * ndof;                     // [4]
+    double* s_arc = s_wsum + kBlock / 64;                     // [cpb]
+    unsigned long long* s_mask = (unsigned long long*)(s_arc + cpb);  // [cpb]
+    int* s_feas = (int*)(s_mask + cpb);                       // [cpb]
+    int* s_surv = s_feas + cpb;                               // [cpb + 1] (last = count)
+
+    // ---- prologue: control points (+ sampleWithNoise) in LDS
+    if (ctrl_in) {
+        const double* src = ctrl_in + cand0 * ndof;
+        for (int e = tid; e < nvalid * ndof; e += kBlock) s_ctrl[e] = src[e];
+    } else {
+        const int npert = (n - 2 * P) * D;
+        const bool from_pert = !a.insample && !(a.ablate & 1);
+        for (int e = tid; e < cpb * ndof; e += kBlock) {
+            const int sl = e / ndof, r = e - sl * ndof;
+            const int k = r - P * D;
+            s_ctrl[e] = (from_pert && k >= 0 && k < npert && sl < nvalid)
+                            ? pert[(cand0 + sl) * npert + k]
+                            : init_ctrl[r];
+        }
+        if (a.insample && !(a.ablate & 1)) {
+            __syncthreads();
+            const int npairs = (npert + 1) >> 1;
+            for (int e = tid; e < nvalid * npairs; e += kBlock) {
+                const int sl = e / npairs, m = e - sl * npairs;
+                double z0, z1;
+                normal_pair(a.seed, (unsigned long long)(first_id + cand0 + sl), (unsigned)m, 0u, &z0, &z1);
+                double* c = s_ctrl + sl * ndof + P * D;
+                const int k0 = 2 * m, k1 = 2 * m + 1;
+                c[k0] = c[k0] + (a.sigma * z0) * limits[k0 % D];
+                if (k1 < npert) c[k1] = c[k1] + (a.sigma * z1) * limits[k1 % D];
+            }
+        }
+    }
+    __syncthreads();
+    if (ctrl_out) {
+        double* dst = ctrl_out + cand0 * ndof;
+        for (int e = tid; e < nvalid * ndof; e += kBlock) dst[e] = s_ctrl[e];
+    }
+
+    const SceneT TT = T;
+    const bool collide_on = a.has_scene && !(a.ablate & 2);
+    // ---- phase 1: G1 lanes per candidate, first n1 waypoints of the coarse-to-fine order
+    {
+        const int g = tid / g1, l = tid - g * g1, wg = (tid & 63) / g1;
+        const unsigned long long low = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
+        const unsigned long long gbits = low << (wg * g1);
+        const bool valid = g < nvalid;
+        const double* myc = s_ctrl + (valid ? g : 0) * ndof;
+        bool ghit = false;
+        if (collide_on) {
+            const unsigned long long mymask = group_hull_mask<D, NM>(
+                myc, n, a.sc.npairs, (cpair_t)TT.pairs, (cgeom_t)TT.geoms, (cmover_t)TT.movers, g1, l, wg);
+            // union over the wave's groups (wave-uniform)
+            unsigned long long umask = 0ull;
+            for (int w = 0; w < 64; w += g1) umask |= __shfl(mymask, w, 64);
+            if (l == 0) s_mask[g] = mymask;
+            const bool live = valid && l < a.n1 && !a.sc.static_block;
+            double q[D];
+            const int row = l < a.npts ? l : 0;
+            eval_pt<D, P>(myc, otab + row * P1, ospan[row], q);
+            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mymask, umask, gbits, nullptr, a.sc, TT);
+        }
+        if (l == 0) s_feas[g] = valid && !ghit && !(collide_on && a.sc.static_block);
+    }
+    __syncthreads();
+    // ---- phase 2: survivors' remaining waypoints over the whole workgroup
+    const int R = a.npts - a.n1;
+    if (collide_on && R > 0) {
+        if (tid == 0) {
+            int ns = 0;
+            for (int s = 0; s < nvalid; ++s)
+                if (s_feas[s]) s_surv[ns++] = s;
+            s_surv[cpb] = ns;
+        }
+        __syncthreads();
+        const int ns = s_surv[cpb];
+        unsigned long long umask = 0ull;
+        for (int i = 0; i < ns; ++i) umask |= s_mask[s_surv[i]];
+        const int items = ns * R;
+        for (int base = 0; base < items; base += kBlock) {  // workgroup-uniform trip count
+            const int it = base + tid;
+            bool live = it < items;
+            const int si = live ? it / R : 0;
+            const int s = s_surv[si];
+            const int j = a.n1 + (live ? it - si * R : 0);
+            live = live && __hip_atomic_load(s_feas + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+            // lanes of this wave that work on the same survivor
+            const int wave_it0 = base + (tid & ~63);
+            int lo = si * R - wave_it0, hi = (si + 1) * R - wave_it0;
+            lo = lo < 0 ? 0 : lo;
+            hi = hi > 64 ? 64 : hi;
+            unsigned long long gb = 0ull;
+            if (it < items && hi > lo) gb = (hi - lo >= 64) ? ~0ull : (((1ull << (hi - lo)) - 1ull) << lo);
+            double q[D];
+            eval_pt<D, P>(s_ctrl + s * ndof, otab + j * P1, ospan[j], q);
+            const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s], umask, gb, s_feas + s, a.sc, TT);
+            if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    // ---- phase 3: arc length, canonical order (lanes = a.lpc per candidate)
+    const int lpc = a.lpc, cpp = kBlock / lpc;
+    const int pc = tid / lpc, vl = tid - pc * lpc;
+    for (int s0 = 0; s0 < cpb; s0 += cpp) {  // workgroup-uniform
+        const int s = s0 + pc;
+        double acc = 0.0;
+        if (pc < cpp && s < nvalid && !(a.ablate & 4)) {
+            const double* myc = s_ctrl + s * ndof;
+            for (int jj = vl; jj < W - 1; jj += lpc) {
+                const int i = jj + 1;
+                double q[D], q2[D];
+                eval_pt<D, P>(myc, atab + (i - 1) * P1, aspan[i - 1], q);
+                eval_pt<D, P>(myc, atab + i * P1, aspan[i], q2);
+                acc = acc + dist_nd<D>(q, q2);
+            }
+        }
+        acc = wave_sum(acc);
+        __syncthreads();
+        if ((tid & 63) == 0) s_wsum[tid >> 6] = acc;
+        __syncthreads();
+        if (vl == 0 && pc < cpp && s < nvalid) {
+            const int w0 = (pc * lpc) >> 6, nw = lpc >> 6;
+            double t = s_wsum[w0];
+            for (int w = 1; w < nw; ++w) t = t + s_wsum[w0 + w];
+            s_arc[s] = t;
+        }
+    }
+    __syncthreads();
+    if (tid < nvalid) {
+        const long long c = cand0 + tid;
+        arc[c] = s_arc[tid];
+        feasible[c] = (unsigned char)(s_feas[tid] != 0);
+    }
+    BlockBest bb;
+    if (tid == 0) {
+        bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
+        for (int s = 0; s < nvalid; ++s) {
+            if (!s_feas[s]) continue;
+            bb.count++;
+            if (s_arc[s] < bb.cost) { bb.cost = s_arc[s]; bb.idx = first_id + cand0 + s; }
+        }
+    }
+    finish_batch(bb, part, sync, best);
+}
+
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
 // tab: (cp+1) rows of 3 basis values at u = i * (1/cp); Minv: collocation inverse (n x n).
 template <int NM, bool ONEGEOM>
@@ -922,6 +1236,11 @@ struct sspp_job {
     double* d_pert = nullptr;  // sampler output: perturbed columns [max_batch][(n-2p)*D]
     int npert = 0;
     int insample = 0;          // sample inside the scoring kernel (SSPP_INSAMPLE=1)
+    // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
+    int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16;
+    size_t lds2 = 0;
+    double* d_otab = nullptr;  // collision rows in coarse-to-fine order
+    int* d_ospan = nullptr;
     ArgminSync* d_sync = nullptr;  // sharded arrival counters of the fused argmin
     double start[4], end[4], lo[4], hi[4];
     double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
@@ -1212,6 +1531,25 @@ static SceneT scene_t(const sspp_scene* s) {
     return t;
 }
 
+// Coarse-to-fine order of the collision waypoints 0..W: breadth-first interval bisection, so
+// every prefix is spread evenly over the path (k_sspp_c2f phase 1 tests a prefix).
+static std::vector<int> c2f_order(int W) {
+    std::vector<int> ord;
+    std::vector<std::pair<int, int>> cur{{0, W}}, next;
+    while (!cur.empty()) {
+        next.clear();
+        for (auto [lo, hi] : cur) {
+            if (lo > hi) continue;
+            const int mid = lo + (hi - lo) / 2;
+            ord.push_back(mid);
+            next.push_back({lo, mid - 1});
+            next.push_back({mid + 1, hi});
+        }
+        cur.swap(next);
+    }
+    return ord;
+}
+
 // Basis rows for a list of parameters (same A2.1/A2.2 code as the device header).
 static int upload_basis(const std::vector<double>& us, int p, const double* knots, int nknots,
                         double** d_tab, int** d_span) {
@@ -1267,7 +1605,26 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     }
     j->npert = (n - 2 * p) * D;
     if (j->npert < 0) j->npert = 0;
-    { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : 0; }
+    { const char* e = getenv("SSPP_KERNEL"); j->c2f = e ? atoi(e) != 0 : 1; }
+    { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : (j->c2f ? 1 : 0); }
+    {
+        const char* e = getenv("SSPP_G1");
+        int g1 = e ? atoi(e) : 16;
+        if (g1 != 4 && g1 != 8 && g1 != 16 && g1 != 32 && g1 != 64) g1 = 16;
+        j->g1 = g1;
+        j->cpb2 = kBlock / g1;
+        j->n1 = std::min(g1, W + 1);
+        std::vector<int> ord = c2f_order(W);
+        std::vector<double> uo;
+        for (int i : ord) uo.push_back((double)i / W);
+        if ((rc = upload_basis(uo, p, a->knots, j->nknots, &j->d_otab, &j->d_ospan))) {
+            sspp_job_free(j);
+            return rc;
+        }
+        j->lds2 = sizeof(double) * ((size_t)j->cpb2 * n * D + kBlock / 64 + j->cpb2) +
+                  sizeof(unsigned long long) * j->cpb2 + sizeof(int) * (2 * j->cpb2 + 1);
+        if (j->lds2 > 64 * 1024) j->c2f = 0;
+    }
     if (j->npert > 0 && hipMalloc((void**)&j->d_pert, sizeof(double) * (size_t)max_batch * j->npert) != hipSuccess) {
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc sampler buffer");
@@ -1303,6 +1660,42 @@ static hipError_t launch_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs&
                        scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
                        j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
     return hipGetLastError();
+}
+
+template <int D, int NM, int P>
+static hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                             hipStream_t st) {
+    const double* atab = j->d_tab + (size_t)(j->W + 1) * (P + 1);
+    const int* aspan = j->d_span + (j->W + 1);
+    if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
+        hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true>), dim3(nblk), dim3(kBlock), j->lds2, st, k,
+                           scene_t(j->scene), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
+                           o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((k_sspp_c2f<D, NM, P, false>), dim3(nblk), dim3(kBlock), j->lds2, st, k,
+                       scene_t(j->scene), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
+                       o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
+    return hipGetLastError();
+}
+
+template <int P>
+static hipError_t dispatch_c2f_p(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                                 hipStream_t st) {
+    if (j->nm == 2) {
+        if (j->D == 9) return launch_c2f<9, 2, P>(k, j, o, nblk, st);
+        return hipErrorInvalidValue;
+    }
+    switch (j->D) {
+        case 1: return launch_c2f<1, 1, P>(k, j, o, nblk, st);
+        case 2: return launch_c2f<2, 1, P>(k, j, o, nblk, st);
+        case 3: return launch_c2f<3, 1, P>(k, j, o, nblk, st);
+        case 4: return launch_c2f<4, 1, P>(k, j, o, nblk, st);
+        case 6: return launch_c2f<6, 1, P>(k, j, o, nblk, st);
+        case 7: return launch_c2f<7, 1, P>(k, j, o, nblk, st);
+        case 9: return launch_c2f<9, 1, P>(k, j, o, nblk, st);
+    }
+    return hipErrorInvalidValue;
 }
 
 template <int P>
@@ -1341,7 +1734,8 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     k.ablate = ablate;
     k.insample = j->insample;
     SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
-    const int nblk = (int)((B + j->cpb - 1) / j->cpb);
+    const int cpb = j->c2f ? j->cpb2 : j->cpb;
+    const int nblk = (int)((B + cpb - 1) / cpb);
     hipStream_t st = (hipStream_t)stream;
     if (!d_ctrl && j->npert > 0 && !j->insample) {  // sampleWithNoise over the whole chip
         const long long work = B * (long long)((j->npert + 1) / 2);
@@ -1351,7 +1745,18 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         hipError_t es = hipGetLastError();
         if (es != hipSuccess) return hip_fail(es, "k_sample_sspp launch");
     }
-    hipError_t e = j->p == 3 ? dispatch_sspp_p<3>(k, j, o, nblk, st) : dispatch_sspp_p<2>(k, j, o, nblk, st);
+    hipError_t e;
+    if (j->c2f) {
+        SsppC2F c{};
+        c.sc = k.sc; c.has_scene = k.has_scene; c.ablate = k.ablate; c.insample = j->insample;
+        c.p = j->p; c.n = j->n; c.W = j->W; c.sigma = j->sigma; c.seed = j->seed;
+        c.first_id = first_id; c.B = B;
+        c.g1 = j->g1; c.cpb = j->cpb2; c.npts = j->W + 1; c.n1 = j->n1;
+        c.lpc = lanes_for(j->W - 1);
+        e = j->p == 3 ? dispatch_c2f_p<3>(c, j, o, nblk, st) : dispatch_c2f_p<2>(c, j, o, nblk, st);
+    } else {
+        e = j->p == 3 ? dispatch_sspp_p<3>(k, j, o, nblk, st) : dispatch_sspp_p<2>(k, j, o, nblk, st);
+    }
     if (e != hipSuccess) return hip_fail(e, "k_sspp launch");
     return SSPP_OK;
 }
@@ -1478,6 +1883,8 @@ extern "C" void sspp_job_free(sspp_job* j) {
     for (double* p : {j->d_knots, j->d_tab, j->d_init, j->d_limits, j->d_Minv, j->d_mean, j->d_sigma})
         if (p) (void)hipFree(p);
     if (j->d_span) (void)hipFree(j->d_span);
+    if (j->d_otab) (void)hipFree(j->d_otab);
+    if (j->d_ospan) (void)hipFree(j->d_ospan);
     if (j->d_part) (void)hipFree(j->d_part);
     if (j->d_pert) (void)hipFree(j->d_pert);
     if (j->d_sync) (void)hipFree(j->d_sync);
@@ -1493,6 +1900,73 @@ extern "C" int sspp_best_reduce_device(const sspp_best* d_parts, int n, sspp_bes
                        reinterpret_cast<const BlockBest*>(d_parts), n, d_out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_argmin launch");
+    return SSPP_OK;
+}
+
+// ---------------------------------------------------------------- step enqueue (host executor)
+// A planning loop issues one small batch after another (4096 candidates = a few microseconds
+// of GPU work).  Steps are independent, so they are spread round robin over several HIP
+// streams and overlap on the chip; the host side of a step is one kernel launch issued from
+// this C++ loop (no per-step Python).  Measured on MI355X: hipGraph replays of the same steps
+// ran 1.5-4x slower than this (graph kernel nodes did not overlap), so there is no graph path.
+namespace {
+__global__ __launch_bounds__(64) void k_argmin_steps(const BlockBest* __restrict__ parts, int R,
+                                                     int G, sspp_best* out) {
+    // block g: lexicographic (cost, id) reduction of parts[r * G + g], r < R (one wave)
+    const int g = blockIdx.x;
+    double bc = INFINITY;
+    long long bi = -1, cnt = 0;
+    for (int r = threadIdx.x; r < R; r += 64) {
+        const BlockBest b = parts[(long long)r * G + g];
+        cnt += b.count;
+        if (better(b.cost, b.idx, bc, bi)) { bc = b.cost; bi = b.idx; }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double oc = __shfl_xor(bc, off, 64);
+        const long long oi = __shfl_xor(bi, off, 64);
+        cnt += __shfl_xor(cnt, off, 64);
+        if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
+    }
+    if (threadIdx.x == 0) {
+        out[g].cost = bi < 0 ? INFINITY : bc;
+        out[g].index = bi;
+        out[g].count = cnt;
+        out[g].reserved = 0;
+    }
+}
+}  // namespace
+
+extern "C" int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void* const* streams,
+                                       int64_t B, int nsteps, int64_t first_id,
+                                       int64_t step_stride, double* const* d_arc,
+                                       uint8_t* const* d_feasible, sspp_best* d_best) {
+    sspp::clear_error();
+    if (!jobs || !streams || !d_arc || !d_feasible || nbranch < 1 || nsteps < 0 || B < 1)
+        return sspp::set_error(SSPP_E_INVAL, "sspp_steps_enqueue_sspp: bad argument");
+    for (int b = 0; b < nbranch; ++b) {
+        if (!jobs[b] || jobs[b]->kind != 0 || !d_arc[b] || !d_feasible[b])
+            return sspp::set_error(SSPP_E_INVAL, "sspp_steps_enqueue_sspp: bad branch");
+        for (int c = 0; c < b; ++c)
+            if (jobs[c] == jobs[b]) return sspp::set_error(SSPP_E_INVAL, "branches need distinct jobs");
+    }
+    for (int i = 0; i < nsteps; ++i) {
+        const int b = i % nbranch;
+        const int rc = run_sspp(jobs[b], nullptr, first_id + (int64_t)i * step_stride, B, d_arc[b],
+                                d_feasible[b], nullptr, d_best ? d_best + i : nullptr, streams[b]);
+        if (rc != SSPP_OK) return rc;
+    }
+    return SSPP_OK;
+}
+
+extern "C" int sspp_best_reduce_steps(const sspp_best* d_parts, int R, int G, sspp_best* d_out,
+                                      void* stream) {
+    sspp::clear_error();
+    if (!d_parts || !d_out || R < 1 || G < 1) return sspp::set_error(SSPP_E_INVAL, "sspp_best_reduce_steps: bad argument");
+    hipLaunchKernelGGL(k_argmin_steps, dim3(G), dim3(64), 0, (hipStream_t)stream,
+                       reinterpret_cast<const BlockBest*>(d_parts), R, G, d_out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_argmin_steps launch");
     return SSPP_OK;
 }
 

@@ -284,11 +284,39 @@ class TspJob(_Job):
                                             _ptr(best), _stream(stream)), "tsp score_vias")
 
 
+class SsppSteps:
+    """Back-to-back SamplingPathPlanner batches enqueued by the C++ step executor
+    (sspp_steps_enqueue_sspp): step i runs on branch i % len(jobs) — jobs[b] with streams[b] and
+    its scratch arc/feasible buffers — scoring ids first_id + i * step_stride + [0, B)."""
+
+    def __init__(self, jobs, streams, B, arc_bufs, feas_bufs):
+        nb = len(jobs)
+        self._keep = (jobs, streams, arc_bufs, feas_bufs)
+        self._J = (C.c_void_p * nb)(*[j._h for j in jobs])
+        self._S = (C.c_void_p * nb)(*[_stream(s).value for s in streams])
+        self._A = (C.c_void_p * nb)(*[_ptr(a).value for a in arc_bufs])
+        self._F = (C.c_void_p * nb)(*[_ptr(f).value for f in feas_bufs])
+        self.nb, self.B = nb, int(B)
+
+    def enqueue(self, nsteps, first_id, step_stride, best=None):
+        """best: None or an (nsteps, 4) int64 device tensor for the per-step argmin records."""
+        check(lib().sspp_steps_enqueue_sspp(self._J, self.nb, self._S, self.B, int(nsteps),
+                                            int(first_id), int(step_stride), self._A, self._F,
+                                            _ptr(best)), "steps enqueue")
+
+
+def reduce_best_steps(parts, out, stream=None):
+    """parts: (R, G, 4) int64 device tensor of per-rank step records -> out (G, 4)."""
+    R, G = parts.shape[0], parts.shape[1]
+    check(lib().sspp_best_reduce_steps(_ptr(parts), int(R), int(G), _ptr(out), _stream(stream)),
+          "reduce_best_steps")
+
+
 def device_count():
     n = C.c_int()
     rc = lib().sspp_device_count(C.byref(n))
     return n.value if rc == 0 else 0
 
 
-__all__ = ["Model", "Scene", "SsppJob", "TspJob", "interpolate", "spline_eval", "best_tensor",
+__all__ = ["Model", "Scene", "SsppJob", "TspJob", "SsppSteps", "reduce_best_steps", "interpolate", "spline_eval", "best_tensor",
            "decode_best", "reduce_best", "reduce_best_device", "device_count", "DEFAULT_SEED", "math"]

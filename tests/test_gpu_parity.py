@@ -55,9 +55,17 @@ def run_sspp(job, B, first=0, with_ctrl=True):
     return res
 
 
+# scoring kernels: (SSPP_KERNEL, SSPP_G1) — coarse-to-fine k_sspp_c2f with several phase-1
+# lane-group sizes, and the one-waypoint-per-lane k_sspp
+KERNELS = [("1", "16"), ("1", "4"), ("1", "64"), ("0", "16")]
+
+
+@pytest.mark.parametrize("kernel,g1", KERNELS)
 @pytest.mark.parametrize("B,W", [(4096, 128), (257, 128), (1, 128), (300, 50), (100, 256), (64, 2)])
-def test_robocrane_sample_score_matches_oracle(robocrane, B, W):
+def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g1, B, W):
     import sspp_amd as S
+    monkeypatch.setenv("SSPP_KERNEL", kernel)
+    monkeypatch.setenv("SSPP_G1", g1)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=0x5EED, max_batch=B)
@@ -88,10 +96,13 @@ def test_robocrane_config2_is_nontrivial(robocrane):
     assert 0 < nfeas < 4096, nfeas  # SURVEY config 2 (sigma 0.08): ~0.3% clear the brick stack
 
 
-def test_score_ctrl_mode_matches_oracle(robocrane):
+@pytest.mark.parametrize("kernel,g1", KERNELS)
+def test_score_ctrl_mode_matches_oracle(robocrane, monkeypatch, kernel, g1):
     """Caller-supplied splines (checkCollision + computeArcLength on arbitrary ctrl)."""
     import sspp_amd as S
     import torch
+    monkeypatch.setenv("SSPP_KERNEL", kernel)
+    monkeypatch.setenv("SSPP_G1", g1)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     rng = np.random.default_rng(7)
@@ -164,9 +175,12 @@ def test_stacking_tsp_matches_oracle(cuda, B, cp, K):
         assert 0 < st.sum() < B  # both outcomes present
 
 
-def test_planner_scene_sspp(cuda):
+@pytest.mark.parametrize("kernel,g1", KERNELS)
+def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1):
     """planner.xml: block1 (free) vs static wall/block2, 7-DoF window, path through the wall."""
     import sspp_amd as S
+    monkeypatch.setenv("SSPP_KERNEL", kernel)
+    monkeypatch.setenv("SSPP_G1", g1)
     model = S.Model(PLANNER)
     scene = S.Scene(model, 0, 7)
     oscene = O.Scene(mjcf_ref.load(PLANNER), 0, 7)
@@ -182,8 +196,9 @@ def test_planner_scene_sspp(cuda):
     assert r["best"][1] == O.argmin(arc_o, feas_o)[0]
 
 
+@pytest.mark.parametrize("kernel", ["0", "1"])
 @pytest.mark.parametrize("insample", [0, 1])
-def test_fused_argmin_back_to_back(robocrane, monkeypatch, insample):
+def test_fused_argmin_back_to_back(robocrane, monkeypatch, insample, kernel):
     """100 batches queued back to back: each launch's in-kernel argmin (sharded arrival
     counters, re-armed by the last workgroup) must equal the argmin of that batch's outputs.
     insample=1 draws the candidates inside the scoring kernel: same candidates, same results."""
@@ -191,6 +206,7 @@ def test_fused_argmin_back_to_back(robocrane, monkeypatch, insample):
     import torch
     _, scene, _ = robocrane
     monkeypatch.setenv("SSPP_INSAMPLE", str(insample))
+    monkeypatch.setenv("SSPP_KERNEL", kernel)
     knots, ctrl0 = linear_init(START7, END7, 10)
     B, steps = 4096, 100
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.12, np.ones(7), 128, max_batch=B)
@@ -211,3 +227,51 @@ def test_fused_argmin_back_to_back(robocrane, monkeypatch, insample):
     # same candidates as the separate sampler: compare one batch against the oracle sampler
     r = run_sspp(job, 257, first=77)
     assert np.abs(r["ctrl"] - O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 0x5EED, 77, 257)).max() <= 1e-12
+
+
+def test_step_executor_matches_eager(robocrane):
+    """C++ step executor: G batches round robin over 3 streams; every step's argmin record
+    equals a single eager launch on the same candidate ids."""
+    import sspp_amd as S
+    import torch
+    _, scene, _ = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    B, G, stride, first = 4096, 7, 2 * 4096, 5 * 4096
+    jobs = [S.SsppJob(scene, knots, 3, ctrl0, 0.12, np.ones(7), 128, max_batch=B) for _ in range(3)]
+    bufs = [j.alloc(B) for j in jobs]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(2)]
+    ex = S.SsppSteps(jobs, streams, B, [b["arc"] for b in bufs], [b["feasible"] for b in bufs])
+    best = torch.zeros((G, 4), dtype=torch.int64, device="cuda")
+    ex.enqueue(G, first, stride, best)
+    torch.cuda.synchronize()
+    got = best.cpu()
+    ref = jobs[0].alloc(B)
+    for i in range(G):
+        jobs[0].sample_score(first + i * stride, B, ref["arc"], ref["feasible"], ref["best"])
+        torch.cuda.synchronize()
+        assert S.decode_best(got[i]) == S.decode_best(ref["best"]), i
+
+
+def test_reduce_best_steps(cuda):
+    import sspp_amd as S
+    import torch
+    rng = np.random.default_rng(3)
+    R, G = 3, 9
+    recs = np.zeros((R, G, 4), np.int64)
+    for r in range(R):
+        for g in range(G):
+            c = rng.choice([0.5, 0.25, np.inf])
+            idx = -1 if np.isinf(c) else int(rng.integers(0, 100))
+            recs[r, g, 0] = np.array([c]).view(np.int64)[0]
+            recs[r, g, 1] = idx
+            recs[r, g, 2] = int(rng.integers(0, 5))
+    out = torch.zeros((G, 4), dtype=torch.int64, device="cuda")
+    S.reduce_best_steps(torch.from_numpy(recs).cuda(), out)
+    torch.cuda.synchronize()
+    out = out.cpu().numpy()
+    for g in range(G):
+        cands = [(recs[r, g, :1].view(np.float64)[0], recs[r, g, 1]) for r in range(R) if recs[r, g, 1] >= 0]
+        want = min(cands) if cands else (np.inf, -1)
+        cost, idx, cnt = S.decode_best(out[g])
+        assert (cost, idx) == (float(want[0]), int(want[1]))
+        assert cnt == int(recs[:, g, 2].sum())

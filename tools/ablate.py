@@ -81,5 +81,5 @@ for i in range(200):
     run(i, o["best"])
 torch.cuda.synchronize()
 res["one_stream_wall"] = (time.perf_counter() - t0) / 200 * 1e6
-print(json.dumps(dict(config=cfg, lib=os.path.basename(os.environ.get("SSPP_LIB_PATH", "default")),
+print(json.dumps(dict(env={k: v for k, v in os.environ.items() if k.startswith("SSPP_")}, config=cfg, lib=os.path.basename(os.environ.get("SSPP_LIB_PATH", "default")),
                       ablate=int(os.environ.get("SSPP_ABLATE", "0")), B=B, us=res, feasible=feas())))
