@@ -53,7 +53,10 @@ def parse():
     ap.add_argument("--mode", default="native", choices=["native", "eager"],
                     help="native: the C++ step executor enqueues --chunk steps per call "
                          "(robocrane); eager: one Python-level launch per step")
-    ap.add_argument("--chunk", type=int, default=50)
+    ap.add_argument("--chunk", type=int, default=64)
+    ap.add_argument("--steps-per-launch", type=int, default=1,
+                    help="native mode: independent steps (each its own B candidates, outputs and "
+                         "argmin) grouped into one kernel launch")
     return ap.parse_args()
 
 
@@ -79,8 +82,11 @@ def setup_robocrane(args, device):
     def kernel_only(first_id):
         job.sample_score(first_id, B, bufs[0]["arc"], bufs[0]["feasible"], None)
 
-    def make_executor(streams):
-        return S.SsppSteps(jobs, streams, B, [b["arc"] for b in bufs], [b["feasible"] for b in bufs])
+    def make_executor(streams, spl):
+        import torch
+        arcs = [torch.empty(spl * B, dtype=torch.float64, device=device) for _ in jobs]
+        feas = [torch.empty(spl * B, dtype=torch.uint8, device=device) for _ in jobs]
+        return S.SsppSteps(jobs, streams, B, arcs, feas, steps_per_launch=spl)
 
     n_, D, p = 10, 7, 3
     # SURVEY §8(d) algorithmic work per candidate
@@ -216,7 +222,7 @@ def main():
         G = max(1, args.chunk)
         main = torch.cuda.current_stream()
         streams = [main] + [torch.cuda.Stream(device) for _ in range(ns - 1)]
-        ex = ctx["make_executor"](streams)
+        ex = ctx["make_executor"](streams, args.steps_per_launch)
         best = torch.zeros((G, 4), dtype=torch.int64, device=device)
         gbufs = {}
         counter = [0]
@@ -315,7 +321,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (on-device Philox candidates around a linear init spline)",
-            "config": dict(meta, streams=ns, launch=("native executor, %d steps/call" % args.chunk)
+            "config": dict(meta, streams=ns, launch=("native executor, %d steps/call, %d steps/launch"
+                                                     % (args.chunk, args.steps_per_launch))
                            if native else "eager",
                            parallelism="dp%d (candidate shards, RCCL all-gather argmin)" % world),
             "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -186,14 +186,18 @@ int sspp_job_info(const sspp_job* job, int* lanes_per_candidate, int* candidates
 void sspp_job_free(sspp_job* job);
 
 /* ---- step executor: a planning loop's back-to-back batches in one call ----
- * Enqueues nsteps independent SamplingPathPlanner batches (sampleWithNoise + checkCollision +
- * computeArcLength + findBestPath each, include/sspp.h:194-225), step i on branch i % nbranch:
- * jobs[b] (distinct jobs: each owns its argmin counters), streams[b], scratch outputs
- * d_arc[b] [B] / d_feasible[b] [B]; candidate ids [first_id + i * step_stride, ... + B);
- * step i's argmin record to d_best[i] (nullable).  Asynchronous.                          */
+ * Enqueues nsteps independent SamplingPathPlanner steps (each = one plan() batch of B
+ * candidates: sampleWithNoise + checkCollision + computeArcLength + findBestPath,
+ * include/sspp.h:194-225).  Step i scores candidate ids [first_id + i * step_stride, ... + B)
+ * and writes its own argmin record to d_best[i] (nullable).  Steps are grouped
+ * steps_per_launch (1..16) to a kernel launch — each step keeps its own workgroups, outputs and
+ * argmin — and launch l goes to branch l % nbranch: jobs[b] (distinct jobs: each owns its argmin
+ * counters), streams[b], scratch outputs d_arc[b] / d_feasible[b] of steps_per_launch * B
+ * entries.  Asynchronous.                                                                  */
 int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void* const* streams, int64_t B,
-                            int nsteps, int64_t first_id, int64_t step_stride,
-                            double* const* d_arc, uint8_t* const* d_feasible, sspp_best* d_best);
+                            int nsteps, int steps_per_launch, int64_t first_id,
+                            int64_t step_stride, double* const* d_arc, uint8_t* const* d_feasible,
+                            sspp_best* d_best);
 
 /* ---- multi-GPU helpers: reduce gathered per-rank results (lowest cost, lowest id) ---- */
 int sspp_best_reduce(const sspp_best* parts, int n, sspp_best* out);          /* host */

@@ -783,6 +783,35 @@ int or_point_contacts(const or_scene* s, const double* q, int count_static, doub
     return ncon;
 }
 
+/* Analysis hook (tools/ only): contact count of every pair at q, in the scene's pair order
+ * (static pairs included), plus the pair's geoms.  Same FK and narrowphase as above. */
+int or_point_pair_contacts(const or_scene* s, const double* q, int* counts, int* g1_out, int* g2_out) {
+    int nb = s->nbody, ng = s->ngeom;
+    if (s->nq > 256 || nb > 64 || ng > 128) return -1;
+    double qpos[256], xpos[3 * 64], xquat[4 * 64], xmat[9 * 64], gxpos[3 * 128], gxmat[9 * 128];
+    set_qpos(s, q, qpos);
+    fk(s, qpos, xpos, xquat, xmat, gxpos, gxmat);
+    for (int k = 0; k < s->npair; ++k) {
+        const or_pair* pr = s->pairs + k;
+        int g1 = pr->g1, g2 = pr->g2;
+        if (g1_out) g1_out[k] = g1;
+        if (g2_out) g2_out[k] = g2;
+        counts[k] = 0;
+        double dc[3] = {gxpos[3 * g2] - gxpos[3 * g1], gxpos[3 * g2 + 1] - gxpos[3 * g1 + 1],
+                        gxpos[3 * g2 + 2] - gxpos[3 * g1 + 2]};
+        double r1 = s->rbound[g1], r2 = s->rbound[g2];
+        if (r1 > 0.0 && r2 > 0.0) {
+            double thr = r1 + r2 + pr->margin;
+            if (dot3(dc, dc) > thr * thr) continue;
+        }
+        int nd = 0;
+        counts[k] = collide(s->geom_type[g1], gxpos + 3 * g1, gxmat + 9 * g1, s->geom_size + 3 * g1,
+                            s->geom_type[g2], gxpos + 3 * g2, gxmat + 9 * g2, s->geom_size + 3 * g2,
+                            pr->margin, &nd);
+    }
+    return s->npair;
+}
+
 /* ------------------------------------------------------------------ reductions
  * Canonical order (shared with the GPU kernels): `lanes` lanes, lane l accumulates
  * x[l], x[l+lanes], ... sequentially from 0.0; each 64-lane wave reduces its lanes by

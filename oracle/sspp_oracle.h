@@ -103,6 +103,8 @@ void   or_sample_tsp(const double* mean /* [K][4] */, const double* sigma /* [K]
    that are counted in this mode); deep_cost receives the Collision.h cost. */
 int    or_point_contacts(const or_scene* s, const double* q, int count_static,
                          double* deep_cost, int* n_deep);
+/* analysis hook: per-pair contact counts at q (counts/g1/g2 [npair]); returns npair */
+int    or_point_pair_contacts(const or_scene* s, const double* q, int* counts, int* g1, int* g2);
 /* geom world poses after FK for q (test hook). xpos [ngeom][3], xmat [ngeom][9] */
 void   or_fk_geoms(const or_scene* s, const double* q, double* xpos, double* xmat);
 

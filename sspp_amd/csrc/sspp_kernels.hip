@@ -35,6 +35,7 @@ constexpr int kBlock = 256;
 #define SSPP_SCORE_WAVES_PER_EU 4  // min waves per SIMD (4 -> <=128 VGPRs; measured best on gfx950)
 #endif
 constexpr int kMaxMovers = 2;
+constexpr int kMaxSteps = 16;  // steps per launch (k_sspp_c2f)
 
 struct KScene {
     int npairs;
@@ -427,11 +428,12 @@ __device__ __forceinline__ BlockBest ld_rec(BlockBest* p) {
     return b;
 }
 
-// block-wide lexicographic reduction of records idx0 + stride*i, i < n (all threads call)
+// block-wide lexicographic reduction of records idx0 + stride*i, i < n (all NT threads call)
+template <int NT = kBlock>
 __device__ BlockBest reduce_recs(BlockBest* recs, int idx0, int stride, int n, double* scratch) {
     double bc = INFINITY;
     long long bi = -1, cnt = 0;
-    for (int i = threadIdx.x; i < n; i += kBlock) {
+    for (int i = threadIdx.x; i < n; i += NT) {
         const BlockBest b = ld_rec(recs + idx0 + (long long)stride * i);
         cnt += b.count;
         if (better(b.cost, b.idx, bc, bi)) { bc = b.cost; bi = b.idx; }
@@ -456,7 +458,7 @@ __device__ BlockBest reduce_recs(BlockBest* recs, int idx0, int stride, int n, d
     r.idx = __double_as_longlong(scratch[1]);
     r.count = __double_as_longlong(scratch[2]);
     r.pad = 0;
-    for (int k = 1; k < kBlock / 64; ++k) {
+    for (int k = 1; k < NT / 64; ++k) {
         const double oc = scratch[3 * k];
         const long long oi = __double_as_longlong(scratch[3 * k + 1]);
         r.count += __double_as_longlong(scratch[3 * k + 2]);
@@ -465,11 +467,13 @@ __device__ BlockBest reduce_recs(BlockBest* recs, int idx0, int stride, int n, d
     return r;
 }
 
-// All threads of the workgroup call this after thread 0 filled `bb`.
+// All NT threads of the workgroup call this after thread 0 filled `bb`.
+template <int NT = kBlock>
 __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, ArgminSync* sync,
-                             sspp_best* out) {
+                             sspp_best* out, int nblk = -1, int b = -1) {
     __shared__ double scratch[16];
-    const int nblk = gridDim.x, b = blockIdx.x, sh = b & 7;
+    if (nblk < 0) { nblk = gridDim.x; b = blockIdx.x; }
+    const int sh = b & 7;
     const int nsh = nblk < 8 ? nblk : 8;
     int* flag = reinterpret_cast<int*>(scratch + 14);
     if (!out) {
@@ -485,7 +489,7 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
     }
     __syncthreads();
     if (!*flag) return;
-    const BlockBest shard_best = reduce_recs(part, sh, 8, (nblk - sh + 7) >> 3, scratch);
+    const BlockBest shard_best = reduce_recs<NT>(part, sh, 8, (nblk - sh + 7) >> 3, scratch);
     if (threadIdx.x == 0) {
         st_rec(sync->rec + sh, shard_best);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -494,7 +498,7 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
     }
     __syncthreads();
     if (!*flag) return;
-    const BlockBest r = reduce_recs(sync->rec, 0, 1, nsh, scratch);
+    const BlockBest r = reduce_recs<NT>(sync->rec, 0, 1, nsh, scratch);
     if (threadIdx.x == 0) {
         out->cost = r.idx < 0 ? INFINITY : r.cost;
         out->index = r.idx;
@@ -724,53 +728,12 @@ struct SsppC2F {
     int g1, cpb;   // phase-1 lanes per candidate (divides 64), candidates per workgroup
     int npts, n1;  // collision waypoints per candidate (W+1), phase-1 waypoints (<= g1)
     int lpc;       // canonical lanes of the arc-length sum (or_lanes_for(W-1))
+    // several independent steps (batches) per launch: workgroup b belongs to step b / nblk_step;
+    // step s scores ids first_id + s * step_stride + [0, B) into arc/feasible + s * B, its own
+    // argmin records / counters (part + s * nblk_step, sync + s) and best[s]
+    int nblk_step;
+    long long step_stride;
 };
-
-// Hull mask of one candidate for a lane group of G1 lanes (lane l of group wg in its wave):
-// pairs k = l, l+G1, ... tested one per lane, then a ballot; every lane of the group gets the
-// group's mask.
-template <int D, int NM>
-__device__ __forceinline__ unsigned long long group_hull_mask(const double* ctrl, int n, int npairs,
-                                                              cpair_t pairs, cgeom_t geoms,
-                                                              cmover_t movers, int g1, int l,
-                                                              int wg) {
-    double lo[NM][3], hi[NM][3];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const int col = 7 * m + d;
-            if (col < D) {
-                double a = ctrl[col], b = ctrl[col];
-                for (int j = 1; j < n; ++j) {
-                    const double v = ctrl[j * D + col];
-                    a = v < a ? v : a;
-                    b = v > b ? v : b;
-                }
-                lo[m][d] = a; hi[m][d] = b;
-            } else {
-                lo[m][d] = hi[m][d] = (double)movers[m].qpos0[d];
-            }
-        }
-    }
-    const unsigned long long low = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
-    unsigned long long mask = 0ull;
-    const int lim = npairs < 64 ? npairs : 64;
-    for (int base = 0; base < lim; base += g1) {
-        const int k = base + l;
-        bool act = false;
-        if (k < lim) {
-            const DPair pr = load_pair(pairs + k);
-            const DGeom G = load_geom(geoms + pr.gm);
-            const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
-            act = pair_may_touch(pr, G, lo[m], hi[m]);
-        }
-        const unsigned long long b = __ballot(act);
-        mask |= ((b >> (wg * g1)) & low) << base;
-    }
-    if (npairs > 64) mask = ~0ull;
-    return mask;
-}
 
 // Pair loop of one waypoint per lane.  All 64 lanes run the (wave-uniform) loop; `live` lanes
 // test the pairs of their own mask.  gbits = the lanes of this lane's candidate within the
@@ -845,8 +808,11 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
     return ghit;
 }
 
-template <int D, int NM, int P, bool ONEGEOM>
-__global__ __launch_bounds__(kBlock) void k_sspp_c2f(
+#ifndef SSPP_C2F_WAVES_PER_EU
+#define SSPP_C2F_WAVES_PER_EU 1
+#endif
+template <int D, int NM, int P, bool ONEGEOM, int NT>
+__global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     SsppC2F a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
     const double* __restrict__ atab, const int* __restrict__ aspan,
     const double* __restrict__ init_ctrl, const double* __restrict__ limits,
@@ -855,73 +821,141 @@ __global__ __launch_bounds__(kBlock) void k_sspp_c2f(
     BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int P1 = P + 1;
+    constexpr int NB = 3 * NM;  // AABB extents per candidate (x, y, z per mover)
     const int tid = threadIdx.x, cpb = a.cpb, n = a.n, W = a.W, g1 = a.g1;
-    const int ndof = n * D;
-    const long long cand0 = (long long)blockIdx.x * cpb;
+    const int lg1 = __builtin_ctz(g1);
+    const int ndof = n * D, nch = W - 1;
+    const int step = blockIdx.x / a.nblk_step, blk = blockIdx.x - step * a.nblk_step;
+    const long long cand0 = (long long)blk * cpb;
     const int nvalid = (int)min((long long)cpb, a.B - cand0);
-    const long long first_id = a.first_id;
+    const long long first_id = a.first_id + step * a.step_stride;
+    if (a.ablate & 64) return;  // profiling: launch + dispatch cost only
+    if (step) {
+        arc += step * a.B;
+        feasible += step * a.B;
+        if (ctrl_out) ctrl_out += step * a.B * ndof;
+        part += step * a.nblk_step;
+        sync += step;
+        if (best) best += step;
+    }
     double* s_ctrl = smem;                                    // [cpb][n][D]
-    double* s_wsum = s_ctrl + cpb * ndof;                     // [4]
-    double* s_arc = s_wsum + kBlock / 64;                     // [cpb]
-    unsigned long long* s_mask = (unsigned long long*)(s_arc + cpb);  // [cpb]
+    double* s_chord = s_ctrl + cpb * ndof;                    // [cpb][W-1]
+    double* s_vsum = s_chord + cpb * nch;                     // [cpb][lpc/64]
+    double* s_arc = s_vsum + cpb * (a.lpc >> 6);              // [cpb]
+    double* s_box = s_arc + cpb;                              // [cpb][2][NB]
+    unsigned long long* s_mask = (unsigned long long*)(s_box + cpb * 2 * NB);  // [cpb]
     int* s_feas = (int*)(s_mask + cpb);                       // [cpb]
     int* s_surv = s_feas + cpb;                               // [cpb + 1] (last = count)
 
-    // ---- prologue: control points (+ sampleWithNoise) in LDS
-    if (ctrl_in) {
-        const double* src = ctrl_in + cand0 * ndof;
-        for (int e = tid; e < nvalid * ndof; e += kBlock) s_ctrl[e] = src[e];
-    } else {
-        const int npert = (n - 2 * P) * D;
-        const bool from_pert = !a.insample && !(a.ablate & 1);
-        for (int e = tid; e < cpb * ndof; e += kBlock) {
-            const int sl = e / ndof, r = e - sl * ndof;
-            const int k = r - P * D;
-            s_ctrl[e] = (from_pert && k >= 0 && k < npert && sl < nvalid)
-                            ? pert[(cand0 + sl) * npert + k]
-                            : init_ctrl[r];
-        }
-        if (a.insample && !(a.ablate & 1)) {
-            __syncthreads();
-            const int npairs = (npert + 1) >> 1;
-            for (int e = tid; e < nvalid * npairs; e += kBlock) {
-                const int sl = e / npairs, m = e - sl * npairs;
-                double z0, z1;
-                normal_pair(a.seed, (unsigned long long)(first_id + cand0 + sl), (unsigned)m, 0u, &z0, &z1);
-                double* c = s_ctrl + sl * ndof + P * D;
-                const int k0 = 2 * m, k1 = 2 * m + 1;
-                c[k0] = c[k0] + (a.sigma * z0) * limits[k0 % D];
-                if (k1 < npert) c[k1] = c[k1] + (a.sigma * z1) * limits[k1 % D];
+    // ---- prologue: control points (+ sampleWithNoise) in LDS.  Element e = sl * ndof + r is
+    // walked with one division up front and add-with-carry afterwards.
+    {
+        const int dsl = NT / ndof, dr = NT - dsl * ndof;
+        int sl = tid / ndof, r = tid - sl * ndof;
+        if (ctrl_in) {
+            const double* src = ctrl_in + cand0 * ndof;
+            for (; sl < nvalid; sl += dsl) {
+                s_ctrl[sl * ndof + r] = src[sl * ndof + r];
+                r += dr;
+                if (r >= ndof) { r -= ndof; ++sl; }
+            }
+        } else {
+            const int npert = (n - 2 * P) * D;
+            const bool from_pert = !a.insample && !(a.ablate & 1);
+            for (; sl < cpb; sl += dsl) {
+                const int k = r - P * D;
+                s_ctrl[sl * ndof + r] = (from_pert && k >= 0 && k < npert && sl < nvalid)
+                                            ? pert[(cand0 + sl) * npert + k]
+                                            : init_ctrl[r];
+                r += dr;
+                if (r >= ndof) { r -= ndof; ++sl; }
             }
         }
     }
+    if (tid < cpb) s_mask[tid] = 0ull;
     __syncthreads();
+    if (!ctrl_in && a.insample && !(a.ablate & 1)) {
+        const int npert = (n - 2 * P) * D;
+        const int npairs = (npert + 1) >> 1;
+        const int dsl = NT / npairs, dm = NT - dsl * npairs;
+        int sl = tid / npairs, m = tid - sl * npairs;
+        for (; sl < nvalid; sl += dsl) {
+            double z0, z1;
+            normal_pair(a.seed, (unsigned long long)(first_id + cand0 + sl), (unsigned)m, 0u, &z0, &z1);
+            double* c = s_ctrl + sl * ndof + P * D;
+            const int k0 = 2 * m, k1 = 2 * m + 1;
+            c[k0] = c[k0] + (a.sigma * z0) * limits[k0 % D];
+            if (k1 < npert) c[k1] = c[k1] + (a.sigma * z1) * limits[k1 % D];
+            m += dm;
+            if (m >= npairs) { m -= npairs; ++sl; }
+        }
+        __syncthreads();
+    }
     if (ctrl_out) {
         double* dst = ctrl_out + cand0 * ndof;
-        for (int e = tid; e < nvalid * ndof; e += kBlock) dst[e] = s_ctrl[e];
+        for (int e = tid; e < nvalid * ndof; e += NT) dst[e] = s_ctrl[e];
     }
 
     const SceneT TT = T;
     const bool collide_on = a.has_scene && !(a.ablate & 2);
+    const int np = a.sc.npairs;
+    // ---- candidate-level broadphase (convex hull of the control points, see pair_may_touch):
+    // AABB per (candidate, mover, axis), then one (candidate, pair) test per thread; the mask
+    // bits are OR-ed into LDS.
+    if (collide_on && !(a.ablate & 32)) {
+        for (int e = tid; e < cpb * NB; e += NT) {
+            const int sl = e / NB, md = e - sl * NB, m = md / 3, d = md - m * 3;
+            const int col = 7 * m + d;
+            double lo, hi;
+            if (col < D) {
+                const double* c = s_ctrl + sl * ndof + col;
+                lo = hi = c[0];
+                for (int j = 1; j < n; ++j) {
+                    const double v = c[j * D];
+                    lo = v < lo ? v : lo;
+                    hi = v > hi ? v : hi;
+                }
+            } else {
+                lo = hi = (double)((cmover_t)TT.movers)[m].qpos0[d];
+            }
+            s_box[sl * 2 * NB + md] = lo;
+            s_box[sl * 2 * NB + NB + md] = hi;
+        }
+        __syncthreads();
+        if (np > 64) {
+            if (tid < cpb) s_mask[tid] = ~0ull;
+        } else {
+            for (int e = tid; e < cpb * np; e += NT) {
+                const int sl = e / np, k = e - sl * np;
+                const DPair pr = load_pair((cpair_t)TT.pairs + k);
+                const DGeom G = load_geom((cgeom_t)TT.geoms + pr.gm);
+                const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
+                const double* bx = s_box + sl * 2 * NB;
+                if (pair_may_touch(pr, G, bx + 3 * m, bx + NB + 3 * m))
+                    atomicOr(s_mask + sl, 1ull << k);
+            }
+        }
+        __syncthreads();
+    } else if (collide_on) {
+        if (tid < cpb) s_mask[tid] = ~0ull;
+        __syncthreads();
+    }
     // ---- phase 1: G1 lanes per candidate, first n1 waypoints of the coarse-to-fine order
     {
-        const int g = tid / g1, l = tid - g * g1, wg = (tid & 63) / g1;
+        const int g = tid >> lg1, l = tid & (g1 - 1), wg = (tid & 63) >> lg1;
         const unsigned long long low = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
         const unsigned long long gbits = low << (wg * g1);
         const bool valid = g < nvalid;
-        const double* myc = s_ctrl + (valid ? g : 0) * ndof;
         bool ghit = false;
         if (collide_on) {
-            const unsigned long long mymask = group_hull_mask<D, NM>(
-                myc, n, a.sc.npairs, (cpair_t)TT.pairs, (cgeom_t)TT.geoms, (cmover_t)TT.movers, g1, l, wg);
-            // union over the wave's groups (wave-uniform)
-            unsigned long long umask = 0ull;
-            for (int w = 0; w < 64; w += g1) umask |= __shfl(mymask, w, 64);
-            if (l == 0) s_mask[g] = mymask;
-            const bool live = valid && l < a.n1 && !a.sc.static_block;
+            const unsigned long long mymask = s_mask[g];
+            unsigned long long umask = 0ull;  // union over the wave's groups (wave-uniform)
+            const int g0 = (tid & ~63) >> lg1;
+            for (int w = 0; w < (64 >> lg1); ++w) umask |= s_mask[g0 + w];
+            const bool live = valid && l < a.n1 && !a.sc.static_block && !(a.ablate & 16);
             double q[D];
             const int row = l < a.npts ? l : 0;
-            eval_pt<D, P>(myc, otab + row * P1, ospan[row], q);
+            eval_pt<D, P>(s_ctrl + (valid ? g : 0) * ndof, otab + row * P1, ospan[row], q);
             ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mymask, umask, gbits, nullptr, a.sc, TT);
         }
         if (l == 0) s_feas[g] = valid && !ghit && !(collide_on && a.sc.static_block);
@@ -929,7 +963,7 @@ __global__ __launch_bounds__(kBlock) void k_sspp_c2f(
     __syncthreads();
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
     const int R = a.npts - a.n1;
-    if (collide_on && R > 0) {
+    if (collide_on && R > 0 && !(a.ablate & 8)) {
         if (tid == 0) {
             int ns = 0;
             for (int s = 0; s < nvalid; ++s)
@@ -941,7 +975,7 @@ __global__ __launch_bounds__(kBlock) void k_sspp_c2f(
         unsigned long long umask = 0ull;
         for (int i = 0; i < ns; ++i) umask |= s_mask[s_surv[i]];
         const int items = ns * R;
-        for (int base = 0; base < items; base += kBlock) {  // workgroup-uniform trip count
+        for (int base = 0; base < items; base += NT) {  // workgroup-uniform trip count
             const int it = base + tid;
             bool live = it < items;
             const int si = live ? it / R : 0;
@@ -961,32 +995,45 @@ __global__ __launch_bounds__(kBlock) void k_sspp_c2f(
             if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
-    // ---- phase 3: arc length, canonical order (lanes = a.lpc per candidate)
-    const int lpc = a.lpc, cpp = kBlock / lpc;
-    const int pc = tid / lpc, vl = tid - pc * lpc;
-    for (int s0 = 0; s0 < cpb; s0 += cpp) {  // workgroup-uniform
-        const int s = s0 + pc;
-        double acc = 0.0;
-        if (pc < cpp && s < nvalid && !(a.ablate & 4)) {
-            const double* myc = s_ctrl + s * ndof;
-            for (int jj = vl; jj < W - 1; jj += lpc) {
-                const int i = jj + 1;
-                double q[D], q2[D];
-                eval_pt<D, P>(myc, atab + (i - 1) * P1, aspan[i - 1], q);
-                eval_pt<D, P>(myc, atab + i * P1, aspan[i], q2);
-                acc = acc + dist_nd<D>(q, q2);
+    // ---- phase 3: arc length.  Chords v_j -> v_{j+1} (v_i = s(i/(W-1))) are computed by G1
+    // threads per candidate over consecutive runs (each point evaluated once) into LDS, then
+    // summed per candidate in the canonical order of oracle/sspp_oracle.c::or_canon_sum:
+    // lpc lane partials (chords vl, vl+lpc, ...), an xor butterfly per 64 lanes, 64-lane
+    // groups in order.
+    if (!(a.ablate & 4)) {
+        const int g = tid >> lg1, l = tid & (g1 - 1);
+        const int per = (nch + g1 - 1) >> lg1;
+        const int j0 = l * per, j1 = min(j0 + per, nch);
+        if (g < nvalid && j0 < j1) {
+            const double* myc = s_ctrl + g * ndof;
+            double* ch = s_chord + g * nch;
+            double qa[D], qb[D];
+            eval_pt<D, P>(myc, atab + j0 * P1, aspan[j0], qa);
+            for (int j = j0; j < j1; ++j) {
+                eval_pt<D, P>(myc, atab + (j + 1) * P1, aspan[j + 1], qb);
+                ch[j] = dist_nd<D>(qa, qb);
+#pragma unroll
+                for (int d = 0; d < D; ++d) qa[d] = qb[d];
             }
         }
-        acc = wave_sum(acc);
         __syncthreads();
-        if ((tid & 63) == 0) s_wsum[tid >> 6] = acc;
-        __syncthreads();
-        if (vl == 0 && pc < cpp && s < nvalid) {
-            const int w0 = (pc * lpc) >> 6, nw = lpc >> 6;
-            double t = s_wsum[w0];
-            for (int w = 1; w < nw; ++w) t = t + s_wsum[w0 + w];
-            s_arc[s] = t;
+        const int lpc = a.lpc, nvw = lpc >> 6, lane = tid & 63;
+        for (int vw = tid >> 6; vw < nvalid * nvw; vw += NT / 64) {  // wave-uniform
+            const int s = vw / nvw, vl = (vw - s * nvw) * 64 + lane;
+            const double* ch = s_chord + s * nch;
+            double acc = 0.0;
+            for (int j = vl; j < nch; j += lpc) acc = acc + ch[j];
+            acc = wave_sum(acc);
+            if (lane == 0) s_vsum[vw] = acc;
         }
+        __syncthreads();
+        if (tid < nvalid) {
+            double t = s_vsum[tid * nvw];
+            for (int w = 1; w < nvw; ++w) t = t + s_vsum[tid * nvw + w];
+            s_arc[tid] = t;
+        }
+    } else if (tid < nvalid) {
+        s_arc[tid] = 0.0;
     }
     __syncthreads();
     if (tid < nvalid) {
@@ -1003,7 +1050,7 @@ __global__ __launch_bounds__(kBlock) void k_sspp_c2f(
             if (s_arc[s] < bb.cost) { bb.cost = s_arc[s]; bb.idx = first_id + cand0 + s; }
         }
     }
-    finish_batch(bb, part, sync, best);
+    finish_batch<NT>(bb, part, sync, best, a.nblk_step, blk);
 }
 
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
@@ -1237,11 +1284,12 @@ struct sspp_job {
     int npert = 0;
     int insample = 0;          // sample inside the scoring kernel (SSPP_INSAMPLE=1)
     // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
-    int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16;
+    int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16, nt2 = 256;
     size_t lds2 = 0;
     double* d_otab = nullptr;  // collision rows in coarse-to-fine order
     int* d_ospan = nullptr;
-    ArgminSync* d_sync = nullptr;  // sharded arrival counters of the fused argmin
+    DPair* d_pairs = nullptr;  // this job's pair table (closest-to-the-mean-path first)
+    ArgminSync* d_sync = nullptr;  // sharded arrival counters of the fused argmin [kMaxSteps]
     double start[4], end[4], lo[4], hi[4];
     double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
 };
@@ -1531,6 +1579,75 @@ static SceneT scene_t(const sspp_scene* s) {
     return t;
 }
 
+// Pair order for the feasibility scan of one job.  checkCollision's answer is an OR over pairs,
+// so the order is free; the scan stops at the first pair in contact, so the pairs the sampled
+// paths most often touch should come first.  Heuristic: the smallest bounding-sphere gap
+// (planes: height of the geom centre minus its radius) between the moving geom and the partner
+// along the mean path (the init spline, 33 points), ascending; ties keep the scene order.
+static std::vector<DPair> pairs_for_job(const sspp_scene* sc, const double* knots, int nknots, int p,
+                                        const double* ctrl, int D) {
+    std::vector<DPair> out = sc->pairs;
+    const int np = (int)out.size();
+    if (np < 2) return out;
+    std::vector<double> gap(np, 1e300);
+    const int nm = (int)sc->movers.size();
+    const int n = nknots - p - 1;
+    for (int t = 0; t <= 32; ++t) {
+        const double u = t / 32.0;
+        const int sp = span_of(u, p, knots, nknots);
+        double N[kMaxP + 1];
+        basis_funcs(u, p, sp, knots, N);
+        double q[16] = {0};
+        for (int d = 0; d < D && d < 16; ++d) {
+            double acc = 0.0;
+            for (int r = 0; r <= p; ++r) {
+                const int j = sp - p + r;
+                if (j >= 0 && j < n) acc += N[r] * ctrl[j * D + d];
+            }
+            q[d] = acc;
+        }
+        double mp[kMaxMovers][3], mR[kMaxMovers][9];
+        for (int m = 0; m < nm && m < kMaxMovers; ++m) {
+            double qp[7];
+            for (int k = 0; k < 7; ++k) qp[k] = (7 * m + k < D) ? q[7 * m + k] : sc->movers[m].qpos0[k];
+            normalize4(qp + 3);
+            quat2mat(qp + 3, mR[m]);
+            for (int k = 0; k < 3; ++k) mp[m][k] = qp[k];
+        }
+        for (int k = 0; k < np; ++k) {
+            const DPair& pr = out[k];
+            const DGeom& G = sc->geoms[pr.gm];
+            const int m = G.mover > 0 ? G.mover : 0;
+            double t3[3], gp[3], op[3];
+            matvec3(mR[m], G.pos, t3);
+            for (int d = 0; d < 3; ++d) gp[d] = mp[m][d] + t3[d];
+            if (pr.omover >= 0) {
+                matvec3(mR[pr.omover], pr.opos, t3);
+                for (int d = 0; d < 3; ++d) op[d] = mp[pr.omover][d] + t3[d];
+            } else {
+                for (int d = 0; d < 3; ++d) op[d] = pr.opos[d];
+            }
+            double g;
+            if (pr.otype == 0) {
+                const double nz[3] = {pr.omat[2], pr.omat[5], pr.omat[8]};
+                g = (gp[0] - op[0]) * nz[0] + (gp[1] - op[1]) * nz[1] + (gp[2] - op[2]) * nz[2] - G.rbound;
+            } else if (G.rbound > 0.0 && pr.orbound > 0.0) {
+                const double dx = gp[0] - op[0], dy = gp[1] - op[1], dz = gp[2] - op[2];
+                g = std::sqrt(dx * dx + dy * dy + dz * dz) - G.rbound - pr.orbound;
+            } else {
+                g = 0.0;
+            }
+            gap[k] = std::min(gap[k], g);
+        }
+    }
+    std::vector<int> idx(np);
+    for (int k = 0; k < np; ++k) idx[k] = k;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return gap[a] < gap[b]; });
+    std::vector<DPair> sorted(np);
+    for (int k = 0; k < np; ++k) sorted[k] = out[idx[k]];
+    return sorted;
+}
+
 // Coarse-to-fine order of the collision waypoints 0..W: breadth-first interval bisection, so
 // every prefix is spread evenly over the path (k_sspp_c2f phase 1 tests a prefix).
 static std::vector<int> c2f_order(int W) {
@@ -1611,8 +1728,12 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
         const char* e = getenv("SSPP_G1");
         int g1 = e ? atoi(e) : 16;
         if (g1 != 4 && g1 != 8 && g1 != 16 && g1 != 32 && g1 != 64) g1 = 16;
+        const char* t = getenv("SSPP_NT");
+        int nt = t ? atoi(t) : 256;
+        if (nt != 64 && nt != 128 && nt != 256) nt = 256;
         j->g1 = g1;
-        j->cpb2 = kBlock / g1;
+        j->nt2 = nt;
+        j->cpb2 = nt / g1;
         j->n1 = std::min(g1, W + 1);
         std::vector<int> ord = c2f_order(W);
         std::vector<double> uo;
@@ -1621,7 +1742,18 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
             sspp_job_free(j);
             return rc;
         }
-        j->lds2 = sizeof(double) * ((size_t)j->cpb2 * n * D + kBlock / 64 + j->cpb2) +
+        if (scene && !scene->pairs.empty()) {
+            const char* po = getenv("SSPP_PAIR_ORDER");  // 0 = scene order (profiling)
+            std::vector<DPair> jp = (po && atoi(po) == 0)
+                                        ? scene->pairs
+                                        : pairs_for_job(scene, a->knots, j->nknots, p, a->init_ctrl, D);
+            if ((rc = upload(&j->d_pairs, jp.data(), jp.size()))) {
+                sspp_job_free(j);
+                return rc;
+            }
+        }
+        const int nm = j->nm < 1 ? 1 : j->nm;
+        j->lds2 = sizeof(double) * ((size_t)j->cpb2 * (n * D + (W - 1) + lanes_for(W - 1) / 64 + 1 + 6 * nm)) +
                   sizeof(unsigned long long) * j->cpb2 + sizeof(int) * (2 * j->cpb2 + 1);
         if (j->lds2 > 64 * 1024) j->c2f = 0;
     }
@@ -1629,9 +1761,10 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc sampler buffer");
     }
-    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess ||
-        hipMalloc((void**)&j->d_sync, sizeof(ArgminSync)) != hipSuccess ||
-        hipMemset(j->d_sync, 0, sizeof(ArgminSync)) != hipSuccess) {
+    // one record per workgroup: at most max_batch workgroups per step whatever the layout
+    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * std::max<int64_t>(nblk, max_batch) * kMaxSteps) != hipSuccess ||
+        hipMalloc((void**)&j->d_sync, sizeof(ArgminSync) * kMaxSteps) != hipSuccess ||
+        hipMemset(j->d_sync, 0, sizeof(ArgminSync) * kMaxSteps) != hipSuccess) {
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
     }
@@ -1662,21 +1795,35 @@ static hipError_t launch_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs&
     return hipGetLastError();
 }
 
-template <int D, int NM, int P>
-static hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
-                             hipStream_t st) {
+static SceneT scene_t_job(const sspp_job* j) {
+    SceneT t = scene_t(j->scene);
+    if (j->d_pairs) t.pairs = j->d_pairs;
+    return t;
+}
+
+template <int D, int NM, int P, int NT>
+static hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                                hipStream_t st) {
     const double* atab = j->d_tab + (size_t)(j->W + 1) * (P + 1);
     const int* aspan = j->d_span + (j->W + 1);
     if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
-        hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true>), dim3(nblk), dim3(kBlock), j->lds2, st, k,
-                           scene_t(j->scene), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
+        hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true, NT>), dim3(nblk), dim3(NT), j->lds2, st, k,
+                           scene_t_job(j), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
                            o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((k_sspp_c2f<D, NM, P, false>), dim3(nblk), dim3(kBlock), j->lds2, st, k,
-                       scene_t(j->scene), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
+    hipLaunchKernelGGL((k_sspp_c2f<D, NM, P, false, NT>), dim3(nblk), dim3(NT), j->lds2, st, k,
+                       scene_t_job(j), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
                        o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
     return hipGetLastError();
+}
+
+template <int D, int NM, int P>
+static hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                             hipStream_t st) {
+    if (j->nt2 == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
+    if (j->nt2 == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st);
+    return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
 }
 
 template <int P>
@@ -1718,7 +1865,8 @@ static hipError_t dispatch_sspp_p(const SsppK& k, const sspp_job* j, const SsppP
 }
 
 static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B, double* d_arc,
-                    uint8_t* d_feasible, double* d_ctrl_out, sspp_best* d_best, void* stream) {
+                    uint8_t* d_feasible, double* d_ctrl_out, sspp_best* d_best, void* stream,
+                    int steps = 1, int64_t step_stride = 0) {
     sspp::clear_error();
     if (!j || j->kind != 0) return sspp::set_error(SSPP_E_INVAL, "not a SamplingPathPlanner job");
     if (B < 1 || B > j->max_batch) return sspp::set_error(SSPP_E_INVAL, "batch size out of range");
@@ -1734,6 +1882,8 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     k.ablate = ablate;
     k.insample = j->insample;
     SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
+    if (steps < 1 || steps > kMaxSteps || (steps > 1 && (!j->c2f || d_ctrl || (j->npert > 0 && !j->insample))))
+        return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..16, coarse-to-fine kernel with in-kernel sampling only");
     const int cpb = j->c2f ? j->cpb2 : j->cpb;
     const int nblk = (int)((B + cpb - 1) / cpb);
     hipStream_t st = (hipStream_t)stream;
@@ -1753,7 +1903,9 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         c.first_id = first_id; c.B = B;
         c.g1 = j->g1; c.cpb = j->cpb2; c.npts = j->W + 1; c.n1 = j->n1;
         c.lpc = lanes_for(j->W - 1);
-        e = j->p == 3 ? dispatch_c2f_p<3>(c, j, o, nblk, st) : dispatch_c2f_p<2>(c, j, o, nblk, st);
+        c.nblk_step = nblk;
+        c.step_stride = step_stride;
+        e = j->p == 3 ? dispatch_c2f_p<3>(c, j, o, nblk * steps, st) : dispatch_c2f_p<2>(c, j, o, nblk * steps, st);
     } else {
         e = j->p == 3 ? dispatch_sspp_p<3>(k, j, o, nblk, st) : dispatch_sspp_p<2>(k, j, o, nblk, st);
     }
@@ -1884,6 +2036,7 @@ extern "C" void sspp_job_free(sspp_job* j) {
         if (p) (void)hipFree(p);
     if (j->d_span) (void)hipFree(j->d_span);
     if (j->d_otab) (void)hipFree(j->d_otab);
+    if (j->d_pairs) (void)hipFree(j->d_pairs);
     if (j->d_ospan) (void)hipFree(j->d_ospan);
     if (j->d_part) (void)hipFree(j->d_part);
     if (j->d_pert) (void)hipFree(j->d_pert);
@@ -1938,7 +2091,7 @@ __global__ __launch_bounds__(64) void k_argmin_steps(const BlockBest* __restrict
 }  // namespace
 
 extern "C" int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void* const* streams,
-                                       int64_t B, int nsteps, int64_t first_id,
+                                       int64_t B, int nsteps, int steps_per_launch, int64_t first_id,
                                        int64_t step_stride, double* const* d_arc,
                                        uint8_t* const* d_feasible, sspp_best* d_best) {
     sspp::clear_error();
@@ -1950,10 +2103,13 @@ extern "C" int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void*
         for (int c = 0; c < b; ++c)
             if (jobs[c] == jobs[b]) return sspp::set_error(SSPP_E_INVAL, "branches need distinct jobs");
     }
-    for (int i = 0; i < nsteps; ++i) {
-        const int b = i % nbranch;
+    const int S = steps_per_launch;
+    if (S < 1 || S > kMaxSteps) return sspp::set_error(SSPP_E_INVAL, "steps_per_launch must be in [1, 16]");
+    for (int i = 0, l = 0; i < nsteps; i += S, ++l) {
+        const int b = l % nbranch, s = std::min(S, nsteps - i);
         const int rc = run_sspp(jobs[b], nullptr, first_id + (int64_t)i * step_stride, B, d_arc[b],
-                                d_feasible[b], nullptr, d_best ? d_best + i : nullptr, streams[b]);
+                                d_feasible[b], nullptr, d_best ? d_best + i : nullptr, streams[b],
+                                s, step_stride);
         if (rc != SSPP_OK) return rc;
     }
     return SSPP_OK;

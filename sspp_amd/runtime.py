@@ -285,24 +285,25 @@ class TspJob(_Job):
 
 
 class SsppSteps:
-    """Back-to-back SamplingPathPlanner batches enqueued by the C++ step executor
-    (sspp_steps_enqueue_sspp): step i runs on branch i % len(jobs) — jobs[b] with streams[b] and
-    its scratch arc/feasible buffers — scoring ids first_id + i * step_stride + [0, B)."""
+    """Back-to-back SamplingPathPlanner steps enqueued by the C++ step executor
+    (sspp_steps_enqueue_sspp): step i scores ids first_id + i * step_stride + [0, B); steps go
+    steps_per_launch to a kernel launch, launch l to branch l % len(jobs) — jobs[b] with
+    streams[b] and its scratch arc/feasible buffers (steps_per_launch * B entries each)."""
 
-    def __init__(self, jobs, streams, B, arc_bufs, feas_bufs):
+    def __init__(self, jobs, streams, B, arc_bufs, feas_bufs, steps_per_launch=1):
         nb = len(jobs)
         self._keep = (jobs, streams, arc_bufs, feas_bufs)
         self._J = (C.c_void_p * nb)(*[j._h for j in jobs])
         self._S = (C.c_void_p * nb)(*[_stream(s).value for s in streams])
         self._A = (C.c_void_p * nb)(*[_ptr(a).value for a in arc_bufs])
         self._F = (C.c_void_p * nb)(*[_ptr(f).value for f in feas_bufs])
-        self.nb, self.B = nb, int(B)
+        self.nb, self.B, self.spl = nb, int(B), int(steps_per_launch)
 
     def enqueue(self, nsteps, first_id, step_stride, best=None):
         """best: None or an (nsteps, 4) int64 device tensor for the per-step argmin records."""
         check(lib().sspp_steps_enqueue_sspp(self._J, self.nb, self._S, self.B, int(nsteps),
-                                            int(first_id), int(step_stride), self._A, self._F,
-                                            _ptr(best)), "steps enqueue")
+                                            self.spl, int(first_id), int(step_stride), self._A,
+                                            self._F, _ptr(best)), "steps enqueue")
 
 
 def reduce_best_steps(parts, out, stream=None):

@@ -57,15 +57,17 @@ def run_sspp(job, B, first=0, with_ctrl=True):
 
 # scoring kernels: (SSPP_KERNEL, SSPP_G1) — coarse-to-fine k_sspp_c2f with several phase-1
 # lane-group sizes, and the one-waypoint-per-lane k_sspp
-KERNELS = [("1", "16"), ("1", "4"), ("1", "64"), ("0", "16")]
+KERNELS = [("1", "16", "256"), ("1", "4", "256"), ("1", "64", "64"), ("1", "16", "128"),
+           ("1", "16", "64"), ("0", "16", "256")]
 
 
-@pytest.mark.parametrize("kernel,g1", KERNELS)
+@pytest.mark.parametrize("kernel,g1,nt", KERNELS)
 @pytest.mark.parametrize("B,W", [(4096, 128), (257, 128), (1, 128), (300, 50), (100, 256), (64, 2)])
-def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g1, B, W):
+def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g1, nt, B, W):
     import sspp_amd as S
     monkeypatch.setenv("SSPP_KERNEL", kernel)
     monkeypatch.setenv("SSPP_G1", g1)
+    monkeypatch.setenv("SSPP_NT", nt)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=0x5EED, max_batch=B)
@@ -96,13 +98,14 @@ def test_robocrane_config2_is_nontrivial(robocrane):
     assert 0 < nfeas < 4096, nfeas  # SURVEY config 2 (sigma 0.08): ~0.3% clear the brick stack
 
 
-@pytest.mark.parametrize("kernel,g1", KERNELS)
-def test_score_ctrl_mode_matches_oracle(robocrane, monkeypatch, kernel, g1):
+@pytest.mark.parametrize("kernel,g1,nt", KERNELS)
+def test_score_ctrl_mode_matches_oracle(robocrane, monkeypatch, kernel, g1, nt):
     """Caller-supplied splines (checkCollision + computeArcLength on arbitrary ctrl)."""
     import sspp_amd as S
     import torch
     monkeypatch.setenv("SSPP_KERNEL", kernel)
     monkeypatch.setenv("SSPP_G1", g1)
+    monkeypatch.setenv("SSPP_NT", nt)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     rng = np.random.default_rng(7)
@@ -175,12 +178,13 @@ def test_stacking_tsp_matches_oracle(cuda, B, cp, K):
         assert 0 < st.sum() < B  # both outcomes present
 
 
-@pytest.mark.parametrize("kernel,g1", KERNELS)
-def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1):
+@pytest.mark.parametrize("kernel,g1,nt", KERNELS)
+def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1, nt):
     """planner.xml: block1 (free) vs static wall/block2, 7-DoF window, path through the wall."""
     import sspp_amd as S
     monkeypatch.setenv("SSPP_KERNEL", kernel)
     monkeypatch.setenv("SSPP_G1", g1)
+    monkeypatch.setenv("SSPP_NT", nt)
     model = S.Model(PLANNER)
     scene = S.Scene(model, 0, 7)
     oscene = O.Scene(mjcf_ref.load(PLANNER), 0, 7)
@@ -229,18 +233,20 @@ def test_fused_argmin_back_to_back(robocrane, monkeypatch, insample, kernel):
     assert np.abs(r["ctrl"] - O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 0x5EED, 77, 257)).max() <= 1e-12
 
 
-def test_step_executor_matches_eager(robocrane):
-    """C++ step executor: G batches round robin over 3 streams; every step's argmin record
-    equals a single eager launch on the same candidate ids."""
+@pytest.mark.parametrize("spl", [1, 3, 16])
+def test_step_executor_matches_eager(robocrane, spl):
+    """C++ step executor: G steps, spl per launch, launches round robin over 3 streams; every
+    step's argmin record equals a single eager launch on the same candidate ids."""
     import sspp_amd as S
     import torch
     _, scene, _ = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
-    B, G, stride, first = 4096, 7, 2 * 4096, 5 * 4096
+    B, G, stride, first = 4096, 19, 2 * 4096, 5 * 4096
     jobs = [S.SsppJob(scene, knots, 3, ctrl0, 0.12, np.ones(7), 128, max_batch=B) for _ in range(3)]
-    bufs = [j.alloc(B) for j in jobs]
+    arcs = [torch.empty(spl * B, dtype=torch.float64, device="cuda") for _ in jobs]
+    feas = [torch.empty(spl * B, dtype=torch.uint8, device="cuda") for _ in jobs]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(2)]
-    ex = S.SsppSteps(jobs, streams, B, [b["arc"] for b in bufs], [b["feasible"] for b in bufs])
+    ex = S.SsppSteps(jobs, streams, B, arcs, feas, steps_per_launch=spl)
     best = torch.zeros((G, 4), dtype=torch.int64, device="cuda")
     ex.enqueue(G, first, stride, best)
     torch.cuda.synchronize()

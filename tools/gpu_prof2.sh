@@ -1,0 +1,15 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/prof2; mkdir -p $O; rm -f $O/*.json*
+for m in 0 1 2 4 6 3 7; do
+  SSPP_ABLATE=$m timeout -k 10 200 python bench.py --no-cpu-baseline --steps 1000 --warmup 50 --roofline-launches 50 >> $O/bench.jsonl 2>>$O/err.log || exit 1
+done
+cd /tmp && export TMPDIR=/tmp
+for m in 0 2 6; do
+SSPP_ABLATE=$m timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU -d $O/sq$m -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --roofline-launches 10 > $O/sq$m.log 2>&1 || exit 1
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d $O/sqb -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --roofline-launches 10 > $O/sqb.log 2>&1 || exit 1
+cd $R && python -c "
+import json
+for l in open('$O/bench.jsonl'):
+    d=json.loads(l); print(round(d['value']/1e6,1), 'M/s', round(d['ms_per_step']*1e3,2), 'us/step', round(d['roofline']['kernel_us'],1))
+"
