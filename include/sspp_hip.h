@@ -118,6 +118,9 @@ typedef struct sspp_sspp_args {
     const double* limits;   /* host [dof] */
     int check_points;       /* W: collision at i/W, i=0..W; arc on W points */
     uint64_t seed;
+    int arc_all;            /* 0 (reference): arc length only for collision-free candidates
+                               (findBestPath, include/sspp.h:171-192), +inf for the others;
+                               1: arc length for every candidate                         */
 } sspp_sspp_args;
 
 typedef struct sspp_tsp_args {

@@ -72,7 +72,8 @@ def lib():
         L.or_canon_sum.argtypes = [_d, C.c_int, C.c_int]
         L.or_lanes_for.argtypes = [C.c_int]
         L.or_sspp_score.argtypes = [C.c_void_p, _d, C.c_int, C.c_int, _d, C.c_int, C.c_int,
-                                    C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, _d, _u8]
+                                    C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    _d, _u8]
         L.or_argmin.restype = C.c_int64
         L.or_argmin.argtypes = [_d, _u8, C.c_int64, C.POINTER(C.c_double)]
         L.or_tsp_score.argtypes = [C.c_void_p, _d, _d, _d, C.c_int, C.c_int64, C.c_int,
@@ -244,14 +245,17 @@ def canon_sum(x, lanes=None):
     return lib().or_canon_sum(x, len(x), lanes)
 
 
-def sspp_score(scene, knots, p, ctrl, W, count_static=False, sequential=False, nthreads=0):
+def sspp_score(scene, knots, p, ctrl, W, count_static=False, sequential=False, nthreads=0,
+               arc_all=False):
+    """checkCollision + computeArcLength per candidate.  arc_all=False follows findBestPath
+    (include/sspp.h:171-192): only collision-free candidates get an arc length, the rest +inf."""
     knots, ctrl = _f64(knots), _f64(ctrl)
     B, n, D = ctrl.shape
     arc = np.zeros(B)
     feas = np.zeros(B, np.uint8)
     rc = lib().or_sspp_score(scene.ptr if scene is not None else None, knots, len(knots), p,
                              ctrl, n, D, B, W, int(count_static), int(sequential), nthreads,
-                             arc, feas)
+                             int(bool(arc_all)), arc, feas)
     if rc != 0:
         raise RuntimeError("or_sspp_score failed %d" % rc)
     return arc, feas

@@ -858,7 +858,7 @@ static double dist_nd(const double* a, const double* b, int D) {
 /* ------------------------------------------------------------------ SamplingPathPlanner */
 int or_sspp_score(const or_scene* s, const double* knots, int nknots, int p, const double* ctrl,
                   int n, int D, int64_t B, int W, int count_static, int sequential_sum,
-                  int nthreads, double* arc_out, uint8_t* feasible_out) {
+                  int nthreads, int arc_all, double* arc_out, uint8_t* feasible_out) {
     if (W < 2 || D > OR_MAXD || p > OR_MAXP || nknots != n + p + 1) return -1;
     if (s && s->mode == 0 && s->arg != D) return -2;
     int bad = 0;
@@ -880,6 +880,9 @@ int or_sspp_score(const or_scene* s, const double* knots, int nknots, int p, con
                 if (nc > 0) { feasible = 0; break; }
             }
         }
+        feasible_out[b] = (uint8_t)feasible;
+        /* include/sspp.h:171-192 findBestPath scores only the successful paths */
+        if (!feasible && !arc_all) { arc_out[b] = INFINITY; continue; }
         /* include/sspp.h:152-169 computeArcLength: chords between u=(i-1)/(W-1), i/(W-1) */
         double chords[4096];
         double* ch = W - 1 <= 4096 ? chords : (double*)malloc(sizeof(double) * (size_t)(W - 1));
@@ -892,7 +895,6 @@ int or_sspp_score(const or_scene* s, const double* knots, int nknots, int p, con
         }
         arc_out[b] = sequential_sum ? seq_sum(ch, W - 1) : or_canon_sum(ch, W - 1, or_lanes_for(W - 1));
         if (ch != chords) free(ch);
-        feasible_out[b] = (uint8_t)feasible;
     }
     return bad ? -3 : 0;
 }

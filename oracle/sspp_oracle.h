@@ -116,6 +116,7 @@ int    or_lanes_for(int items);
 int    or_sspp_score(const or_scene* s /* NULL = no collision */, const double* knots, int nknots,
                      int p, const double* ctrl /* [B][n][D] */, int n, int D, int64_t B, int W,
                      int count_static, int sequential_sum, int nthreads,
+                     int arc_all /* 0: +inf for colliding candidates (findBestPath) */,
                      double* arc_out, uint8_t* feasible_out);
 int64_t or_argmin(const double* cost, const uint8_t* feasible, int64_t B, double* best_cost);
 

@@ -51,7 +51,7 @@ class SsppArgs(C.Structure):
     _fields_ = [("knots", C.POINTER(C.c_double)), ("degree", C.c_int),
                 ("init_ctrl", C.POINTER(C.c_double)), ("n_ctrl", C.c_int), ("dof", C.c_int),
                 ("sigma", C.c_double), ("limits", C.POINTER(C.c_double)),
-                ("check_points", C.c_int), ("seed", C.c_uint64)]
+                ("check_points", C.c_int), ("seed", C.c_uint64), ("arc_all", C.c_int)]
 
 
 class TspArgs(C.Structure):

@@ -185,6 +185,7 @@ struct SsppK {
     unsigned long long seed;
     long long first_id, B;
     int lpc, cpb, shared_endpoints;
+    int arc_all;
 };
 
 struct TspK {
@@ -679,7 +680,7 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
         for (int w = 1; w < nw; ++w) t = t + s_wsum[w0 + w];
         const long long c = cand0 + slot;
         const int f = s_flag[slot] & s_flag[cpb];
-        arc[c] = t;
+        arc[c] = (f || a.arc_all) ? t : INFINITY;
         feasible[c] = (unsigned char)f;
         s_arc[slot] = f ? t : INFINITY;
     }
@@ -733,6 +734,7 @@ struct SsppC2F {
     // argmin records / counters (part + s * nblk_step, sync + s) and best[s]
     int nblk_step;
     long long step_stride;
+    int arc_all;   // 0: arc length only for collision-free candidates (+inf otherwise)
 };
 
 // Pair loop of one waypoint per lane.  All 64 lanes run the (wave-uniform) loop; `live` lanes
@@ -995,45 +997,69 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
-    // ---- phase 3: arc length.  Chords v_j -> v_{j+1} (v_i = s(i/(W-1))) are computed by G1
-    // threads per candidate over consecutive runs (each point evaluated once) into LDS, then
-    // summed per candidate in the canonical order of oracle/sspp_oracle.c::or_canon_sum:
-    // lpc lane partials (chords vl, vl+lpc, ...), an xor butterfly per 64 lanes, 64-lane
-    // groups in order.
+    // ---- phase 3: arc length (computeArcLength, include/sspp.h:152-169) of the listed
+    // candidates: the collision-free ones (findBestPath scores only successful paths), or all
+    // of them with arc_all.  Chords v_j -> v_{j+1} (v_i = s(i/(W-1))) go to LDS, then each
+    // candidate's chords are summed in the canonical order of oracle/sspp_oracle.c::or_canon_sum:
+    // lpc lane partials (chords vl, vl+lpc, ...), an xor butterfly per 64 lanes, 64-lane groups
+    // in order.
+    if (tid < cpb) s_arc[tid] = INFINITY;
     if (!(a.ablate & 4)) {
-        const int g = tid >> lg1, l = tid & (g1 - 1);
-        const int per = (nch + g1 - 1) >> lg1;
-        const int j0 = l * per, j1 = min(j0 + per, nch);
-        if (g < nvalid && j0 < j1) {
-            const double* myc = s_ctrl + g * ndof;
-            double* ch = s_chord + g * nch;
-            double qa[D], qb[D];
-            eval_pt<D, P>(myc, atab + j0 * P1, aspan[j0], qa);
-            for (int j = j0; j < j1; ++j) {
-                eval_pt<D, P>(myc, atab + (j + 1) * P1, aspan[j + 1], qb);
-                ch[j] = dist_nd<D>(qa, qb);
+        __syncthreads();
+        int* s_list = s_surv;  // phase 2 is done with it
+        if (tid == 0) {
+            int nl = 0;
+            for (int s = 0; s < nvalid; ++s)
+                if (a.arc_all || s_feas[s]) s_list[nl++] = s;
+            s_list[cpb] = nl;
+        }
+        __syncthreads();
+        const int nl = s_list[cpb];
+        if (a.arc_all) {
+            // every candidate: G1 threads per candidate over consecutive runs of chords, each
+            // point evaluated once
+            const int g = tid >> lg1, l = tid & (g1 - 1);
+            const int per = (nch + g1 - 1) >> lg1;
+            const int j0 = l * per, j1 = min(j0 + per, nch);
+            if (g < nvalid && j0 < j1) {
+                const double* myc = s_ctrl + g * ndof;
+                double* ch = s_chord + g * nch;
+                double qa[D], qb[D];
+                eval_pt<D, P>(myc, atab + j0 * P1, aspan[j0], qa);
+                for (int j = j0; j < j1; ++j) {
+                    eval_pt<D, P>(myc, atab + (j + 1) * P1, aspan[j + 1], qb);
+                    ch[j] = dist_nd<D>(qa, qb);
 #pragma unroll
-                for (int d = 0; d < D; ++d) qa[d] = qb[d];
+                    for (int d = 0; d < D; ++d) qa[d] = qb[d];
+                }
+            }
+        } else {
+            // the few collision-free candidates: one chord per thread over the workgroup
+            for (int it = tid; it < nl * nch; it += NT) {
+                const int si = it / nch, j = it - si * nch, sl = s_list[si];
+                const double* myc = s_ctrl + sl * ndof;
+                double qa[D], qb[D];
+                eval_pt<D, P>(myc, atab + j * P1, aspan[j], qa);
+                eval_pt<D, P>(myc, atab + (j + 1) * P1, aspan[j + 1], qb);
+                s_chord[sl * nch + j] = dist_nd<D>(qa, qb);
             }
         }
         __syncthreads();
         const int lpc = a.lpc, nvw = lpc >> 6, lane = tid & 63;
-        for (int vw = tid >> 6; vw < nvalid * nvw; vw += NT / 64) {  // wave-uniform
-            const int s = vw / nvw, vl = (vw - s * nvw) * 64 + lane;
-            const double* ch = s_chord + s * nch;
+        for (int vw = tid >> 6; vw < nl * nvw; vw += NT / 64) {  // wave-uniform
+            const int si = vw / nvw, vl = (vw - si * nvw) * 64 + lane;
+            const double* ch = s_chord + s_list[si] * nch;
             double acc = 0.0;
             for (int j = vl; j < nch; j += lpc) acc = acc + ch[j];
             acc = wave_sum(acc);
             if (lane == 0) s_vsum[vw] = acc;
         }
         __syncthreads();
-        if (tid < nvalid) {
+        if (tid < nl) {
             double t = s_vsum[tid * nvw];
             for (int w = 1; w < nvw; ++w) t = t + s_vsum[tid * nvw + w];
-            s_arc[tid] = t;
+            s_arc[s_list[tid]] = t;
         }
-    } else if (tid < nvalid) {
-        s_arc[tid] = 0.0;
     }
     __syncthreads();
     if (tid < nvalid) {
@@ -1285,6 +1311,7 @@ struct sspp_job {
     int insample = 0;          // sample inside the scoring kernel (SSPP_INSAMPLE=1)
     // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
     int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16, nt2 = 256;
+    int arc_all = 0;           // arc length for every candidate (else collision-free only)
     size_t lds2 = 0;
     double* d_otab = nullptr;  // collision rows in coarse-to-fine order
     int* d_ospan = nullptr;
@@ -1698,6 +1725,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     auto* j = new sspp_job();
     j->kind = 0; j->scene = scene; j->D = D; j->p = p; j->n = n; j->W = W;
     j->nknots = n + p + 1; j->sigma = a->sigma; j->seed = a->seed; j->max_batch = max_batch;
+    j->arc_all = a->arc_all ? 1 : 0;
     j->nm = scene ? (int)scene->movers.size() : 1;
     if (j->nm < 1) j->nm = 1;
     j->lpc = lanes_for(W - 1);
@@ -1881,6 +1909,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     static const int ablate = [] { const char* e = getenv("SSPP_ABLATE"); return e ? atoi(e) : 0; }();
     k.ablate = ablate;
     k.insample = j->insample;
+    k.arc_all = j->arc_all;
     SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
     if (steps < 1 || steps > kMaxSteps || (steps > 1 && (!j->c2f || d_ctrl || (j->npert > 0 && !j->insample))))
         return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..16, coarse-to-fine kernel with in-kernel sampling only");
@@ -1905,6 +1934,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         c.lpc = lanes_for(j->W - 1);
         c.nblk_step = nblk;
         c.step_stride = step_stride;
+        c.arc_all = j->arc_all;
         e = j->p == 3 ? dispatch_c2f_p<3>(c, j, o, nblk * steps, st) : dispatch_c2f_p<2>(c, j, o, nblk * steps, st);
     } else {
         e = j->p == 3 ? dispatch_sspp_p<3>(k, j, o, nblk, st) : dispatch_sspp_p<2>(k, j, o, nblk, st);

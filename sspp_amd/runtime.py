@@ -202,7 +202,9 @@ class SsppJob(_Job):
     """SamplingPathPlanner::plan's candidate loop on the GPU (include/sspp.h:194-225)."""
 
     def __init__(self, scene, knots, degree, init_ctrl, sigma, limits, check_points,
-                 seed=DEFAULT_SEED, max_batch=4096):
+                 seed=DEFAULT_SEED, max_batch=4096, arc_all=False):
+        """arc_all=False follows the reference: arc length only for collision-free candidates
+        (findBestPath scores only successful paths), +inf for the others."""
         init_ctrl = np.ascontiguousarray(np.asarray(init_ctrl, dtype=np.float64))
         n, D = init_ctrl.shape
         self.knots = _f64(knots, n + degree + 1)
@@ -212,7 +214,7 @@ class SsppJob(_Job):
         self.max_batch = int(max_batch)
         a = SsppArgs(knots=_dptr(self.knots), degree=self.degree, init_ctrl=_dptr(init_ctrl),
                      n_ctrl=n, dof=D, sigma=float(sigma), limits=_dptr(self.limits),
-                     check_points=self.W, seed=int(seed) & (2 ** 64 - 1))
+                     check_points=self.W, seed=int(seed) & (2 ** 64 - 1), arc_all=int(bool(arc_all)))
         h = C.c_void_p()
         check(lib().sspp_job_create_sspp(scene.handle if scene is not None else None, C.byref(a),
                                          self.max_batch, C.byref(h)), "job create (sspp)")

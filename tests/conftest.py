@@ -35,3 +35,14 @@ def cuda():
         pytest.skip("no GPU visible (run with -m gpu on an MI355X)")
     import torch
     return torch.device("cuda:0")
+
+
+def arc_err(got, want):
+    """Max |got - want| over finite entries; +inf when the +inf patterns differ (collision-free
+    candidates carry an arc length, colliding ones +inf — findBestPath semantics)."""
+    import numpy as np
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    if not np.array_equal(np.isinf(got), np.isinf(want)):
+        return float("inf")
+    fin = np.isfinite(want)
+    return float(np.abs(got[fin] - want[fin]).max()) if fin.any() else 0.0

@@ -12,7 +12,7 @@ import pytest
 
 from oracle import mjcf_ref
 from oracle import oracle as O
-from tests.conftest import SCENES
+from tests.conftest import SCENES, arc_err
 
 pytestmark = pytest.mark.gpu
 
@@ -61,24 +61,27 @@ KERNELS = [("1", "16", "256"), ("1", "4", "256"), ("1", "64", "64"), ("1", "16",
            ("1", "16", "64"), ("0", "16", "256")]
 
 
+@pytest.mark.parametrize("arc_all", [False, True])
 @pytest.mark.parametrize("kernel,g1,nt", KERNELS)
 @pytest.mark.parametrize("B,W", [(4096, 128), (257, 128), (1, 128), (300, 50), (100, 256), (64, 2)])
-def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g1, nt, B, W):
+def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g1, nt, B, W, arc_all):
     import sspp_amd as S
     monkeypatch.setenv("SSPP_KERNEL", kernel)
     monkeypatch.setenv("SSPP_G1", g1)
     monkeypatch.setenv("SSPP_NT", nt)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
-    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=0x5EED, max_batch=B)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=0x5EED, max_batch=B,
+                    arc_all=arc_all)
     r = run_sspp(job, B, first=1000)
     # sampling parity (Philox + Box-Muller restated on the host)
     ctrl_o = O.sample_sspp(ctrl0, 3, 0.08, np.ones(7), 0x5EED, 1000, B)
     assert np.abs(r["ctrl"] - ctrl_o).max() <= 1e-12
     # scoring parity on the exact control points the GPU scored
-    arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], W)
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], W, arc_all=arc_all)
     np.testing.assert_array_equal(r["feasible"], feas_o)
-    assert np.abs(r["arc"] - arc_o).max() <= COST_TOL
+    assert np.isinf(r["arc"]).sum() == (0 if arc_all else int((feas_o == 0).sum()))
+    assert arc_err(r["arc"], arc_o) <= COST_TOL
     idx_o, best_o = O.argmin(arc_o, feas_o)
     cost, idx, cnt = r["best"]
     assert cnt == int(feas_o.sum())
@@ -117,7 +120,7 @@ def test_score_ctrl_mode_matches_oracle(robocrane, monkeypatch, kernel, g1, nt):
     torch.cuda.synchronize()
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, ctrl, 128)
     np.testing.assert_array_equal(_np(out["feasible"]), feas_o)
-    assert np.abs(_np(out["arc"]) - arc_o).max() <= COST_TOL
+    assert arc_err(_np(out["arc"]), arc_o) <= COST_TOL
     assert S.decode_best(out["best"])[1] == O.argmin(arc_o, feas_o)[0]
 
 
@@ -196,7 +199,7 @@ def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1, nt):
     r = run_sspp(job, 2048)
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 100)
     np.testing.assert_array_equal(r["feasible"], feas_o)
-    assert np.abs(r["arc"] - arc_o).max() <= COST_TOL
+    assert arc_err(r["arc"], arc_o) <= COST_TOL
     assert r["best"][1] == O.argmin(arc_o, feas_o)[0]
 
 
