@@ -16,22 +16,23 @@ OBJDIR   = build/obj
 LIB      = $(LIBDIR)/libsspp_hip.so
 PYEXT    = $(shell $(PY) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
 PYMOD    = sspp/_sspp$(PYEXT)
+PYMOD2   = sspp/_tsp$(PYEXT)
 PYINC    = $(shell $(PY) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
 PBINC    = $(shell $(PY) -c "import pybind11;print(pybind11.get_include())")
 
 HDRS = include/sspp_hip.h $(SRC)/model.h $(SRC)/sspp_device.h $(SRC)/xml_lite.h
 
-all: $(LIB) $(PYMOD) oracle
+all: $(LIB) $(PYMOD) $(PYMOD2) oracle
 
 $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HOSTFLAGS) -c $< -o $@
 
-$(OBJDIR)/sspp_kernels.o: $(SRC)/sspp_kernels.hip $(HDRS)
+$(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(OBJDIR)/sspp_kernels.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o
+$(LIB): $(OBJDIR)/sspp_kernels.o $(OBJDIR)/ces.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
@@ -39,11 +40,15 @@ $(PYMOD): $(SRC)/sspp_pybind.cpp $(LIB) include/sspp_hip.h
 	g++ $(CXXSTD) -O2 -fPIC -shared -I$(PYINC) -I$(PBINC) -Iinclude $< -o $@ \
 	    -L$(LIBDIR) -lsspp_hip -Wl,-rpath,'$$ORIGIN/../sspp_amd/lib'
 
+$(PYMOD2): $(SRC)/tsp_pybind.cpp $(LIB) include/sspp_hip.h
+	g++ $(CXXSTD) -O2 -fPIC -shared -I$(PYINC) -I$(PBINC) -Iinclude $< -o $@ \
+	    -L$(LIBDIR) -lsspp_hip -Wl,-rpath,'$$ORIGIN/../sspp_amd/lib'
+
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf build $(LIB) $(PYMOD)
+	rm -rf build $(LIB) $(PYMOD) $(PYMOD2)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

@@ -29,6 +29,18 @@
  *                               = Sampler::sample_set (tsp_sampler.h:40-51) + PathModel::fromVias
  *                               + Evaluator::eval_one_pass (tsp_evaluator.h:18-32)
  *   sspp_job_tsp_score_vias  <- the same on caller-supplied via sets
+ *   sspp_ces_create          <- tsp::Planner(model, body, cfg, lo, hi, z_min)  tsp_planner.h:33-51
+ *                               via tsp::TaskSpacePlanner's ctor                include/sspp/tsp.h:12-55
+ *   sspp_ces_begin           <- Planner::plan prologue: reset() / initLinear   tsp_planner.h:54-75
+ *                               + seed list (mean set, forwarded best)          tsp_planner.h:78-93
+ *   sspp_ces_eval            <- Planner::plan evaluation loop                  tsp_planner.h:95-119
+ *   sspp_ces_update          <- EliteSelector::select/weights                  tsp_elites.h:13-32
+ *                               + Distribution::update/adapt                    tsp_distribution.h:31-83
+ *                               + best pick / last_best_ forwarding             tsp_planner.h:121-142
+ *   sspp_ces_plan            <- TaskSpacePlanner::plan(start, end, iterate)    include/sspp/tsp.h:58-60
+ *                               (repeated `iterations` times, no host round trip)
+ *   sspp_ces_read            <- successes()/failures()/sampled_sets()/mean()/sigma() getters
+ *                               tsp_planner.h:151-158, tsp.h:63-78
  *
  * Device pointers: every `d_` argument is device memory (hipMalloc / torch.cuda); the job
  * run functions issue only asynchronous work on `stream` (hipStream_t passed as void*; NULL =
@@ -187,6 +199,68 @@ int sspp_job_tsp_score_vias(sspp_job* job, const double* d_vias /* [B][K][4] */,
 int sspp_job_info(const sspp_job* job, int* lanes_per_candidate, int* candidates_per_block,
                   int* block_threads, size_t* lds_bytes);
 void sspp_job_free(sspp_job* job);
+
+/* ---- TaskSpacePlanner CES iteration on the device (tsp::Planner::plan) ----
+ * An iteration's candidate list is [mean set, forwarded best (iterate && last_best), samples]
+ * (n_fixed + samples slots; ranks own slots_per_rank consecutive slots each).  All state
+ * (distribution, last best, per-slot results) stays on the device; sspp_ces_read copies it
+ * out synchronously.  Random samples of iteration t use Philox ids t * samples + [0, samples). */
+typedef struct sspp_ces sspp_ces;
+typedef struct sspp_ces_config {
+    int samples;            /* PlannerConfig::samples (sample_count)                      */
+    int checks;             /* check_points                                              */
+    int total_points;       /* init_points (start + K vias + end), 3..34                 */
+    double w_collision, elite_fraction, inc, dec;
+    double sigma_floor, var_beta, mean_lr, stddev_min, stddev_max;
+    double z_min;           /* PlannerConfig::z_min: seed / sample z clamp               */
+    double dist_z_min;      /* Distribution::z_min — TaskSpacePlanner passes stddev_initial
+                               here (tsp.h:53 -> tsp_planner.h:45)             */
+    double sigma0;          /* Planner::sigma0_ = 0.3 (tsp_planner.h:177)                 */
+    const double* lo;       /* host [4] limits_min (Sampler + Distribution bounds)       */
+    const double* hi;       /* host [4] limits_max                                       */
+    double floor_z_min, floor_margin, floor_scale; /* Evaluator (0, 0.01, 10)  */
+    uint64_t seed;
+} sspp_ces_config;
+typedef struct sspp_ces_info {
+    int n_vias, n_slots, slots_per_rank, world, elite_capacity;
+    int64_t iteration;
+} sspp_ces_info;
+typedef struct sspp_ces_state {
+    int n_fixed;            /* 1 (mean set) or 2 (+ forwarded best) in the last list     */
+    int n_candidates;       /* n_fixed + samples                                          */
+    int n_success, n_elite, has_best;
+    int64_t best_slot;      /* slot of the last update's best, -1 if no success          */
+    double best_cost;
+    int64_t iteration;      /* completed updates                                          */
+} sspp_ces_state;
+typedef struct sspp_ces_buffers {   /* device pointers, n_slots entries (vias: [n_slots][K][4]) */
+    double *L, *C_nf, *C_wf, *cost;
+    uint8_t* status;        /* 1 = SolverStatus::Converged (C_nf == 0.0)                  */
+    double* vias;
+    double *mean, *sigma, *last_best;  /* [K][4] */
+    int32_t* elites;        /* slots of the last update's elites, best first             */
+} sspp_ces_buffers;
+int sspp_ces_create(const sspp_scene* scene /* SSPP_MODE_BODY */, const sspp_ces_config* cfg,
+                    int world, sspp_ces** out);
+int sspp_ces_get_info(const sspp_ces* ces, sspp_ces_info* out);
+int sspp_ces_begin(sspp_ces* ces, const double* start /* [4] */, const double* end /* [4] */,
+                   int iterate, void* stream);
+int sspp_ces_eval(sspp_ces* ces, int rank, void* stream);  /* this rank's slots */
+int sspp_ces_update(sspp_ces* ces, void* stream);           /* needs every slot's results */
+int sspp_ces_plan(sspp_ces* ces, const double* start, const double* end, int iterate,
+                  int iterations, void* stream);            /* world == 1 */
+int sspp_ces_get_buffers(const sspp_ces* ces, sspp_ces_buffers* out);
+/* multi-rank exchange: this rank's slots_per_rank slots as packed f64 records
+ * [L, C_nf, C_wf, cost, status, vias(4K)] (5 + 4K doubles each) into d_out; unpack scatters
+ * the all-gathered records of every rank (n_slots records) into the planner's arrays.     */
+int sspp_ces_pack(const sspp_ces* ces, int rank, double* d_out, void* stream);
+int sspp_ces_unpack(sspp_ces* ces, const double* d_in, void* stream);
+int sspp_ces_read(sspp_ces* ces, sspp_ces_state* state, double* L, double* C_nf, double* C_wf,
+                  double* cost, uint8_t* status, double* vias, double* mean, double* sigma,
+                  double* last_best, int32_t* elites);     /* synchronous; outputs nullable */
+int sspp_ces_set_state(sspp_ces* ces, const double* mean, const double* sigma,
+                       const double* last_best, int has_best /* -1 = keep */);
+void sspp_ces_free(sspp_ces* ces);
 
 /* ---- step executor: a planning loop's back-to-back batches in one call ----
  * Enqueues nsteps independent SamplingPathPlanner steps (each = one plan() batch of B

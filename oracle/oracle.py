@@ -35,6 +35,13 @@ class _Model(C.Structure):
     ]
 
 
+class _CesCfg(C.Structure):
+    _fields_ = [("K", C.c_int), ("frac", C.c_double), ("inc", C.c_double), ("dec", C.c_double),
+                ("sigma_floor", C.c_double), ("var_beta", C.c_double), ("mean_lr", C.c_double),
+                ("sd_min", C.c_double), ("sd_max", C.c_double), ("dist_z_min", C.c_double),
+                ("lo", C.c_double * 4), ("hi", C.c_double * 4), ("sequential", C.c_int)]
+
+
 _lib = None
 
 
@@ -78,6 +85,10 @@ def lib():
         L.or_argmin.argtypes = [_d, _u8, C.c_int64, C.POINTER(C.c_double)]
         L.or_tsp_score.argtypes = [C.c_void_p, _d, _d, _d, C.c_int, C.c_int64, C.c_int,
                                    C.c_double, C.c_int, C.c_int, _d, _d, _d, _u8, _d]
+        L.or_ces_update.restype = C.c_int
+        L.or_ces_update.argtypes = [C.POINTER(_CesCfg), _d, _u8, _d, C.c_int64, _d, _d, _d,
+                                    C.POINTER(C.c_int), _i32, C.POINTER(C.c_int),
+                                    C.POINTER(C.c_int64)]
         L.or_tsp_best.restype = C.c_int64
         L.or_tsp_best.argtypes = [_d, _u8, C.c_int64, C.POINTER(C.c_double)]
         _lib = L
@@ -288,3 +299,80 @@ def tsp_best(cost, status):
     best = C.c_double()
     idx = lib().or_tsp_best(cost, st, len(cost), C.byref(best))
     return int(idx), best.value
+
+
+# ------------------------------------------------------------------ TaskSpacePlanner CES
+CES_DEFAULTS = dict(frac=0.3, inc=1.5, dec=0.95, sigma_floor=0.0, var_beta=0.2, mean_lr=0.5,
+                    sd_min=0.01, sd_max=0.5, dist_z_min=0.3, lo=(-2.0,) * 4, hi=(2.0,) * 4)
+
+
+def ces_update(cost, status, vias, mean, sigma, last_best, has_best, sequential=False, **cfg):
+    """tsp::Planner::plan's update (tsp_planner.h:121-142) on one iteration's candidate list.
+    Returns (mean, sigma, last_best, has_best, n_success, elites, best_slot)."""
+    c = dict(CES_DEFAULTS, **cfg)
+    vias = _f64(vias)
+    n, K = vias.shape[0], vias.shape[1]
+    cc = _CesCfg(K=K, frac=c["frac"], inc=c["inc"], dec=c["dec"], sigma_floor=c["sigma_floor"],
+                 var_beta=c["var_beta"], mean_lr=c["mean_lr"], sd_min=c["sd_min"],
+                 sd_max=c["sd_max"], dist_z_min=c["dist_z_min"],
+                 lo=(C.c_double * 4)(*c["lo"]), hi=(C.c_double * 4)(*c["hi"]),
+                 sequential=int(bool(sequential)))
+    mean, sigma = _f64(mean).reshape(K, 4).copy(), _f64(sigma).reshape(K, 4).copy()
+    lb = _f64(last_best).reshape(K, 4).copy()
+    hb = C.c_int(int(bool(has_best)))
+    elites = np.zeros(max(n, 1), np.int32)
+    ne, bs = C.c_int(), C.c_int64()
+    ns = lib().or_ces_update(C.byref(cc), _f64(cost), np.ascontiguousarray(status, np.uint8), vias,
+                             n, mean, sigma, lb, C.byref(hb), elites, C.byref(ne), C.byref(bs))
+    return mean, sigma, lb, bool(hb.value), ns, elites[:ne.value].copy(), int(bs.value)
+
+
+def ces_reset(start, end, total_points, z_min=0.0, dist_z_min=0.3, sigma0=0.3, sd_min=0.01,
+              sd_max=0.5, sigma_floor=0.0, lo=(-2.0,) * 4, hi=(2.0,) * 4):
+    """Planner::reset + Distribution::reset (tsp_planner.h:54-69, tsp_distribution.h:16-29)."""
+    K = total_points - 2
+    start, end = _f64(start), _f64(end)
+    mean = np.zeros((K, 4))
+    for i in range(K):
+        t = (i + 1) / (total_points - 1)
+        for d in range(4):
+            v = (1.0 - t) * start[d] + t * end[d]
+            if d == 2:
+                v = max(v, z_min)
+                v = v if v >= dist_z_min else dist_z_min
+            v = lo[d] if v < lo[d] else (hi[d] if hi[d] < v else v)
+            mean[i, d] = v
+    s = sigma0
+    s = sd_min if s < sd_min else s
+    s = sd_max if s > sd_max else s
+    s = sigma_floor if s < sigma_floor else s
+    return mean, np.full((K, 4), s)
+
+
+def ces_plan(scene, start, end, iterations, samples, checks, total_points=3, seed=0x5EED,
+             z_min=0.0, w_collision=1.0, nthreads=0, sequential=False, **cfg):
+    """CPU restatement of TaskSpacePlanner::plan(start, end, iterate) repeated `iterations`
+    times (first call iterate=False): seeds, evaluation, update.  Same Philox ids as the GPU
+    (iteration t samples t * samples + [0, samples)).  Returns the per-iteration records."""
+    c = dict(CES_DEFAULTS, **cfg)
+    K = total_points - 2
+    mean, sigma = ces_reset(start, end, total_points, z_min, c["dist_z_min"], 0.3, c["sd_min"],
+                            c["sd_max"], c["sigma_floor"], c["lo"], c["hi"])
+    lb, hb = np.zeros((K, 4)), False
+    out = []
+    for t in range(iterations):
+        seeds = [np.where(np.arange(4) == 2, np.maximum(mean, z_min), mean)]
+        if hb:
+            seeds.append(lb.copy())
+        smp = sample_tsp(mean, sigma, c["lo"], c["hi"], z_min, seed, t * samples, samples)
+        vias = np.concatenate([np.array(seeds).reshape(-1, K, 4), smp.reshape(-1, K, 4)])
+        L, Cnf, Cwf, st, cost = tsp_score(scene, start, end, vias, checks, w_collision,
+                                          nthreads=nthreads)
+        rec = dict(vias=vias, L=L, C_nf=Cnf, C_wf=Cwf, status=st, cost=cost,
+                   mean_in=mean.copy(), sigma_in=sigma.copy())
+        mean, sigma, lb, hb, ns, el, bs = ces_update(cost, st, vias, mean, sigma, lb, hb,
+                                                     sequential=sequential, **cfg)
+        rec.update(mean=mean, sigma=sigma, last_best=lb, has_best=hb, n_success=ns, elites=el,
+                   best_slot=bs)
+        out.append(rec)
+    return out

@@ -976,3 +976,93 @@ int64_t or_tsp_best(const double* cost, const uint8_t* status, int64_t B, double
     /* tsp_planner.h:131-134 min_element over successes; lowest index on ties */
     return or_argmin(cost, status, B, best_cost);
 }
+
+/* ================================================================ TaskSpacePlanner CES update
+ * tsp::Planner::plan after the evaluation loop (include/sspp/tsp_planner.h:121-142):
+ *   successes -> EliteSelector::select (tsp_elites.h:13-22: top k = max(1, int(n * frac)) by
+ *   L + w * C_wf), ::weights (24-32: log(k + 0.5) - log(i + 1), normalised),
+ *   Distribution::update (tsp_distribution.h:52-83), best = std::min_element, adapt (31-38).
+ * Candidate order = slot order and ties go to the lowest slot.  sequential = 1
+ * sums in the reference's order; 0 in the GPU's canonical wave order (or_canon_sum, 64 lanes). */
+typedef struct { double cost; int64_t slot; } or_ces_key;
+
+static int or_ces_cmp(const void* a, const void* b) {
+    const or_ces_key* x = (const or_ces_key*)a;
+    const or_ces_key* y = (const or_ces_key*)b;
+    if (x->cost < y->cost) return -1;
+    if (y->cost < x->cost) return 1;
+    return (x->slot > y->slot) - (x->slot < y->slot);
+}
+
+static double or_ces_clamp_sd(double s, const or_ces_cfg* c) {
+    s = s < c->sd_min ? c->sd_min : s;
+    s = s > c->sd_max ? c->sd_max : s;
+    return s < c->sigma_floor ? c->sigma_floor : s;
+}
+
+static double or_wrap_diff(double a, double b, double mn, double mx) {
+    const double range = mx - mn;
+    double d = a - b;
+    while (d > 0.5 * range) d -= range;
+    while (d < -0.5 * range) d += range;
+    return d;
+}
+
+static double or_ces_sum(const double* x, int n, int sequential) {
+    return sequential ? seq_sum(x, n) : or_canon_sum(x, n, 64);
+}
+
+int or_ces_update(const or_ces_cfg* c, const double* cost, const uint8_t* status,
+                  const double* vias, int64_t n, double* mean, double* sigma, double* last_best,
+                  int* has_best, int32_t* elites, int* n_elite, int64_t* best_slot) {
+    const int K = c->K, KD = 4 * K;
+    int64_t ns = 0;
+    for (int64_t i = 0; i < n; ++i) ns += status[i] != 0;
+    *n_elite = 0;
+    *best_slot = -1;
+    if (ns == 0) {
+        for (int q = 0; q < KD; ++q) sigma[q] = or_ces_clamp_sd(sigma[q] * c->inc, c);
+        return 0;
+    }
+    or_ces_key* keys = (or_ces_key*)malloc(sizeof(or_ces_key) * (size_t)ns);
+    int64_t m = 0;
+    for (int64_t i = 0; i < n; ++i)
+        if (status[i]) { keys[m].cost = cost[i]; keys[m].slot = i; ++m; }
+    qsort(keys, (size_t)ns, sizeof(or_ces_key), or_ces_cmp);
+    int k = (int)((double)ns * c->frac);
+    if (k < 1) k = 1;
+    double* w = (double*)malloc(sizeof(double) * (size_t)k);
+    double* x = (double*)malloc(sizeof(double) * (size_t)k);
+    const double lk = log((double)k + 0.5);
+    for (int j = 0; j < k; ++j) x[j] = lk - log((double)j + 1.0);
+    const double sumw = or_ces_sum(x, k, c->sequential);
+    for (int j = 0; j < k; ++j) w[j] = x[j] / sumw;
+    for (int q = 0; q < KD; ++q) {
+        const int d = q & 3;
+        for (int j = 0; j < k; ++j) x[j] = w[j] * vias[keys[j].slot * KD + q];
+        const double em = or_ces_sum(x, k, c->sequential);
+        const double m0 = mean[q];
+        double nm = m0 + c->mean_lr * (em - m0);
+        if (d == 2) nm = nm < c->dist_z_min ? c->dist_z_min : nm;
+        nm = nm < c->lo[d] ? c->lo[d] : (c->hi[d] < nm ? c->hi[d] : nm);
+        const int wrap = d == 3 && c->lo[3] != c->hi[3];
+        for (int j = 0; j < k; ++j) {
+            const double v = vias[keys[j].slot * KD + q];
+            const double df = wrap ? or_wrap_diff(v, nm, c->lo[3], c->hi[3]) : v - nm;
+            x[j] = w[j] * (df * df);
+        }
+        const double ve = or_ces_sum(x, k, c->sequential);
+        const double pv = sigma[q] * sigma[q];
+        const double blend = (1.0 - c->var_beta) * pv + c->var_beta * ve;
+        double sg = or_ces_clamp_sd(sqrt(blend), c);
+        sigma[q] = or_ces_clamp_sd(sg * c->dec, c);
+        mean[q] = nm;
+    }
+    for (int q = 0; q < KD; ++q) last_best[q] = vias[keys[0].slot * KD + q];
+    *has_best = 1;
+    *best_slot = keys[0].slot;
+    for (int j = 0; j < k; ++j) elites[j] = (int32_t)keys[j].slot;
+    *n_elite = k;
+    free(keys); free(w); free(x);
+    return (int)ns;
+}

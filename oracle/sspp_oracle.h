@@ -127,6 +127,20 @@ int    or_tsp_score(const or_scene* s, const double* start, const double* end,
                     double* L, double* Cnf, double* Cwf, uint8_t* status, double* cost);
 int64_t or_tsp_best(const double* cost, const uint8_t* status, int64_t B, double* best_cost);
 
+/* ---- TaskSpacePlanner CES update (tsp_planner.h:121-142, tsp_elites.h, tsp_distribution.h) ---- */
+typedef struct or_ces_cfg {
+    int K;
+    double frac, inc, dec, sigma_floor, var_beta, mean_lr, sd_min, sd_max, dist_z_min;
+    double lo[4], hi[4];
+    int sequential;   /* 1: reference summation order; 0: GPU canonical wave order */
+} or_ces_cfg;
+/* in/out: mean, sigma, last_best [K][4], has_best; out: elites (slots, best first), n_elite,
+   best_slot (-1 if no success).  Returns the number of successes. */
+int    or_ces_update(const or_ces_cfg* c, const double* cost, const uint8_t* status,
+                     const double* vias /* [n][K][4] */, int64_t n, double* mean, double* sigma,
+                     double* last_best, int* has_best, int32_t* elites, int* n_elite,
+                     int64_t* best_slot);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,6 +63,33 @@ class TspArgs(C.Structure):
                 ("floor_margin", C.c_double), ("floor_scale", C.c_double)]
 
 
+class CesConfig(C.Structure):
+    _fields_ = [("samples", C.c_int), ("checks", C.c_int), ("total_points", C.c_int),
+                ("w_collision", C.c_double), ("elite_fraction", C.c_double), ("inc", C.c_double),
+                ("dec", C.c_double), ("sigma_floor", C.c_double), ("var_beta", C.c_double),
+                ("mean_lr", C.c_double), ("stddev_min", C.c_double), ("stddev_max", C.c_double),
+                ("z_min", C.c_double), ("dist_z_min", C.c_double), ("sigma0", C.c_double),
+                ("lo", C.POINTER(C.c_double)), ("hi", C.POINTER(C.c_double)),
+                ("floor_z_min", C.c_double), ("floor_margin", C.c_double),
+                ("floor_scale", C.c_double), ("seed", C.c_uint64)]
+
+
+class CesInfo(C.Structure):
+    _fields_ = [("n_vias", C.c_int), ("n_slots", C.c_int), ("slots_per_rank", C.c_int),
+                ("world", C.c_int), ("elite_capacity", C.c_int), ("iteration", C.c_int64)]
+
+
+class CesState(C.Structure):
+    _fields_ = [("n_fixed", C.c_int), ("n_candidates", C.c_int), ("n_success", C.c_int),
+                ("n_elite", C.c_int), ("has_best", C.c_int), ("best_slot", C.c_int64),
+                ("best_cost", C.c_double), ("iteration", C.c_int64)]
+
+
+class CesBuffers(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("L", "C_nf", "C_wf", "cost", "status", "vias", "mean",
+                                          "sigma", "last_best", "elites")]
+
+
 _vp, _i64, _d, _i = C.c_void_p, C.c_int64, C.POINTER(C.c_double), C.c_int
 
 SIGNATURES = {
@@ -102,6 +129,19 @@ SIGNATURES = {
                                        C.POINTER(C.c_uint8), C.POINTER(Best)]),
     "sspp_sample_ctrl_host": (C.c_int, [_d, _i, _d, _i, _i, C.c_double, _d, C.c_uint64, _i64,
                                         _i64, _d]),
+    "sspp_ces_create": (C.c_int, [_vp, C.POINTER(CesConfig), _i, C.POINTER(_vp)]),
+    "sspp_ces_get_info": (C.c_int, [_vp, C.POINTER(CesInfo)]),
+    "sspp_ces_begin": (C.c_int, [_vp, _d, _d, _i, _vp]),
+    "sspp_ces_eval": (C.c_int, [_vp, _i, _vp]),
+    "sspp_ces_update": (C.c_int, [_vp, _vp]),
+    "sspp_ces_plan": (C.c_int, [_vp, _d, _d, _i, _i, _vp]),
+    "sspp_ces_get_buffers": (C.c_int, [_vp, C.POINTER(CesBuffers)]),
+    "sspp_ces_read": (C.c_int, [_vp, C.POINTER(CesState), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _vp, _vp]),
+    "sspp_ces_set_state": (C.c_int, [_vp, _vp, _vp, _vp, _i]),
+    "sspp_ces_pack": (C.c_int, [_vp, _i, _vp, _vp]),
+    "sspp_ces_unpack": (C.c_int, [_vp, _vp, _vp]),
+    "sspp_ces_free": (None, [_vp]),
 }
 
 

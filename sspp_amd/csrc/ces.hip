@@ -1,0 +1,606 @@
+// ces.hip — tsp::Planner's cross-entropy (CES) iteration on the device (gfx950).
+//
+// Reference (include/sspp/tsp_planner.h:72-145, tsp_elites.h:13-32, tsp_distribution.h:16-83):
+//   seeds = [mean set, forwarded best (iterate && last_best_), samples x Sampler::sample_set]
+//   evaluate every seed (k_tsp in CES slot mode, sspp_kernels.hip)
+//   successes -> top-k by L + w * C_wf (k = max(1, int(|succ| * elite_fraction)))
+//             -> CES log weights -> Distribution::update -> best = min cost -> adapt(true)
+//   no success -> adapt(false)
+// Everything between two evaluations runs in one workgroup of k_ces_update: no host round
+// trip, so a planning loop of many iterations is a chain of asynchronous launches.
+//
+// Deliberate, documented differences:
+//   * candidates are ordered by slot (mean set, forwarded best, samples in Philox order); the
+//     reference's order of successes_ depends on OpenMP merge timing.  Ties in
+//     the elite sort and the best pick go to the lowest slot.
+//   * the weighted sums of Distribution::update and the weight normaliser use the canonical
+//     wave order (lane j % 64 partials, xor butterfly) that oracle/sspp_oracle.c restates;
+//     the reference sums sequentially (differences ~1e-16 relative).
+//   * log(k + 0.5) and log(i + 1) come from host tables (glibc log), so every weight is the
+//     reference's value bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "model.h"
+
+namespace {
+
+constexpr int kCesThreads = 1024;
+constexpr int kCesWaves = kCesThreads / 64;
+constexpr int kMaxVias = 32;
+constexpr int kEliteCap = 8192;  // LDS: 8192 x (8 B key + 4 B slot) = 96 KiB
+
+struct CesHdr {
+    int nfixed;      // fixed slots (mean set [+ forwarded best]) of the current iteration
+    int has_best;    // Planner::last_best_ is set
+    int nsucc;       // successes of the last update
+    int nelite;      // elites of the last update
+    long long best_slot;
+    double best_cost;
+    long long iter;  // completed updates (informational)
+    long long pad;
+};
+
+struct CesK {
+    int K, nslots, samples, cap;
+    double frac, inc, dec, sigma_floor, var_beta, mean_lr, sd_min, sd_max, dist_z_min, z_min;
+    double lo[4], hi[4];
+};
+
+struct CesReset {
+    double mean0[kMaxVias * 4];  // Distribution::reset(mean0) values (z + bound clamps applied)
+    double sigma0;               // sigma0_ after the stddev clamps
+};
+
+// order-preserving map double -> u64 (-0 folded onto +0: IEEE compares them equal)
+__device__ __forceinline__ unsigned long long okey(double x) {
+    if (x == 0.0) x = 0.0;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ double clamp_sd(double s, const CesK& c) {
+    s = s < c.sd_min ? c.sd_min : s;          // cwiseMax(stddev_min)
+    s = s > c.sd_max ? c.sd_max : s;          // cwiseMin(stddev_max)
+    return s < c.sigma_floor ? c.sigma_floor : s;  // cwiseMax(sigma_floor)
+}
+
+// Distribution::wrap_angle_diff (tsp_distribution.h:44-50)
+__device__ __forceinline__ double wrap_diff(double a, double b, double mn, double mx) {
+    const double range = mx - mn;
+    double d = a - b;
+    while (d > 0.5 * range) d -= range;
+    while (d < -0.5 * range) d += range;
+    return d;
+}
+
+// exclusive block scan of a 0/1 flag; *total receives the block's count (all threads call)
+__device__ __forceinline__ int block_scan_flag(bool f, int* s_w, int* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(f);
+    const int in_wave = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_w[w] = __popcll(m);
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int k = 0; k < kCesWaves; ++k) {
+        const int v = s_w[k];
+        before += k < w ? v : 0;
+        tot += v;
+    }
+    __syncthreads();
+    *total = tot;
+    return before + in_wave;
+}
+
+// plan()'s prologue: reset() (iterate == 0) or keep the distribution, then the iteration's
+// fixed seeds: mean set with z >= cfg.z_min (tsp_planner.h:82-84) and the forwarded best.
+__global__ __launch_bounds__(128) void k_ces_begin(CesK c, int iterate, CesReset r, CesHdr* h,
+                                                   double* mean, double* sigma,
+                                                   const double* lbest, double* fixed) {
+    const int e = threadIdx.x;
+    const int hb = iterate ? h->has_best : 0;
+    if (e < c.K * 4) {
+        double m = iterate ? mean[e] : r.mean0[e];
+        if (!iterate) { mean[e] = m; sigma[e] = r.sigma0; }
+        const int d = e & 3;
+        fixed[e] = (d == 2 && m < c.z_min) ? c.z_min : m;
+        fixed[c.K * 4 + e] = lbest[e];
+    }
+    if (e == 0) {
+        if (!iterate) h->has_best = 0;
+        h->nfixed = 1 + hb;
+        h->nsucc = 0;
+        h->nelite = 0;
+        h->best_slot = -1;
+        h->best_cost = INFINITY;
+    }
+}
+
+// Elite selection + Distribution::update + best pick + adapt, one workgroup.
+__global__ __launch_bounds__(kCesThreads) void k_ces_update(
+    CesK c, const double* __restrict__ cost, const unsigned char* __restrict__ status,
+    const double* __restrict__ vias, const double* __restrict__ LT, const double* __restrict__ LH,
+    CesHdr* h, double* mean, double* sigma, double* lbest, int* elite_out) {
+    __shared__ unsigned long long s_key[kEliteCap];  // keys, later the weights (as double)
+    __shared__ int s_idx[kEliteCap];
+    __shared__ int s_hist[256];
+    __shared__ int s_w[kCesWaves];
+    __shared__ int s_sel[4];
+    __shared__ double s_sumw;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nslots = c.nslots;
+
+    // ---- successes
+    int nsucc = 0;
+    for (int base = 0; base < nslots; base += kCesThreads) {
+        const int i = base + tid;
+        int tot;
+        (void)block_scan_flag(i < nslots && status[i], s_w, &tot);
+        nsucc += tot;
+    }
+    if (nsucc == 0) {  // adapt(false)
+        if (tid < c.K * 4) sigma[tid] = clamp_sd(sigma[tid] * c.inc, c);
+        if (tid == 0) { h->nsucc = 0; h->nelite = 0; h->best_slot = -1; h->best_cost = INFINITY; h->iter++; }
+        return;
+    }
+    const int k = (int)((double)nsucc * c.frac) < 1 ? 1 : (int)((double)nsucc * c.frac);
+
+    // ---- radix select of the k-th smallest key among successes (8 passes of 8 bits)
+    unsigned long long prefix = 0ull, pmask = 0ull;
+    int kk = k;
+    for (int pass = 7; pass >= 0; --pass) {
+        for (int b = tid; b < 256; b += kCesThreads) s_hist[b] = 0;
+        __syncthreads();
+        const int sh = 8 * pass;
+        for (int i = tid; i < nslots; i += kCesThreads) {
+            if (!status[i]) continue;
+            const unsigned long long key = okey(cost[i]);
+            if ((key & pmask) == prefix) atomicAdd(&s_hist[(key >> sh) & 255ull], 1);
+        }
+        __syncthreads();
+        if (wv == 0) {  // inclusive scan of 4 bins per lane, first bin reaching kk
+            int v[4], sum = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { v[q] = s_hist[4 * lane + q]; sum += v[q]; }
+            int inc = sum;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int o = __shfl_up(inc, off, 64);
+                if (lane >= off) inc += o;
+            }
+            const unsigned long long hit = __ballot(inc >= kk);
+            const int first = __ffsll((long long)hit) - 1;
+            if (lane == first) {
+                int cum = inc - sum, b = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (cum + v[q] >= kk) { b = q; break; }
+                    cum += v[q];
+                }
+                s_sel[0] = 4 * lane + b;
+                s_sel[1] = kk - cum;
+            }
+        }
+        __syncthreads();
+        prefix |= (unsigned long long)s_sel[0] << sh;
+        pmask |= 0xFFull << sh;
+        kk = s_sel[1];
+        __syncthreads();
+    }
+    const unsigned long long T = prefix;
+    const int need_eq = kk;  // elites with key == T, lowest slots first
+
+    // ---- ordered compaction of the elites (slot order), then bitonic sort on (key, slot)
+    int eq_seen = 0, nsel = 0;
+    for (int base = 0; base < nslots; base += kCesThreads) {
+        const int i = base + tid;
+        unsigned long long key = ~0ull;
+        const bool ok = i < nslots && status[i];
+        if (ok) key = okey(cost[i]);
+        int eq_tot;
+        const int eq_rank = eq_seen + block_scan_flag(ok && key == T, s_w, &eq_tot);
+        const bool sel = ok && (key < T || (key == T && eq_rank < need_eq));
+        int sel_tot;
+        const int pos = nsel + block_scan_flag(sel, s_w, &sel_tot);
+        if (sel) { s_key[pos] = key; s_idx[pos] = i; }
+        eq_seen += eq_tot;
+        nsel += sel_tot;
+    }
+    int P = 1;
+    while (P < k) P <<= 1;
+    for (int i = k + tid; i < P; i += kCesThreads) { s_key[i] = ~0ull; s_idx[i] = INT_MAX; }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < (P >> 1); t += kCesThreads) {
+                const int lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const unsigned long long ka = s_key[lo], kb = s_key[hi];
+                const int ia = s_idx[lo], ib = s_idx[hi];
+                const bool gt = ka > kb || (ka == kb && ia > ib);
+                if (gt == up) { s_key[lo] = kb; s_key[hi] = ka; s_idx[lo] = ib; s_idx[hi] = ia; }
+            }
+            __syncthreads();
+        }
+    }
+
+    // ---- CES log weights (tsp_elites.h:24-32): w_j = log(k + 0.5) - log(j + 1), normalised
+    const double lk = LH[k];
+    if (wv == 0) {
+        double a = 0.0;
+        for (int j = lane; j < k; j += 64) a = a + (lk - LT[j + 1]);
+        a = wave_sum64(a);
+        if (lane == 0) s_sumw = a;
+    }
+    __syncthreads();
+    double* s_wt = reinterpret_cast<double*>(s_key);
+    const double sumw = s_sumw;
+    for (int j = tid; j < k; j += kCesThreads) s_wt[j] = (lk - LT[j + 1]) / sumw;
+    __syncthreads();
+
+    // ---- Distribution::update (tsp_distribution.h:52-83) + adapt(true), one wave per (via, dim)
+    const int K = c.K, KD = 4 * K;
+    for (int q = wv; q < KD; q += kCesWaves) {
+        const int d = q & 3;
+        double a = 0.0;
+        for (int j = lane; j < k; j += 64) a = a + s_wt[j] * vias[(long long)s_idx[j] * KD + q];
+        const double em = wave_sum64(a);
+        const double m0 = mean[q];
+        double nm = m0 + c.mean_lr * (em - m0);
+        if (d == 2) nm = nm < c.dist_z_min ? c.dist_z_min : nm;
+        nm = nm < c.lo[d] ? c.lo[d] : (c.hi[d] < nm ? c.hi[d] : nm);  // std::clamp
+        const bool wrap = d == 3 && c.lo[3] != c.hi[3];
+        double v = 0.0;
+        for (int j = lane; j < k; j += 64) {
+            const double x = vias[(long long)s_idx[j] * KD + q];
+            const double df = wrap ? wrap_diff(x, nm, c.lo[3], c.hi[3]) : x - nm;
+            v = v + s_wt[j] * (df * df);
+        }
+        const double ve = wave_sum64(v);
+        const double s0 = sigma[q];
+        const double pv = s0 * s0;
+        const double blend = (1.0 - c.var_beta) * pv + c.var_beta * ve;
+        double sg = clamp_sd(sqrt(blend), c);
+        sg = clamp_sd(sg * c.dec, c);  // adapt(true)
+        if (lane == 0) { mean[q] = nm; sigma[q] = sg; }
+    }
+
+    // ---- best = first minimum in slot order (std::min_element): the sort's first entry
+    const int b = s_idx[0];
+    for (int e = tid; e < KD; e += kCesThreads) lbest[e] = vias[(long long)b * KD + e];
+    for (int j = tid; j < k; j += kCesThreads) elite_out[j] = s_idx[j];
+    if (tid == 0) {
+        h->has_best = 1;
+        h->nsucc = nsucc;
+        h->nelite = k;
+        h->best_slot = b;
+        h->best_cost = cost[b];
+        h->iter++;
+    }
+}
+
+// Multi-rank exchange: a rank's slots as packed records [L, C_nf, C_wf, cost, status, vias]
+__global__ __launch_bounds__(256) void k_ces_pack(int n, int KD, const double* L, const double* Cnf,
+                                                  const double* Cwf, const double* cost,
+                                                  const unsigned char* st, const double* vias,
+                                                  double* out) {
+    const int R = 5 + KD;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < (long long)n * R;
+         e += (long long)gridDim.x * 256) {
+        const int i = (int)(e / R), f = (int)(e - (long long)i * R);
+        double v;
+        if (f == 0) v = L[i];
+        else if (f == 1) v = Cnf[i];
+        else if (f == 2) v = Cwf[i];
+        else if (f == 3) v = cost[i];
+        else if (f == 4) v = (double)st[i];
+        else v = vias[(long long)i * KD + (f - 5)];
+        out[e] = v;
+    }
+}
+__global__ __launch_bounds__(256) void k_ces_unpack(int n, int KD, const double* in, double* L,
+                                                    double* Cnf, double* Cwf, double* cost,
+                                                    unsigned char* st, double* vias) {
+    const int R = 5 + KD;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < (long long)n * R;
+         e += (long long)gridDim.x * 256) {
+        const int i = (int)(e / R), f = (int)(e - (long long)i * R);
+        const double v = in[e];
+        if (f == 0) L[i] = v;
+        else if (f == 1) Cnf[i] = v;
+        else if (f == 2) Cwf[i] = v;
+        else if (f == 3) cost[i] = v;
+        else if (f == 4) st[i] = (unsigned char)v;
+        else vias[(long long)i * KD + (f - 5)] = v;
+    }
+}
+
+int hip_err(hipError_t e, const char* what) {
+    return sspp::set_error(SSPP_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+struct sspp_ces {
+    sspp_job* job = nullptr;
+    sspp_ces_config cfg{};
+    int K = 0, world = 1, spr = 0, nslots = 0, cap = 0;
+    long long iter = 0;  // completed evaluations: Philox ids of iteration t start at t * samples
+    double lo[4], hi[4];
+    double start[4] = {0, 0, 0, 0}, end[4] = {0, 0, 0, 0};
+    CesHdr* d_hdr = nullptr;
+    double *d_mean = nullptr, *d_sigma = nullptr, *d_lbest = nullptr, *d_fixed = nullptr;
+    double *d_L = nullptr, *d_Cnf = nullptr, *d_Cwf = nullptr, *d_cost = nullptr, *d_vias = nullptr;
+    unsigned char* d_status = nullptr;
+    int* d_elite = nullptr;
+    double *d_LT = nullptr, *d_LH = nullptr;
+};
+
+static CesK ces_k(const sspp_ces* p) {
+    CesK c{};
+    c.K = p->K; c.nslots = p->nslots; c.samples = p->cfg.samples; c.cap = p->cap;
+    c.frac = p->cfg.elite_fraction; c.inc = p->cfg.inc; c.dec = p->cfg.dec;
+    c.sigma_floor = p->cfg.sigma_floor; c.var_beta = p->cfg.var_beta; c.mean_lr = p->cfg.mean_lr;
+    c.sd_min = p->cfg.stddev_min; c.sd_max = p->cfg.stddev_max;
+    c.dist_z_min = p->cfg.dist_z_min; c.z_min = p->cfg.z_min;
+    for (int i = 0; i < 4; ++i) { c.lo[i] = p->lo[i]; c.hi[i] = p->hi[i]; }
+    return c;
+}
+
+extern "C" {
+
+void sspp_ces_free(sspp_ces* p) {
+    if (!p) return;
+    if (p->job) sspp_job_free(p->job);
+    for (void* q : {(void*)p->d_hdr, (void*)p->d_mean, (void*)p->d_sigma, (void*)p->d_lbest,
+                    (void*)p->d_fixed, (void*)p->d_L, (void*)p->d_Cnf, (void*)p->d_Cwf,
+                    (void*)p->d_cost, (void*)p->d_vias, (void*)p->d_status, (void*)p->d_elite,
+                    (void*)p->d_LT, (void*)p->d_LH})
+        if (q) (void)hipFree(q);
+    delete p;
+}
+
+int sspp_ces_create(const sspp_scene* scene, const sspp_ces_config* cfg, int world, sspp_ces** out) {
+    sspp::clear_error();
+    if (!scene || !cfg || !out || !cfg->lo || !cfg->hi)
+        return sspp::set_error(SSPP_E_INVAL, "sspp_ces_create: null argument");
+    const int K = cfg->total_points - 2;
+    if (K < 1 || K > kMaxVias)
+        return sspp::set_error(SSPP_E_INVAL, "total_points must be in [3, 34] (1..32 via points)");
+    if (cfg->samples < 0 || cfg->checks < 1) return sspp::set_error(SSPP_E_INVAL, "samples >= 0, checks >= 1");
+    if (world < 1) return sspp::set_error(SSPP_E_INVAL, "world must be >= 1");
+    if (!(cfg->elite_fraction >= 0.0)) return sspp::set_error(SSPP_E_INVAL, "elite_fraction must be >= 0");
+    const long long maxslots = (long long)cfg->samples + 2;
+    long long cap = (long long)((double)maxslots * cfg->elite_fraction);
+    if (cap < 1) cap = 1;
+    if (cap > kEliteCap)
+        return sspp::set_error(SSPP_E_UNSUPPORTED, "(sample_count + 2) * elite_fraction exceeds 8192 elites");
+    auto* p = new sspp_ces();
+    p->cfg = *cfg;
+    p->cfg.lo = p->cfg.hi = nullptr;
+    p->K = K; p->world = world; p->cap = (int)cap;
+    for (int i = 0; i < 4; ++i) { p->lo[i] = cfg->lo[i]; p->hi[i] = cfg->hi[i]; }
+    p->spr = (int)((maxslots + world - 1) / world);
+    p->nslots = p->spr * world;
+    std::vector<double> zeros(4 * K, 0.0), start(4, 0.0);
+    sspp_tsp_args a{};
+    a.start = start.data(); a.end = start.data(); a.n_vias = K; a.check_points = cfg->checks;
+    a.w_collision = cfg->w_collision; a.mean = zeros.data(); a.sigma = zeros.data();
+    a.lo = p->lo; a.hi = p->hi; a.z_min = cfg->z_min; a.seed = cfg->seed;
+    a.floor_z_min = cfg->floor_z_min; a.floor_margin = cfg->floor_margin; a.floor_scale = cfg->floor_scale;
+    int rc = sspp_job_create_tsp(scene, &a, p->spr, &p->job);
+    if (rc) { delete p; return rc; }
+    const size_t ns = (size_t)p->nslots, kd = (size_t)4 * K;
+    std::vector<double> LT(cap + 2), LH(cap + 2);
+    for (long long m = 0; m <= cap + 1; ++m) {
+        LT[m] = m ? std::log((double)m) : 0.0;            // log(i + 1.0), i = m - 1
+        LH[m] = std::log((double)m + 0.5);                // log(k + 0.5)
+    }
+    hipError_t e;
+    if ((e = hipMalloc((void**)&p->d_hdr, sizeof(CesHdr))) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_mean, sizeof(double) * kd)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_sigma, sizeof(double) * kd)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_lbest, sizeof(double) * kd)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_fixed, sizeof(double) * 2 * kd)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_L, sizeof(double) * ns)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_Cnf, sizeof(double) * ns)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_Cwf, sizeof(double) * ns)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_cost, sizeof(double) * ns)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_vias, sizeof(double) * ns * kd)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_status, ns)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_elite, sizeof(int) * cap)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_LT, sizeof(double) * LT.size())) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_LH, sizeof(double) * LH.size())) != hipSuccess ||
+        (e = hipMemcpy(p->d_LT, LT.data(), sizeof(double) * LT.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(p->d_LH, LH.data(), sizeof(double) * LH.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(p->d_hdr, 0, sizeof(CesHdr))) != hipSuccess ||
+        (e = hipMemset(p->d_lbest, 0, sizeof(double) * kd)) != hipSuccess ||
+        (e = hipMemset(p->d_mean, 0, sizeof(double) * kd)) != hipSuccess ||
+        (e = hipMemset(p->d_sigma, 0, sizeof(double) * kd)) != hipSuccess ||
+        (e = hipMemset(p->d_status, 0, ns)) != hipSuccess) {
+        rc = hip_err(e, "sspp_ces_create allocation");
+        sspp_ces_free(p);
+        return rc;
+    }
+    *out = p;
+    return SSPP_OK;
+}
+
+int sspp_ces_get_info(const sspp_ces* p, sspp_ces_info* out) {
+    if (!p || !out) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_get_info: null argument");
+    out->n_vias = p->K;
+    out->n_slots = p->nslots;
+    out->slots_per_rank = p->spr;
+    out->world = p->world;
+    out->elite_capacity = p->cap;
+    out->iteration = p->iter;
+    return SSPP_OK;
+}
+
+int sspp_ces_begin(sspp_ces* p, const double* start, const double* end, int iterate, void* stream) {
+    sspp::clear_error();
+    if (!p || !start || !end) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_begin: null argument");
+    for (int i = 0; i < 4; ++i) { p->start[i] = start[i]; p->end[i] = end[i]; }
+    CesReset r{};
+    if (!iterate) {
+        // Planner::reset (tsp_planner.h:54-69): linear vias, z >= cfg.z_min, then
+        // Distribution::reset (tsp_distribution.h:16-29): z >= dist.z_min, bounds, sigma clamps
+        const int n = p->cfg.total_points;
+        for (int i = 0; i < p->K; ++i) {
+            const double t = (double)(i + 1) / (n - 1);
+            for (int d = 0; d < 4; ++d) {
+                double v = (1.0 - t) * start[d] + t * end[d];
+                if (d == 2) v = v < p->cfg.z_min ? p->cfg.z_min : v;
+                if (d == 2) v = v < p->cfg.dist_z_min ? p->cfg.dist_z_min : v;
+                v = v < p->lo[d] ? p->lo[d] : (p->hi[d] < v ? p->hi[d] : v);
+                r.mean0[4 * i + d] = v;
+            }
+        }
+        double s = p->cfg.sigma0;
+        s = s < p->cfg.stddev_min ? p->cfg.stddev_min : s;
+        s = s > p->cfg.stddev_max ? p->cfg.stddev_max : s;
+        s = s < p->cfg.sigma_floor ? p->cfg.sigma_floor : s;
+        r.sigma0 = s;
+    }
+    hipLaunchKernelGGL(k_ces_begin, dim3(1), dim3(128), 0, (hipStream_t)stream, ces_k(p), iterate ? 1 : 0,
+                       r, p->d_hdr, p->d_mean, p->d_sigma, p->d_lbest, p->d_fixed);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_err(e, "k_ces_begin launch");
+    return SSPP_OK;
+}
+
+int sspp_ces_eval(sspp_ces* p, int rank, void* stream) {
+    sspp::clear_error();
+    if (!p || rank < 0 || rank >= p->world) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_eval: bad rank");
+    sspp::TspCesEval ev{};
+    ev.fixed = p->d_fixed; ev.nfixed = &p->d_hdr->nfixed;
+    ev.mean = p->d_mean; ev.sigma = p->d_sigma;
+    ev.slot0 = (long long)rank * p->spr;
+    ev.samples = p->cfg.samples;
+    ev.first_id = p->iter * (long long)p->cfg.samples;
+    for (int i = 0; i < 4; ++i) { ev.start[i] = p->start[i]; ev.end[i] = p->end[i]; }
+    const size_t o = (size_t)rank * p->spr;
+    return sspp::tsp_eval_ces(p->job, &ev, p->spr, p->d_L + o, p->d_Cnf + o, p->d_Cwf + o,
+                              p->d_status + o, p->d_cost + o, p->d_vias + o * 4 * p->K, stream);
+}
+
+int sspp_ces_update(sspp_ces* p, void* stream) {
+    sspp::clear_error();
+    if (!p) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_update: null planner");
+    hipLaunchKernelGGL(k_ces_update, dim3(1), dim3(kCesThreads), 0, (hipStream_t)stream, ces_k(p),
+                       p->d_cost, p->d_status, p->d_vias, p->d_LT, p->d_LH, p->d_hdr, p->d_mean,
+                       p->d_sigma, p->d_lbest, p->d_elite);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_err(e, "k_ces_update launch");
+    p->iter++;
+    return SSPP_OK;
+}
+
+int sspp_ces_plan(sspp_ces* p, const double* start, const double* end, int iterate, int iterations,
+                  void* stream) {
+    if (!p || iterations < 1) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_plan: bad argument");
+    if (p->world != 1) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_plan: multi-rank planners step eval/update themselves");
+    for (int t = 0; t < iterations; ++t) {
+        int rc = sspp_ces_begin(p, start, end, (t > 0 || iterate) ? 1 : 0, stream);
+        if (rc) return rc;
+        if ((rc = sspp_ces_eval(p, 0, stream))) return rc;
+        if ((rc = sspp_ces_update(p, stream))) return rc;
+    }
+    return SSPP_OK;
+}
+
+int sspp_ces_pack(const sspp_ces* p, int rank, double* d_out, void* stream) {
+    sspp::clear_error();
+    if (!p || !d_out || rank < 0 || rank >= p->world) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_pack: bad argument");
+    const size_t o = (size_t)rank * p->spr;
+    const int KD = 4 * p->K;
+    const long long tot = (long long)p->spr * (5 + KD);
+    const int g = (int)std::min<long long>((tot + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_ces_pack, dim3(g), dim3(256), 0, (hipStream_t)stream, p->spr, KD, p->d_L + o,
+                       p->d_Cnf + o, p->d_Cwf + o, p->d_cost + o, p->d_status + o, p->d_vias + o * KD, d_out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SSPP_OK : hip_err(e, "k_ces_pack launch");
+}
+
+int sspp_ces_unpack(sspp_ces* p, const double* d_in, void* stream) {
+    sspp::clear_error();
+    if (!p || !d_in) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_unpack: bad argument");
+    const int KD = 4 * p->K;
+    const long long tot = (long long)p->nslots * (5 + KD);
+    const int g = (int)std::min<long long>((tot + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_ces_unpack, dim3(g), dim3(256), 0, (hipStream_t)stream, p->nslots, KD, d_in,
+                       p->d_L, p->d_Cnf, p->d_Cwf, p->d_cost, p->d_status, p->d_vias);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SSPP_OK : hip_err(e, "k_ces_unpack launch");
+}
+
+int sspp_ces_get_buffers(const sspp_ces* p, sspp_ces_buffers* out) {
+    if (!p || !out) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_get_buffers: null argument");
+    out->L = p->d_L; out->C_nf = p->d_Cnf; out->C_wf = p->d_Cwf; out->cost = p->d_cost;
+    out->status = p->d_status; out->vias = p->d_vias;
+    out->mean = p->d_mean; out->sigma = p->d_sigma; out->last_best = p->d_lbest;
+    out->elites = p->d_elite;
+    return SSPP_OK;
+}
+
+int sspp_ces_read(sspp_ces* p, sspp_ces_state* st, double* L, double* Cnf, double* Cwf, double* cost,
+                  uint8_t* status, double* vias, double* mean, double* sigma, double* last_best,
+                  int32_t* elites) {
+    sspp::clear_error();
+    if (!p || !st) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_read: null argument");
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_err(e, "sspp_ces_read synchronize");
+    CesHdr h;
+    if ((e = hipMemcpy(&h, p->d_hdr, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess) return hip_err(e, "read header");
+    st->n_fixed = h.nfixed;
+    st->n_candidates = h.nfixed + p->cfg.samples;
+    st->n_success = h.nsucc;
+    st->n_elite = h.nelite;
+    st->has_best = h.has_best;
+    st->best_slot = h.best_slot;
+    st->best_cost = h.best_cost;
+    st->iteration = p->iter;
+    const size_t n = (size_t)st->n_candidates, kd = (size_t)4 * p->K;
+    struct { void* dst; const void* src; size_t bytes; } cp[] = {
+        {L, p->d_L, 8 * n}, {Cnf, p->d_Cnf, 8 * n}, {Cwf, p->d_Cwf, 8 * n}, {cost, p->d_cost, 8 * n},
+        {status, p->d_status, n}, {vias, p->d_vias, 8 * n * kd}, {mean, p->d_mean, 8 * kd},
+        {sigma, p->d_sigma, 8 * kd}, {last_best, p->d_lbest, 8 * kd},
+        {elites, p->d_elite, sizeof(int32_t) * (size_t)(h.nelite > 0 ? h.nelite : 0)}};
+    for (auto& c : cp)
+        if (c.dst && c.bytes && (e = hipMemcpy(c.dst, c.src, c.bytes, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_err(e, "sspp_ces_read copy");
+    return SSPP_OK;
+}
+
+int sspp_ces_set_state(sspp_ces* p, const double* mean, const double* sigma, const double* last_best,
+                       int has_best) {
+    sspp::clear_error();
+    if (!p) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_set_state: null planner");
+    const size_t kd = (size_t)4 * p->K;
+    hipError_t e;
+    if ((mean && (e = hipMemcpy(p->d_mean, mean, 8 * kd, hipMemcpyHostToDevice)) != hipSuccess) ||
+        (sigma && (e = hipMemcpy(p->d_sigma, sigma, 8 * kd, hipMemcpyHostToDevice)) != hipSuccess) ||
+        (last_best && (e = hipMemcpy(p->d_lbest, last_best, 8 * kd, hipMemcpyHostToDevice)) != hipSuccess))
+        return hip_err(e, "sspp_ces_set_state copy");
+    if (has_best >= 0) {
+        CesHdr h;
+        if ((e = hipMemcpy(&h, p->d_hdr, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess ||
+            (h.has_best = has_best, (e = hipMemcpy(p->d_hdr, &h, sizeof h, hipMemcpyHostToDevice)) != hipSuccess))
+            return hip_err(e, "sspp_ces_set_state header");
+    }
+    return SSPP_OK;
+}
+
+}  // extern "C"

@@ -35,4 +35,19 @@ int interpolate(const double* pts, int n, int D, int p, const double* u, double*
                 double* ctrl);
 // collocation inverse for fixed parameters u (PathModel::fromVias precompute)
 int collocation_inverse(const double* u, int n, int p, double* knots, double* Minv);
+
+// CES slot-mode evaluation of a TaskSpacePlanner job (sspp_kernels.hip; used by ces.hip)
+struct TspCesEval {
+    const double* fixed;   // device [2][K][4]: mean set, forwarded best
+    const int* nfixed;     // device: fixed slots in this iteration's list (1 or 2)
+    const double* mean;    // device [K][4] sampling distribution
+    const double* sigma;   // device [K][4]
+    long long slot0;       // first slot evaluated by this call
+    long long samples;     // random samples in the list
+    long long first_id;    // Philox id of sample 0
+    double start[4], end[4];
+};
+int tsp_eval_ces(sspp_job* j, const TspCesEval* e, int64_t n, double* d_L, double* d_Cnf,
+                 double* d_Cwf, uint8_t* d_status, double* d_cost, double* d_vias_out,
+                 void* stream);
 }  // namespace sspp

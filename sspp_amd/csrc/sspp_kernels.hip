@@ -197,6 +197,14 @@ struct TspK {
     long long first_id, B;
     double w_col, floor_z_min, floor_margin, floor_scale;
     int lpc, cpb;
+    // CES slot mode (tsp_planner.h:78-93 seeds): launch candidate c is slot slot0 + c of the
+    // iteration's list [mean set, forwarded best (if any), samples...].  Slots below *nfixed
+    // copy fixed[slot]; slot s >= *nfixed is random sample s - *nfixed (Philox id first_id +
+    // s - *nfixed); slots past *nfixed + samples are padding (status 0, cost +inf).
+    int ces;
+    const double* fixed;    // [2][K][4]
+    const int* nfixed;
+    long long slot0, samples;
 };
 
 // ---------------------------------------------------------------- Philox4x32-10 + Box-Muller
@@ -1102,6 +1110,7 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_tsp(
     int* s_stat = (int*)(s_best + 4);        // [cpb]
 
     const long long nvalid = min((long long)cpb, a.B - cand0);
+    const long long nfx = a.ces ? (long long)*a.nfixed : 0;  // uniform: scalar load
     for (int e = tid; e < cpb * 2 * D; e += kBlock) {
         const int s = e / (2 * D), r = e - s * 2 * D;
         if (r < D) s_V[s * ndof + r] = a.start[r];
@@ -1118,7 +1127,20 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_tsp(
             const int s = e / (K * D), r = e - s * K * D;
             if (s >= nvalid) continue;
             const int v = r / D, i = r - v * D;
-            const unsigned long long g = (unsigned long long)(a.first_id + cand0 + s);
+            long long gi = cand0 + s;
+            if (a.ces) {
+                const long long slot = a.slot0 + cand0 + s;
+                if (slot < nfx) {  // mean set / forwarded best: no sampling
+                    s_V[s * ndof + D + r] = a.fixed[(slot * K + v) * D + i];
+                    continue;
+                }
+                gi = slot - nfx;
+                if (gi >= a.samples) {  // padding slot
+                    s_V[s * ndof + D + r] = mean[v * D + i];
+                    continue;
+                }
+            }
+            const unsigned long long g = (unsigned long long)(a.first_id + gi);
             const double m = mean[v * D + i], sg = sigma[v * D + i];
             double val;
             if (i < 3) {
@@ -1208,8 +1230,11 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_tsp(
             Cw = Cw + s_wsum[2 * NW + w0 + w];
         }
         const long long c = cand0 + slot;
-        const int st = Cn == 0.0;
-        const double cost = L + a.w_col * Cw;
+        int st = Cn == 0.0;
+        double cost = L + a.w_col * Cw;
+        if (a.ces && a.slot0 + c >= nfx + a.samples) {  // padding slot
+            st = 0; cost = INFINITY; L = 0.0; Cn = 0.0; Cw = 0.0;
+        }
         oL[c] = L; oCnf[c] = Cn; oCwf[c] = Cw; ocost[c] = cost;
         ostatus[c] = (unsigned char)st;
         s_stat[slot] = st;
@@ -2008,7 +2033,8 @@ extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args*
 
 static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t B, double* d_L,
                    double* d_Cnf, double* d_Cwf, uint8_t* d_status, double* d_cost,
-                   double* d_vias_out, sspp_best* d_best, void* stream) {
+                   double* d_vias_out, sspp_best* d_best, void* stream,
+                   const sspp::TspCesEval* ces = nullptr) {
     sspp::clear_error();
     if (!j || j->kind != 1) return sspp::set_error(SSPP_E_INVAL, "not a TaskSpacePlanner job");
     if (B < 1 || B > j->max_batch) return sspp::set_error(SSPP_E_INVAL, "batch size out of range");
@@ -2022,19 +2048,38 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     k.w_col = j->w_col; k.floor_z_min = j->floor_z_min; k.floor_margin = j->floor_margin;
     k.floor_scale = j->floor_scale;
     k.lpc = j->lpc; k.cpb = j->cpb;
+    const double* mean = j->d_mean;
+    const double* sigma = j->d_sigma;
+    if (ces) {
+        if (d_vias) return sspp::set_error(SSPP_E_INVAL, "CES slot mode samples its own via sets");
+        k.ces = 1; k.fixed = ces->fixed; k.nfixed = ces->nfixed;
+        k.slot0 = ces->slot0; k.samples = ces->samples;
+        mean = ces->mean; sigma = ces->sigma;
+        for (int i = 0; i < 4; ++i) { k.start[i] = ces->start[i]; k.end[i] = ces->end[i]; }
+    }
     const int nblk = (int)((B + j->cpb - 1) / j->cpb);
     hipStream_t st = (hipStream_t)stream;
     if (k.sc.onegeom && k.sc.npairs > 0)
         hipLaunchKernelGGL((k_tsp<1, true>), dim3(nblk), dim3(kBlock), j->lds, st, k, scene_t(j->scene),
-                           j->d_tab, j->d_span, j->d_Minv, j->d_mean, j->d_sigma, d_vias, d_vias_out,
+                           j->d_tab, j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out,
                            d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part, j->d_sync, d_best);
     else
         hipLaunchKernelGGL((k_tsp<1, false>), dim3(nblk), dim3(kBlock), j->lds, st, k, scene_t(j->scene),
-                           j->d_tab, j->d_span, j->d_Minv, j->d_mean, j->d_sigma, d_vias, d_vias_out,
+                           j->d_tab, j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out,
                            d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part, j->d_sync, d_best);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_tsp launch");
     return SSPP_OK;
+}
+
+// CES slot-mode evaluation (ces.hip, tsp::Planner::plan eval loop): slots [slot0, slot0 + n)
+int sspp::tsp_eval_ces(sspp_job* j, const TspCesEval* e, int64_t n, double* d_L, double* d_Cnf,
+                       double* d_Cwf, uint8_t* d_status, double* d_cost, double* d_vias_out,
+                       void* stream) {
+    if (!e || !e->fixed || !e->nfixed || !e->mean || !e->sigma || !d_vias_out)
+        return sspp::set_error(SSPP_E_INVAL, "tsp_eval_ces: null argument");
+    return run_tsp(j, nullptr, e->first_id, n, d_L, d_Cnf, d_Cwf, d_status, d_cost, d_vias_out,
+                   nullptr, stream, e);
 }
 
 extern "C" int sspp_job_tsp_sample_score(sspp_job* j, int64_t first_id, int64_t B, double* d_L, double* d_Cnf,

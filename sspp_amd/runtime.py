@@ -11,7 +11,8 @@ import math
 import numpy as np
 
 from . import _lib
-from ._lib import Best, ModelView, SceneInfo, SsppArgs, TspArgs, check, lib
+from ._lib import (Best, CesBuffers, CesConfig, CesInfo, CesState, ModelView, SceneInfo,
+                   SsppArgs, TspArgs, check, lib)
 
 DEFAULT_SEED = 0x5EED
 
@@ -308,6 +309,128 @@ class SsppSteps:
                                             self._F, _ptr(best)), "steps enqueue")
 
 
+class CesPlanner:
+    """tsp::Planner's CES iteration on the device (include/sspp/tsp_planner.h:72-145).
+
+    One iteration = begin (reset() or keep the distribution; seed list [mean set, forwarded
+    best, samples]) -> eval (k_tsp over the slots) -> update (elites, Distribution::update,
+    best, adapt) — all asynchronous on `stream`.  With world > 1 every rank owns
+    slots_per_rank consecutive slots: `step` evaluates this rank's slots, all-gathers the
+    per-slot results (one RCCL all_gather of a packed f64 record per slot) and runs the same
+    update on every rank, so all ranks hold the identical distribution afterwards.
+
+    Arguments follow tsp::TaskSpacePlanner's constructor (include/sspp/tsp.h:12-33); the
+    planner's Distribution::z_min is `stddev_initial` as in the reference (SURVEY Q1).
+    """
+
+    def __init__(self, scene, stddev_initial=0.3, stddev_min=0.01, stddev_max=0.5,
+                 stddev_increase_factor=1.5, stddev_decay_factor=0.95, elite_fraction=0.3,
+                 sample_count=50, check_points=50, init_points=3, collision_weight=1.0,
+                 z_min=0.0, limits_min=(-2.0,) * 4, limits_max=(2.0,) * 4, sigma_floor=0.0,
+                 var_ema_beta=0.2, mean_lr=0.5, floor_margin=0.01, floor_penalty_scale=10.0,
+                 seed=DEFAULT_SEED, world=1, rank=0, group=None):
+        self.lo, self.hi = _f64(limits_min, 4), _f64(limits_max, 4)
+        cfg = CesConfig(samples=int(sample_count), checks=int(check_points),
+                        total_points=int(init_points), w_collision=float(collision_weight),
+                        elite_fraction=float(elite_fraction), inc=float(stddev_increase_factor),
+                        dec=float(stddev_decay_factor), sigma_floor=float(sigma_floor),
+                        var_beta=float(var_ema_beta), mean_lr=float(mean_lr),
+                        stddev_min=float(stddev_min), stddev_max=float(stddev_max),
+                        z_min=float(z_min), dist_z_min=float(stddev_initial), sigma0=0.3,
+                        lo=_dptr(self.lo), hi=_dptr(self.hi),
+                        # Planner never forwards cfg.z_min/floor_* to its Evaluator (SURVEY Q2)
+                        floor_z_min=0.0, floor_margin=0.01, floor_scale=10.0,
+                        seed=int(seed) & (2 ** 64 - 1))
+        self.cfg = cfg
+        self.configured_floor = (float(z_min), float(floor_margin), float(floor_penalty_scale))
+        h = C.c_void_p()
+        check(lib().sspp_ces_create(scene.handle, C.byref(cfg), int(world), C.byref(h)), "ces create")
+        self._h = h
+        self.scene, self.world, self.rank, self.group = scene, int(world), int(rank), group
+        inf = CesInfo()
+        check(lib().sspp_ces_get_info(self._h, C.byref(inf)), "ces info")
+        self.K, self.n_slots, self.spr = inf.n_vias, inf.n_slots, inf.slots_per_rank
+        self.samples = int(sample_count)
+        b = CesBuffers()
+        check(lib().sspp_ces_get_buffers(self._h, C.byref(b)), "ces buffers")
+        self._bufs = b
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib._lib is not None:
+            _lib._lib.sspp_ces_free(self._h)
+            self._h = None
+
+    def begin(self, start, end, iterate, stream=None):
+        self._se = (_f64(start, 4), _f64(end, 4))
+        check(lib().sspp_ces_begin(self._h, _dptr(self._se[0]), _dptr(self._se[1]),
+                                   int(bool(iterate)), _stream(stream)), "ces begin")
+
+    def eval(self, rank=None, stream=None):
+        check(lib().sspp_ces_eval(self._h, self.rank if rank is None else int(rank),
+                                  _stream(stream)), "ces eval")
+
+    def update(self, stream=None):
+        check(lib().sspp_ces_update(self._h, _stream(stream)), "ces update")
+
+    def step(self, start, end, iterate, stream=None):
+        """One plan() iteration on this rank (collective over the group when world > 1)."""
+        self.begin(start, end, iterate, stream)
+        self.eval(stream=stream)
+        if self.world > 1:
+            self._exchange(stream)
+        self.update(stream)
+
+    def _exchange(self, stream=None):
+        """All-gather every rank's slot records (one RCCL collective), then unpack them into
+        this rank's planner so the update sees the whole candidate list."""
+        import torch.distributed as dist
+        torch = _torch()
+        rec = 5 + 4 * self.K
+        if getattr(self, "_xbuf", None) is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            self._xbuf = (torch.empty(self.spr * rec, dtype=torch.float64, device=dev),
+                          torch.empty(self.world * self.spr * rec, dtype=torch.float64, device=dev))
+        local, full = self._xbuf
+        check(lib().sspp_ces_pack(self._h, self.rank, _ptr(local), _stream(stream)), "ces pack")
+        dist.all_gather_into_tensor(full, local, group=self.group)
+        check(lib().sspp_ces_unpack(self._h, _ptr(full), _stream(stream)), "ces unpack")
+
+    def plan(self, start, end, iterate=False, iterations=1, stream=None):
+        """iterations x plan(start, end, iterate) without host synchronisation (world == 1)."""
+        if self.world > 1:
+            for t in range(int(iterations)):
+                self.step(start, end, iterate or t > 0, stream)
+            return
+        s, e = _f64(start, 4), _f64(end, 4)
+        check(lib().sspp_ces_plan(self._h, _dptr(s), _dptr(e), int(bool(iterate)),
+                                  int(iterations), _stream(stream)), "ces plan")
+
+    def read(self):
+        """Synchronous copy of the last iteration: per-candidate results and the state."""
+        st = CesState()
+        n, K = self.samples + 2, self.K
+        L, Cnf, Cwf, cost = (np.zeros(n) for _ in range(4))
+        status = np.zeros(n, np.uint8)
+        vias = np.zeros((n, K, 4))
+        mean, sigma, lbest = np.zeros((K, 4)), np.zeros((K, 4)), np.zeros((K, 4))
+        elites = np.zeros(max(1, n), np.int32)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        check(lib().sspp_ces_read(self._h, C.byref(st), p(L), p(Cnf), p(Cwf), p(cost), p(status),
+                                  p(vias), p(mean), p(sigma), p(lbest), p(elites)), "ces read")
+        m = st.n_candidates
+        return dict(n_fixed=st.n_fixed, n_candidates=m, n_success=st.n_success,
+                    n_elite=st.n_elite, has_best=bool(st.has_best), best_slot=int(st.best_slot),
+                    best_cost=st.best_cost, iteration=int(st.iteration), L=L[:m], C_nf=Cnf[:m],
+                    C_wf=Cwf[:m], cost=cost[:m], status=status[:m], vias=vias[:m], mean=mean,
+                    sigma=sigma, last_best=lbest, elites=elites[:st.n_elite].copy())
+
+    def set_state(self, mean=None, sigma=None, last_best=None, has_best=-1):
+        """Overwrite the device distribution (test / warm-start hook; synchronous)."""
+        keep = [None if a is None else _f64(a, 4 * self.K) for a in (mean, sigma, last_best)]
+        ptrs = [None if a is None else a.ctypes.data_as(C.c_void_p) for a in keep]
+        check(lib().sspp_ces_set_state(self._h, *ptrs, int(has_best)), "ces set_state")
+
+
 def reduce_best_steps(parts, out, stream=None):
     """parts: (R, G, 4) int64 device tensor of per-rank step records -> out (G, 4)."""
     R, G = parts.shape[0], parts.shape[1]
@@ -321,5 +444,5 @@ def device_count():
     return n.value if rc == 0 else 0
 
 
-__all__ = ["Model", "Scene", "SsppJob", "TspJob", "SsppSteps", "reduce_best_steps", "interpolate", "spline_eval", "best_tensor",
+__all__ = ["Model", "Scene", "SsppJob", "TspJob", "CesPlanner", "SsppSteps", "reduce_best_steps", "interpolate", "spline_eval", "best_tensor",
            "decode_best", "reduce_best", "reduce_best_device", "device_count", "DEFAULT_SEED", "math"]
