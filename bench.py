@@ -39,9 +39,10 @@ FP64_PEAK_TFLOPS = 78.6    # FP64 vector (VALU) spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8192)
-    ap.add_argument("--warmup", type=int, default=256)
-    ap.add_argument("--config", default="robocrane", choices=["robocrane", "stacking"])
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: robocrane 8192, stacking 1024, multigoal 128)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: steps / 32)")
+    ap.add_argument("--config", default="robocrane", choices=["robocrane", "stacking", "multigoal"])
     ap.add_argument("--batch", type=int, default=0, help="candidates per GPU per step (default: config)")
     ap.add_argument("--waypoints", type=int, default=128)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
@@ -57,7 +58,12 @@ def parse():
     ap.add_argument("--steps-per-launch", type=int, default=1,
                     help="native mode: independent steps (each its own B candidates, outputs and "
                          "argmin) grouped into one kernel launch")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = {"robocrane": 8192, "stacking": 1024, "multigoal": 128}[a.config]
+    if a.warmup is None:
+        a.warmup = max(1, a.steps // 32)
+    return a
 
 
 def setup_robocrane(args, device):
@@ -136,6 +142,57 @@ def setup_stacking(args, device):
     return B, step, kernel_only, bytes_per, flops_per, meta, ctx
 
 
+# BASELINE.json configs[4] ("TSP multi-goal", SURVEY 8(d) row 5 — build-defined: the reference
+# has no multi-goal logic): 8 independent TaskSpacePlanner problems on robocrane.xml with the
+# free gripper (7 collidable geoms) moving between fixed (start, goal) pairs around the lego
+# wall; 4096 sampled via sets (+ mean set + forwarded best) per problem and CES iteration.
+MULTIGOAL = [((0.5, 0.15, 0.27, 0.0), (0.5, -0.05, 0.27, 0.0)),
+             ((0.5, -0.05, 0.27, 0.0), (0.5, 0.15, 0.27, 0.0)),
+             ((0.5, 0.15, 0.27, 1.5708), (0.5, -0.05, 0.27, 1.5708)),
+             ((0.3, 0.05, 0.22, 0.0), (0.7, 0.05, 0.22, 0.0)),
+             ((0.7, 0.05, 0.22, 0.0), (0.3, 0.05, 0.22, 0.0)),
+             ((0.35, 0.2, 0.25, 0.0), (0.65, -0.1, 0.25, 0.5)),
+             ((0.65, 0.2, 0.25, 0.0), (0.35, -0.1, 0.25, -0.5)),
+             ((0.5, 0.25, 0.3, 0.0), (0.5, -0.15, 0.22, 0.0))]
+MG_LO, MG_HI = (0.0, -0.4, 0.0, -1.6), (1.0, 0.5, 0.8, 1.6)
+
+
+def setup_multigoal(args, device, world, rank):
+    """One CES iteration of every goal this rank owns (goal g -> rank g % world) per step."""
+    import torch
+    import sspp_amd as S
+    model = S.Model(os.path.join(S.SCENE_DIR, "robocrane.xml"))
+    body = model.body_id("gripper_collision_with_block/")
+    scene = S.Scene(model, 1, body)
+    samples, cp = args.batch or 4096, args.waypoints
+    mine = [g for g in range(len(MULTIGOAL)) if g % world == rank]
+    pls = [S.CesPlanner(scene, sample_count=samples, check_points=cp, init_points=3,
+                        limits_min=MG_LO, limits_max=MG_HI, seed=S.DEFAULT_SEED + g) for g in mine]
+    streams = [torch.cuda.Stream(device) for _ in pls]
+    started = [False] * len(pls)
+
+    def run_steps(k):
+        for i, (g, pl) in enumerate(zip(mine, pls)):
+            st, en = MULTIGOAL[g]
+            pl.plan(st, en, iterate=started[i], iterations=k, stream=streams[i])
+            started[i] = True
+
+    def kernel_only(first_id):
+        pls[0].eval(rank=0, stream=torch.cuda.current_stream())
+
+    bytes_per = 3 * 4 * 8 + 8 + 1
+    flops_per = (2 * cp + 1) * 2 * 3 * 4 + cp * (3 * 4 + 1) + cp * (40 + 7 * 42 + 48 + 8 * 450)
+    meta = dict(workload="robocrane TaskSpacePlanner multi-goal (gripper, 7 geoms), %d goals, "
+                         "full CES iterations (eval + elites + distribution update)" % len(MULTIGOAL),
+                goals=len(MULTIGOAL), goals_this_rank=len(mine), samples_per_goal=samples,
+                candidates_per_goal=samples + 2, waypoints=cp, vias=1, degree=2, dof=4)
+    ctx = dict(kind="multigoal", kernel_name="k_tsp", run_steps=run_steps, planners=pls, mine=mine,
+               scene_path=model.path, body=body, cp=cp, samples=samples)
+    # candidates per step over ALL ranks: every goal's list (mean set + best + samples)
+    return (samples + 2) * len(MULTIGOAL) // max(1, world), None, kernel_only, bytes_per, \
+        flops_per, meta, ctx
+
+
 def cpu_baseline(args, ctx, B, device):
     """Oracle (CPU restatement, oracle/) timed on a bounded sample of the same workload."""
     import torch
@@ -145,6 +202,8 @@ def cpu_baseline(args, ctx, B, device):
     threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
         min(16, os.cpu_count() or 1)
     model = mjcf_ref.load(ctx["scene_path"])
+    if ctx["kind"] == "multigoal":
+        return cpu_baseline_multigoal(args, ctx, model, threads)
     if ctx["kind"] == "sspp":
         job = ctx["job"]
         osc = O.Scene(model, 0, 7)
@@ -197,6 +256,39 @@ def cpu_baseline(args, ctx, B, device):
                 parity=parity)
 
 
+def cpu_baseline_multigoal(args, ctx, model, threads):
+    """The oracle's full TaskSpacePlanner iteration (oracle.ces_plan) on goal 0, bounded."""
+    from oracle import oracle as O
+    osc = O.Scene(model, 1, ctx["body"])
+    st, en = (np.array(x) for x in MULTIGOAL[0])
+    # parity on the device planner's first iteration of goal 0 (same Philox ids)
+    import sspp_amd as S
+    import torch
+    pl = S.CesPlanner(ctx["planners"][0].scene, sample_count=ctx["samples"], check_points=ctx["cp"],
+                      init_points=3, limits_min=MG_LO, limits_max=MG_HI, seed=S.DEFAULT_SEED)
+    pl.plan(st, en, iterate=False, iterations=1)
+    torch.cuda.synchronize()
+    r = pl.read()
+    rec = O.ces_plan(osc, st, en, 1, ctx["samples"], ctx["cp"], seed=S.DEFAULT_SEED, lo=MG_LO,
+                     hi=MG_HI, nthreads=threads)[0]
+    parity = dict(candidates=int(r["n_candidates"]),
+                  max_abs_cost_diff=float(np.abs(np.where(np.isfinite(r["cost"]), r["cost"], 0) -
+                                                 np.where(np.isfinite(rec["cost"]), rec["cost"], 0)).max()),
+                  status_identical=bool(np.array_equal(r["status"], rec["status"])),
+                  best_slot_identical=bool(r["best_slot"] == rec["best_slot"]),
+                  mean_max_abs_diff=float(np.abs(r["mean"] - rec["mean"]).max()))
+    done, it, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        O.ces_plan(osc, st, en, 1, ctx["samples"], ctx["cp"], seed=S.DEFAULT_SEED + it, lo=MG_LO,
+                   hi=MG_HI, nthreads=threads)
+        done += ctx["samples"] + 1
+        it += 1
+    dt = time.perf_counter() - t0
+    return dict(value=done / dt, unit="candidate paths scored/s (full CES iterations)", cores=threads,
+                kind="port", sample="%d CES iterations of goal 0 (%d candidates) in %.1f s" % (it, done, dt),
+                parity=parity)
+
+
 def main():
     args = parse()
     import torch
@@ -210,12 +302,17 @@ def main():
     device = torch.device("cuda", local)
     import sspp_amd as S
 
-    setup = setup_robocrane if args.config == "robocrane" else setup_stacking
-    B, step, kernel_only, bytes_per, flops_per, meta, ctx = setup(args, device)
+    if args.config == "multigoal":
+        B, step, kernel_only, bytes_per, flops_per, meta, ctx = setup_multigoal(args, device, world, rank)
+    else:
+        setup = setup_robocrane if args.config == "robocrane" else setup_stacking
+        B, step, kernel_only, bytes_per, flops_per, meta, ctx = setup(args, device)
 
     ns = args.streams
     native = args.mode == "native" and "make_executor" in ctx
-    if native:
+    if "run_steps" in ctx:
+        run_steps = ctx["run_steps"]
+    elif native:
         # The C++ step executor enqueues G steps per call, round robin over ns streams (one job
         # each): step t scores global ids (t * world + rank) * B + [0, B), so the candidate set
         # does not depend on the rank count.  With several ranks each chunk's G per-step argmin
@@ -313,12 +410,16 @@ def main():
 
     if rank == 0:
         total = args.steps * B * world
+        if ctx["kind"] == "multigoal":  # every goal's list, whatever the rank count
+            total = args.steps * (ctx["samples"] + 2) * len(MULTIGOAL)
         value = total / elapsed
-        ach_gbs = bytes_per * B / kernel_s / 1e9
-        ach_tf = flops_per * B / kernel_s / 1e12
+        per_launch = ctx["samples"] + 2 if ctx["kind"] == "multigoal" else B
+        ach_gbs = bytes_per * per_launch / kernel_s / 1e9
+        ach_tf = flops_per * per_launch / kernel_s / 1e12
         line = {
-            "metric": "candidate paths scored/sec (7-DoF, 128 waypts) at 1/2/4/8 MI355X; HBM %peak"
-            if args.config == "robocrane" else "candidate paths scored/sec (stacking.xml TSP)",
+            "metric": {"robocrane": "candidate paths scored/sec (7-DoF, 128 waypts) at 1/2/4/8 MI355X; HBM %peak",
+                       "stacking": "candidate paths scored/sec (stacking.xml TSP)",
+                       "multigoal": "candidate paths scored/sec (TSP multi-goal, full CES iterations)"}[args.config],
             "value": value,
             "unit": "candidate paths/s",
             "n_gpus": world,
@@ -326,18 +427,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if ctx["kind"] == "multigoal" else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (on-device Philox candidates around a linear init spline)",
-            "config": dict(meta, streams=ns, launch=("native executor, %d steps/call, %d steps/launch"
-                                                     % (args.chunk, args.steps_per_launch))
-                           if native else "eager",
+            "config": dict(meta, streams=ns, launch=("CES iteration chains (sspp_ces_plan), one stream per goal"
+                                                     if "run_steps" in ctx else
+                                                     "native executor, %d steps/call, %d steps/launch"
+                                                     % (args.chunk, args.steps_per_launch)
+                                                     if native else "eager"),
                            parallelism="dp%d (candidate shards, RCCL all-gather argmin)" % world),
             "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": bytes_per * B,
+                         "algorithmic_bytes_per_launch": bytes_per * per_launch,
                          "kernel": ctx.get("kernel_name", "k_tsp"),
                          "kernel_us": kernel_s * 1e6, "bytes_per_candidate": bytes_per},
             # SURVEY 8(d)'s fixed charge table: every filter-passing pair at every waypoint, no

@@ -284,3 +284,39 @@ def test_reduce_best_steps(cuda):
         cost, idx, cnt = S.decode_best(out[g])
         assert (cost, idx) == (float(want[0]), int(want[1]))
         assert cnt == int(recs[:, g, 2].sum())
+
+
+def test_config4_full_size_shards(robocrane):
+    """BASELINE configs[3] at full size on one GPU: 262144 candidates x 256 waypoints scored
+    as one batch and as the 8 per-GPU shards of 32768 (global Philox ids) give identical
+    per-candidate results, and the 8 shard records reduce to the whole batch's argmin (the
+    RCCL all-gather path).  A random 512-candidate subset is checked against the oracle."""
+    import sspp_amd as S
+    import torch
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    B, W, R = 262144, 256, 8
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, max_batch=B)
+    whole = job.alloc(B, with_ctrl=True)
+    job.sample_score(0, B, whole["arc"], whole["feasible"], whole["best"], ctrl_out=whole["ctrl"])
+    per = B // R
+    arc = torch.empty(B, dtype=torch.float64, device="cuda")
+    feas = torch.empty(B, dtype=torch.uint8, device="cuda")
+    recs = torch.zeros((R, 4), dtype=torch.int64, device="cuda")
+    for r in range(R):
+        job.sample_score(r * per, per, arc[r * per:(r + 1) * per], feas[r * per:(r + 1) * per], recs[r])
+    out = S.best_tensor()
+    S.reduce_best_device(recs, out)
+    torch.cuda.synchronize()
+    assert torch.equal(arc, whole["arc"]) and torch.equal(feas, whole["feasible"])
+    assert S.decode_best(out) == S.decode_best(whole["best"])
+    cost, idx, cnt = S.decode_best(whole["best"])
+    a, f = _np(whole["arc"]), _np(whole["feasible"])
+    assert cnt == int(f.sum()) and 0 < cnt < B
+    assert idx == O.argmin(a, f)[0] and cost == a[idx]
+    sub = np.sort(np.random.default_rng(0).choice(B, 512, replace=False))
+    sub = np.union1d(sub, [idx])
+    ctrl = _np(whole["ctrl"][torch.from_numpy(sub).cuda()])
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, ctrl, W)
+    np.testing.assert_array_equal(f[sub], feas_o)
+    assert arc_err(a[sub], arc_o) <= COST_TOL
