@@ -55,7 +55,7 @@ def parse():
                     help="native: the C++ step executor enqueues --chunk steps per call "
                          "(robocrane); eager: one Python-level launch per step")
     ap.add_argument("--chunk", type=int, default=64)
-    ap.add_argument("--steps-per-launch", type=int, default=1,
+    ap.add_argument("--steps-per-launch", type=int, default=8,
                     help="native mode: independent steps (each its own B candidates, outputs and "
                          "argmin) grouped into one kernel launch")
     a = ap.parse_args()
@@ -85,14 +85,27 @@ def setup_robocrane(args, device):
         jobs[lane].sample_score(first_id, B, bufs[lane]["arc"], bufs[lane]["feasible"], best,
                                 stream=stream)
 
-    def kernel_only(first_id):
-        job.sample_score(first_id, B, bufs[0]["arc"], bufs[0]["feasible"], None)
+    roof = {}
 
-    def make_executor(streams, spl):
+    def kernel_only(first_id):
+        # one launch exactly as the timed loop issues it: steps_per_launch steps of B
+        # candidates (each with its own outputs and argmin record), on the current stream
         import torch
-        arcs = [torch.empty(spl * B, dtype=torch.float64, device=device) for _ in jobs]
-        feas = [torch.empty(spl * B, dtype=torch.uint8, device=device) for _ in jobs]
-        return S.SsppSteps(jobs, streams, B, arcs, feas, steps_per_launch=spl)
+        spl = args.steps_per_launch if args.mode == "native" else 1
+        if spl == 1:
+            job.sample_score(first_id, B, bufs[0]["arc"], bufs[0]["feasible"], None)
+            return
+        if "ex" not in roof:
+            roof["ex"] = make_executor([torch.cuda.current_stream()], spl, jobs[:1])
+            roof["best"] = torch.zeros((spl, 4), dtype=torch.int64, device=device)
+        roof["ex"].enqueue(spl, first_id * spl, B, roof["best"])
+
+    def make_executor(streams, spl, js=None):
+        import torch
+        js = jobs if js is None else js
+        arcs = [torch.empty(spl * B, dtype=torch.float64, device=device) for _ in js]
+        feas = [torch.empty(spl * B, dtype=torch.uint8, device=device) for _ in js]
+        return S.SsppSteps(js, streams[:len(js)], B, arcs, feas, steps_per_launch=spl)
 
     n_, D, p = 10, 7, 3
     # SURVEY §8(d) algorithmic work per candidate
@@ -103,7 +116,8 @@ def setup_robocrane(args, device):
                 candidates_per_gpu=B, waypoints=W, init_points=n_, degree=p, dof=D)
     ctx = dict(kind="sspp", kernel_name="k_sspp_c2f" if os.environ.get("SSPP_KERNEL", "1") != "0" else "k_sspp",
                job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p,
-               make_executor=make_executor)
+               make_executor=make_executor,
+               per_launch=B * (args.steps_per_launch if args.mode == "native" else 1))
     return B, step, kernel_only, bytes_per, flops_per, meta, ctx
 
 
@@ -400,12 +414,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, ctx, B, device)
 
+    per_launch = ctx["samples"] + 2 if ctx["kind"] == "multigoal" else ctx.get("per_launch", B)
     traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", "traffic_latest.json")
     if os.path.exists(tf):
         rec = json.load(open(tf)).get(args.config)
         if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and \
-                rec.get("candidates_per_launch") == B:
+                rec.get("candidates_per_launch") == per_launch:
             traffic, traffic_src = rec["hbm_bytes_per_launch"], rec["source"]
 
     if rank == 0:
@@ -413,9 +428,14 @@ def main():
         if ctx["kind"] == "multigoal":  # every goal's list, whatever the rank count
             total = args.steps * (ctx["samples"] + 2) * len(MULTIGOAL)
         value = total / elapsed
-        per_launch = ctx["samples"] + 2 if ctx["kind"] == "multigoal" else B
+        exec_per, exec_src, ach_exec = None, None, None
+        ff = os.path.join(ROOT, "profiles", "fp64_latest.json")
+        if os.path.exists(ff):
+            rec = json.load(open(ff)).get(args.config)
+            if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp"):
+                exec_per, exec_src = rec["fp64_flops_per_candidate"], rec["source"]
+                ach_exec = exec_per * per_launch / kernel_s / 1e12
         ach_gbs = bytes_per * per_launch / kernel_s / 1e9
-        ach_tf = flops_per * per_launch / kernel_s / 1e12
         line = {
             "metric": {"robocrane": "candidate paths scored/sec (7-DoF, 128 waypts) at 1/2/4/8 MI355X; HBM %peak",
                        "stacking": "candidate paths scored/sec (stacking.xml TSP)",
@@ -442,14 +462,19 @@ def main():
                          "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": bytes_per * per_launch,
                          "kernel": ctx.get("kernel_name", "k_tsp"),
-                         "kernel_us": kernel_s * 1e6, "bytes_per_candidate": bytes_per},
-            # SURVEY 8(d)'s fixed charge table: every filter-passing pair at every waypoint, no
-            # credit for early exit or broadphase culling -- an upper bound on the work the
-            # reference's own loop would do, not the flops the kernel executes, so this "frac"
-            # can exceed 1 (work avoided, not peak exceeded); executed FP64 counts: profiles/
-            "roofline_fp64_charged": {"bound": "fp64_valu", "achieved": ach_tf, "peak": FP64_PEAK_TFLOPS,
-                                      "unit": "TFLOP/s (charged)", "frac": ach_tf / FP64_PEAK_TFLOPS,
-                                      "flops_per_candidate_charged": flops_per},
+                         "kernel_us": kernel_s * 1e6, "candidates_per_launch": per_launch,
+                         "bytes_per_candidate": bytes_per,
+                         # the same bytes at the timed loop's rate (launches overlap on streams)
+                         "steady_state_GBps": bytes_per * value / 1e9 / max(1, world)},
+            # FP64 VALU roofline with the flops the kernel EXECUTES (PMC: 64 lanes x F64 wave
+            # instructions, FMA = 2; profiles/fp64_latest.json) over the same launches as
+            # `roofline`.  SURVEY 8(d)'s fixed charge table (every pair at every waypoint, no
+            # credit for early exit / culling) is kept for reference only: it overstates the
+            # work ~40x for the early-exit feasibility path.
+            "roofline_fp64": {"bound": "fp64_valu", "achieved": ach_exec, "peak": FP64_PEAK_TFLOPS,
+                              "unit": "TFLOP/s", "frac": None if ach_exec is None else ach_exec / FP64_PEAK_TFLOPS,
+                              "flops_per_candidate_executed": exec_per, "source": exec_src,
+                              "flops_per_candidate_charged": flops_per},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
