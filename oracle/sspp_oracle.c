@@ -1000,7 +1000,7 @@ int64_t or_tsp_best(const double* cost, const uint8_t* status, int64_t B, double
  *   L + w * C_wf), ::weights (24-32: log(k + 0.5) - log(i + 1), normalised),
  *   Distribution::update (tsp_distribution.h:52-83), best = std::min_element, adapt (31-38).
  * Candidate order = slot order and ties go to the lowest slot.  sequential = 1
- * sums in the reference's order; 0 in the GPU's canonical wave order (or_canon_sum, 64 lanes). */
+ * sums in the reference's order; 0 in the GPU's canonical order (or_canon_sum, 512 lanes). */
 typedef struct { double cost; int64_t slot; } or_ces_key;
 
 static int or_ces_cmp(const void* a, const void* b) {
@@ -1026,7 +1026,7 @@ static double or_wrap_diff(double a, double b, double mn, double mx) {
 }
 
 static double or_ces_sum(const double* x, int n, int sequential) {
-    return sequential ? seq_sum(x, n) : or_canon_sum(x, n, 64);
+    return sequential ? seq_sum(x, n) : or_canon_sum(x, n, 512);  /* k_ces_update: 512 lanes */
 }
 
 int or_ces_update(const or_ces_cfg* c, const double* cost, const uint8_t* status,

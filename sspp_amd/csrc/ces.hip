@@ -14,7 +14,8 @@
 //     reference's order of successes_ depends on OpenMP merge timing.  Ties in
 //     the elite sort and the best pick go to the lowest slot.
 //   * the weighted sums of Distribution::update and the weight normaliser use the canonical
-//     wave order (lane j % 64 partials, xor butterfly) that oracle/sspp_oracle.c restates;
+//     512-lane order (lane j % 512 partials, xor butterfly per wave, waves in order) that
+//     oracle/sspp_oracle.c::or_canon_sum restates;
 //     the reference sums sequentially (differences ~1e-16 relative).
 //   * log(k + 0.5) and log(i + 1) come from host tables (glibc log), so every weight is the
 //     reference's value bit for bit.
@@ -22,6 +23,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -31,10 +33,11 @@
 
 namespace {
 
-constexpr int kCesThreads = 1024;
+constexpr int kCesThreads = 512;   // 8 waves: 256 VGPRs per lane, no scratch spills in the serial chain
 constexpr int kCesWaves = kCesThreads / 64;
 constexpr int kMaxVias = 32;
 constexpr int kEliteCap = 8192;  // LDS: 8192 x (8 B key + 4 B slot) = 96 KiB
+constexpr int kLdsKeys = 12288;   // success keys staged in LDS up to this many slots (96 KiB)
 
 struct CesHdr {
     int nfixed;      // fixed slots (mean set [+ forwarded best]) of the current iteration
@@ -49,6 +52,7 @@ struct CesHdr {
 
 struct CesK {
     int K, nslots, samples, cap;
+    int prof;  // profiling only (SSPP_CES_PROF=n): stop after phase n (1 count, 2 select, 3 sort, 4 weights)
     double frac, inc, dec, sigma_floor, var_beta, mean_lr, sd_min, sd_max, dist_z_min, z_min;
     double lo[4], hi[4];
 };
@@ -57,6 +61,8 @@ struct CesReset {
     double mean0[kMaxVias * 4];  // Distribution::reset(mean0) values (z + bound clamps applied)
     double sigma0;               // sigma0_ after the stddev clamps
 };
+
+constexpr unsigned long long kNoKey = ~0ull;  // okey() of a NaN; marks "not a success"
 
 // order-preserving map double -> u64 (-0 folded onto +0: IEEE compares them equal)
 __device__ __forceinline__ unsigned long long okey(double x) {
@@ -104,6 +110,63 @@ __device__ __forceinline__ int block_scan_flag(bool f, int* s_w, int* total) {
     return before + in_wave;
 }
 
+__device__ __forceinline__ int block_sum_int(int v, int* s_w) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < kCesWaves; ++w) t += s_w[w];
+    __syncthreads();
+    return t;
+}
+template <bool MIN>
+__device__ __forceinline__ unsigned long long block_ext_u64(unsigned long long v, unsigned long long* s) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off, 64);
+        v = MIN ? (o < v ? o : v) : (o > v ? o : v);
+    }
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+    __syncthreads();
+    unsigned long long t = s[0];
+    for (int w = 1; w < kCesWaves; ++w) t = MIN ? (s[w] < t ? s[w] : t) : (s[w] > t ? s[w] : t);
+    __syncthreads();
+    return t;
+}
+__device__ __forceinline__ unsigned long long block_min_u64(unsigned long long v, unsigned long long* s) {
+    return block_ext_u64<true>(v, s);
+}
+__device__ __forceinline__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* s) {
+    return block_ext_u64<false>(v, s);
+}
+
+// canonical block sum (or_canon_sum with kCesThreads = 512 lanes): per-wave xor butterfly, then the wave
+// totals in wave order; every thread gets the result
+__device__ __forceinline__ double block_sum(double v, double* s_red) {
+    v = wave_sum64(v);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = s_red[0];
+    for (int w = 1; w < kCesWaves; ++w) t = t + s_red[w];
+    __syncthreads();
+    return t;
+}
+__device__ __forceinline__ void block_sum4(double (&v)[4], double* s_red) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) v[d] = wave_sum64(v[d]);
+    if ((threadIdx.x & 63) == 0)
+        for (int d = 0; d < 4; ++d) s_red[d * kCesWaves + (threadIdx.x >> 6)] = v[d];
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        double t = s_red[d * kCesWaves];
+        for (int w = 1; w < kCesWaves; ++w) t = t + s_red[d * kCesWaves + w];
+        v[d] = t;
+    }
+    __syncthreads();
+}
+
 // plan()'s prologue: reset() (iterate == 0) or keep the distribution, then the iteration's
 // fixed seeds: mean set with z >= cfg.z_min (tsp_planner.h:82-84) and the forwarded best.
 __global__ __launch_bounds__(128) void k_ces_begin(CesK c, int iterate, CesReset r, CesHdr* h,
@@ -133,47 +196,86 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
     CesK c, const double* __restrict__ cost, const unsigned char* __restrict__ status,
     const double* __restrict__ vias, const double* __restrict__ LT, const double* __restrict__ LH,
     CesHdr* h, double* mean, double* sigma, double* lbest, int* elite_out) {
-    __shared__ unsigned long long s_key[kEliteCap];  // keys, later the weights (as double)
+    __shared__ unsigned long long s_key[kLdsKeys];   // all keys, then the elites' keys, then weights
     __shared__ int s_idx[kEliteCap];
-    __shared__ int s_hist[256];
+    __shared__ int s_hist[512];
     __shared__ int s_w[kCesWaves];
-    __shared__ int s_sel[4];
-    __shared__ double s_sumw;
+    __shared__ int s_sel[8];
+    __shared__ double s_red[4 * kCesWaves];
+    __shared__ unsigned long long s_u64[kCesWaves];
+    __shared__ double s_ms[2 * 4 * kMaxVias];  // mean | sigma
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nslots = c.nslots;
-
-    // ---- successes
-    int nsucc = 0;
-    for (int base = 0; base < nslots; base += kCesThreads) {
-        const int i = base + tid;
-        int tot;
-        (void)block_scan_flag(i < nslots && status[i], s_w, &tot);
-        nsucc += tot;
+    // success keys (kNoKey = not a success): staged in LDS once when they fit, else re-read
+    const bool in_lds = nslots <= kLdsKeys;
+    int nmine = 0;
+    unsigned long long kmin = kNoKey, kmax = 0ull;
+#pragma unroll 1
+    for (int i = tid; i < nslots; i += kCesThreads) {
+        unsigned long long key = kNoKey;
+        if (status[i]) key = okey(cost[i]);
+        if (in_lds) s_key[i] = key;
+        if (key != kNoKey) {
+            ++nmine;
+            kmin = key < kmin ? key : kmin;
+            kmax = key > kmax ? key : kmax;
+        }
     }
+    // the distribution, needed at the end, is fetched now (its latency hides under the selection)
+    const int K = c.K, KD = 4 * K;
+    for (int e = tid; e < 2 * KD; e += kCesThreads) s_ms[e] = e < KD ? mean[e] : sigma[e - KD];
+    const int nsucc = block_sum_int(nmine, s_w);  // (its barriers publish s_key and s_ms)
     if (nsucc == 0) {  // adapt(false)
         if (tid < c.K * 4) sigma[tid] = clamp_sd(sigma[tid] * c.inc, c);
         if (tid == 0) { h->nsucc = 0; h->nelite = 0; h->best_slot = -1; h->best_cost = INFINITY; h->iter++; }
         return;
     }
     const int k = (int)((double)nsucc * c.frac) < 1 ? 1 : (int)((double)nsucc * c.frac);
+    if (c.prof == 1) return;
+    kmin = block_min_u64(kmin, s_u64);
+    kmax = block_max_u64(kmax, s_u64);
+    auto key_at = [&](int i) -> unsigned long long {
+        if (in_lds) return s_key[i];
+        return status[i] ? okey(cost[i]) : kNoKey;
+    };
 
-    // ---- radix select of the k-th smallest key among successes (8 passes of 8 bits)
+    // ---- radix select of the k-th smallest key among successes, 8 bits per pass, starting
+    // below the bytes every success key shares (they agree above the top bit of min ^ max)
     unsigned long long prefix = 0ull, pmask = 0ull;
     int kk = k;
-    for (int pass = 7; pass >= 0; --pass) {
-        for (int b = tid; b < 256; b += kCesThreads) s_hist[b] = 0;
-        __syncthreads();
-        const int sh = 8 * pass;
-        for (int i = tid; i < nslots; i += kCesThreads) {
-            if (!status[i]) continue;
-            const unsigned long long key = okey(cost[i]);
-            if ((key & pmask) == prefix) atomicAdd(&s_hist[(key >> sh) & 255ull], 1);
+    const int top = kmin == kmax ? -1 : (63 - __clzll((long long)(kmin ^ kmax))) >> 3;
+    if (top >= 0 && top < 7) {
+        pmask = ~0ull << (8 * (top + 1));
+        prefix = kmin & pmask;
+    }
+    for (int b = tid; b < 512; b += kCesThreads) s_hist[b] = 0;
+    __syncthreads();
+    int eq_cnt = nsucc;  // keys equal to the selected prefix so far (all, before any pass)
+#pragma unroll 1
+    for (int pass = top; pass >= 0; --pass) {
+        int* hist = s_hist + 256 * (pass & 1);  // double-buffered: the other half is cleared
+        const int sh = 8 * pass;                // while wave 0 scans this one
+#pragma unroll 1
+        for (int base = 0; base < nslots; base += kCesThreads) {  // uniform trip count
+            const int i = base + tid;
+            const unsigned long long key = i < nslots ? key_at(i) : kNoKey;
+            bool act = key != kNoKey && (key & pmask) == prefix;
+            const unsigned bin = (unsigned)((key >> sh) & 255ull);
+            // wave-aggregated increments: the high bytes of the keys mostly coincide, so
+            // per-lane LDS atomics on one bin would serialise the whole wave
+            for (unsigned long long m = __ballot(act); m; m = __ballot(act)) {
+                const int leader = __ffsll((long long)m) - 1;
+                const unsigned lb = __shfl(bin, leader, 64);
+                const unsigned long long same = __ballot(act && bin == lb);
+                if (lane == leader) atomicAdd(&hist[lb], __popcll(same));
+                if (bin == lb) act = false;
+            }
         }
         __syncthreads();
         if (wv == 0) {  // inclusive scan of 4 bins per lane, first bin reaching kk
             int v[4], sum = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { v[q] = s_hist[4 * lane + q]; sum += v[q]; }
+            for (int q = 0; q < 4; ++q) { v[q] = hist[4 * lane + q]; sum += v[q]; }
             int inc = sum;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
@@ -189,28 +291,36 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
                     if (cum + v[q] >= kk) { b = q; break; }
                     cum += v[q];
                 }
-                s_sel[0] = 4 * lane + b;
-                s_sel[1] = kk - cum;
+                s_sel[2 * (pass & 1)] = 4 * lane + b;
+                s_sel[2 * (pass & 1) + 1] = kk - cum;
+                s_sel[4 + (pass & 1)] = v[b];
             }
+        } else {
+            int* other = s_hist + 256 * ((pass & 1) ^ 1);
+            for (int b = tid - 64; b < 256; b += kCesThreads - 64) other[b] = 0;
         }
         __syncthreads();
-        prefix |= (unsigned long long)s_sel[0] << sh;
+        prefix |= (unsigned long long)s_sel[2 * (pass & 1)] << sh;
         pmask |= 0xFFull << sh;
-        kk = s_sel[1];
-        __syncthreads();
+        kk = s_sel[2 * (pass & 1) + 1];
+        eq_cnt = s_sel[4 + (pass & 1)];
     }
-    const unsigned long long T = prefix;
+    const unsigned long long T = top < 0 ? kmin : prefix;
     const int need_eq = kk;  // elites with key == T, lowest slots first
+    if (c.prof == 2) return;
 
-    // ---- ordered compaction of the elites (slot order), then bitonic sort on (key, slot)
+    // ---- ordered compaction of the elites (slot order) into s_key / s_idx — in place when
+    // the keys are in LDS: a chunk's keys are read before the scan's barrier and written to
+    // positions <= their own index — then a bitonic sort on (key, slot)
     int eq_seen = 0, nsel = 0;
+#pragma unroll 1
     for (int base = 0; base < nslots; base += kCesThreads) {
         const int i = base + tid;
-        unsigned long long key = ~0ull;
-        const bool ok = i < nslots && status[i];
-        if (ok) key = okey(cost[i]);
-        int eq_tot;
-        const int eq_rank = eq_seen + block_scan_flag(ok && key == T, s_w, &eq_tot);
+        const unsigned long long key = i < nslots ? key_at(i) : kNoKey;
+        const bool ok = key != kNoKey;
+        int eq_tot = 0, eq_rank = 0;
+        if (need_eq < eq_cnt)  // uniform: only a tie at the threshold needs the slot order
+            eq_rank = eq_seen + block_scan_flag(ok && key == T, s_w, &eq_tot);
         const bool sel = ok && (key < T || (key == T && eq_rank < need_eq));
         int sel_tot;
         const int pos = nsel + block_scan_flag(sel, s_w, &sel_tot);
@@ -218,6 +328,7 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
         eq_seen += eq_tot;
         nsel += sel_tot;
     }
+    __syncthreads();
     int P = 1;
     while (P < k) P <<= 1;
     for (int i = k + tid; i < P; i += kCesThreads) { s_key[i] = ~0ull; s_idx[i] = INT_MAX; }
@@ -232,49 +343,94 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
                 const bool gt = ka > kb || (ka == kb && ia > ib);
                 if (gt == up) { s_key[lo] = kb; s_key[hi] = ka; s_idx[lo] = ib; s_idx[hi] = ia; }
             }
-            __syncthreads();
+            // With stride <= 64 the pairs of wave w lie in entries [128 w, 128 w + 128) (t runs
+            // over 64 consecutive values, a multiple of stride), so consecutive stages that both
+            // have stride <= 64 touch wave-private data: a wave-level fence is enough.  After
+            // stride 1 the next stage starts a new size (stride = size): full barrier.
+            if (stride > 1 && stride <= 64) {
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            } else {
+                __syncthreads();
+            }
         }
     }
 
-    // ---- CES log weights (tsp_elites.h:24-32): w_j = log(k + 0.5) - log(j + 1), normalised
+    // ---- CES log weights (tsp_elites.h:24-32): w_j = log(k + 0.5) - log(j + 1), normalised.
+    // Every sum below is the canonical 512-lane order of or_canon_sum(x, n, 512): thread t
+    // accumulates j = t, t + 512, ... in order, xor butterfly per wave, waves in order.
+    if (c.prof == 3) return;
     const double lk = LH[k];
-    if (wv == 0) {
-        double a = 0.0;
-        for (int j = lane; j < k; j += 64) a = a + (lk - LT[j + 1]);
-        a = wave_sum64(a);
-        if (lane == 0) s_sumw = a;
-    }
-    __syncthreads();
+    double a = 0.0;
+    for (int j = tid; j < k; j += kCesThreads) a = a + (lk - LT[j + 1]);
+    const double sumw = block_sum(a, s_red);
     double* s_wt = reinterpret_cast<double*>(s_key);
-    const double sumw = s_sumw;
     for (int j = tid; j < k; j += kCesThreads) s_wt[j] = (lk - LT[j + 1]) / sumw;
     __syncthreads();
 
-    // ---- Distribution::update (tsp_distribution.h:52-83) + adapt(true), one wave per (via, dim)
-    const int K = c.K, KD = 4 * K;
-    for (int q = wv; q < KD; q += kCesWaves) {
-        const int d = q & 3;
-        double a = 0.0;
-        for (int j = lane; j < k; j += 64) a = a + s_wt[j] * vias[(long long)s_idx[j] * KD + q];
-        const double em = wave_sum64(a);
-        const double m0 = mean[q];
-        double nm = m0 + c.mean_lr * (em - m0);
-        if (d == 2) nm = nm < c.dist_z_min ? c.dist_z_min : nm;
-        nm = nm < c.lo[d] ? c.lo[d] : (c.hi[d] < nm ? c.hi[d] : nm);  // std::clamp
-        const bool wrap = d == 3 && c.lo[3] != c.hi[3];
-        double v = 0.0;
-        for (int j = lane; j < k; j += 64) {
-            const double x = vias[(long long)s_idx[j] * KD + q];
-            const double df = wrap ? wrap_diff(x, nm, c.lo[3], c.hi[3]) : x - nm;
-            v = v + s_wt[j] * (df * df);
+    if (c.prof == 4) return;
+    // ---- Distribution::update (tsp_distribution.h:52-83) + adapt(true), via by via: every
+    // thread gathers its elites' 4 coordinates once per pass, all 512 lanes reduce
+    const bool cache = k <= 2 * kCesThreads;  // each thread's <= 2 elites stay in registers
+    for (int v = 0; v < K; ++v) {
+        double em[4] = {0.0, 0.0, 0.0, 0.0}, xc0[4], xc1[4];
+        int r = 0;
+        for (int j = tid; j < k; j += kCesThreads, ++r) {
+            const double* x = vias + (long long)s_idx[j] * KD + 4 * v;
+            const double w = s_wt[j];
+            double xv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) xv[d] = x[d];
+            if (cache) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    if (r == 0) xc0[d] = xv[d];
+                    else xc1[d] = xv[d];
+                }
+            }
+#pragma unroll
+            for (int d = 0; d < 4; ++d) em[d] = em[d] + w * xv[d];
         }
-        const double ve = wave_sum64(v);
-        const double s0 = sigma[q];
-        const double pv = s0 * s0;
-        const double blend = (1.0 - c.var_beta) * pv + c.var_beta * ve;
-        double sg = clamp_sd(sqrt(blend), c);
-        sg = clamp_sd(sg * c.dec, c);  // adapt(true)
-        if (lane == 0) { mean[q] = nm; sigma[q] = sg; }
+        block_sum4(em, s_red);
+        double nm[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const double m0 = s_ms[4 * v + d];
+            double t = m0 + c.mean_lr * (em[d] - m0);
+            if (d == 2) t = t < c.dist_z_min ? c.dist_z_min : t;
+            nm[d] = t < c.lo[d] ? c.lo[d] : (c.hi[d] < t ? c.hi[d] : t);  // std::clamp
+        }
+        const bool wrap = c.lo[3] != c.hi[3];
+        double ve[4] = {0.0, 0.0, 0.0, 0.0};
+        r = 0;
+        for (int j = tid; j < k; j += kCesThreads, ++r) {
+            double xv[4];
+            if (cache) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) xv[d] = r == 0 ? xc0[d] : xc1[d];
+            } else {
+                const double* x = vias + (long long)s_idx[j] * KD + 4 * v;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) xv[d] = x[d];
+            }
+            const double w = s_wt[j];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const double df = (d == 3 && wrap) ? wrap_diff(xv[3], nm[3], c.lo[3], c.hi[3]) : xv[d] - nm[d];
+                ve[d] = ve[d] + w * (df * df);
+            }
+        }
+        block_sum4(ve, s_red);
+        if (tid < 4) {
+            const int d = tid;
+            const double s0 = s_ms[KD + 4 * v + d];
+            const double pv = s0 * s0;
+            const double blend = (1.0 - c.var_beta) * pv + c.var_beta * ve[d];
+            double sg = clamp_sd(sqrt(blend), c);
+            sg = clamp_sd(sg * c.dec, c);  // adapt(true)
+            mean[4 * v + d] = nm[d];
+            sigma[4 * v + d] = sg;
+        }
     }
 
     // ---- best = first minimum in slot order (std::min_element): the sort's first entry
@@ -356,6 +512,8 @@ static CesK ces_k(const sspp_ces* p) {
     c.sd_min = p->cfg.stddev_min; c.sd_max = p->cfg.stddev_max;
     c.dist_z_min = p->cfg.dist_z_min; c.z_min = p->cfg.z_min;
     for (int i = 0; i < 4; ++i) { c.lo[i] = p->lo[i]; c.hi[i] = p->hi[i]; }
+    static const int prof = [] { const char* e = getenv("SSPP_CES_PROF"); return e ? atoi(e) : 0; }();
+    c.prof = prof;
     return c;
 }
 

@@ -297,7 +297,15 @@ __device__ __forceinline__ void mover_poses(const double* q, cmover_t movers,
         } else {
             double half = q[3] * 0.5;
             qp[0] = q[0]; qp[1] = q[1]; qp[2] = q[2];
+#ifdef SSPP_YAW_SINCOS
+            double sh, ch;
+            sincos(half, &sh, &ch);
+            qp[3] = ch; qp[4] = 0.0; qp[5] = 0.0; qp[6] = sh;
+#elif defined(SSPP_PROF_NOTRIG)  // profiling variant only: wrong poses, timing of the rest
+            qp[3] = 1.0 - half * half; qp[4] = 0.0; qp[5] = 0.0; qp[6] = half;
+#else
             qp[3] = cos(half); qp[4] = 0.0; qp[5] = 0.0; qp[6] = sin(half);
+#endif
         }
         normalize4(qp + 3);
         quat2mat(qp + 3, mR[m]);
@@ -320,6 +328,40 @@ __device__ __forceinline__ void geom_pose(const double* P, const double* R, cons
     }
 }
 
+__device__ __forceinline__ void geom_pos(const double* P, const double* R, const DGeom& G, double* gp) {
+    double t[3];
+    matvec3(R, G.pos, t);
+    gp[0] = P[0] + t[0]; gp[1] = P[1] + t[1]; gp[2] = P[2] + t[2];
+}
+__device__ __forceinline__ void geom_rot(const double* R, const DGeom& G, double* gm) {
+    if (G.relrot) {
+        matmul3(R, G.mat, gm);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) gm[k] = R[k];
+    }
+}
+
+// Per-waypoint broadphase of one pair (exact: it only rejects pairs whose narrowphase cannot
+// report dist < margin).  Two spheres: MuJoCo's bounding-sphere test.  Plane vs a bounded
+// geom: every point of the geom lies within rbound of its centre, so a centre height over the
+// plane above rbound + margin (+ kHullPad for rounding) rules out a contact — the plane-box
+// corners satisfy t >= h - sum_j |n.a_j| e_j >= h - |e| = h - rbound (Cauchy-Schwarz).
+__device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const double* gp,
+                                          const double* op, const double* om) {
+    const double ro = pr.orbound;
+    if (rg > 0.0 && ro > 0.0) {
+        const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
+        const double thr = rg + ro + pr.margin;
+        return !(dot3(dc, dc) > thr * thr);
+    }
+    if (pr.otype == 0 && rg > 0.0) {
+        const double h = (gp[0] - op[0]) * om[2] + (gp[1] - op[1]) * om[5] + (gp[2] - op[2]) * om[8];
+        return !(h - rg > pr.margin + kHullPad);
+    }
+    return true;
+}
+
 // DEEP=false: checkCollision's ncon > 0 for one candidate.  Every active lane of the wave
 //   must belong to that candidate: the scan stops for the whole wave at the first pair where
 //   any lane finds a contact (returns 1 on every lane — the candidate is infeasible whatever
@@ -337,6 +379,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
     double acc = 0.0;
     int cur = -1;
     double gp[3], gmat[9];
+    bool have_rot = true;  // multi-geom movers: a geom's rotation is formed at its first near pair
     DGeom G;
     if (ONEGEOM) {  // every pair shares one moving geom: pose once, mover pose dies here
         cur = pairs[0].gm;
@@ -357,7 +400,8 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             cur = pr.gm;
             G = load_geom(geoms + cur);
             const bool second = NM > 1 && G.mover == 1;
-            geom_pose(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp, gmat);
+            geom_pos(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp);
+            have_rot = false;
         }
         double op_[3], om_[9];
         const double* op = pr.opos;
@@ -372,15 +416,14 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             matmul3(R, pr.omat, om_);
             op = op_; om = om_;
         }
-        const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
-        const double rg = G.rbound, ro = pr.orbound;
-        bool near = true;
-        if (rg > 0.0 && ro > 0.0) {
-            const double thr = rg + ro + pr.margin;
-            near = !(dot3(dc, dc) > thr * thr);
-        }
+        const bool near = pair_near(pr, G.rbound, gp, op, om);
         int nd = 0, nc = 0;
         if (near) {
+            if (!ONEGEOM && !have_rot) {
+                const bool second = NM > 1 && G.mover == 1;
+                geom_rot(second ? mR[NM - 1] : mR[0], G, gmat);
+                have_rot = true;
+            }
             const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
             if (gfirst) nc = collide<DEEP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
             else nc = collide<DEEP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
@@ -391,6 +434,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
                 return 1;
         } else if (nd > 0) {
+            const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
             const double cd = sqrt(dot3(dc, dc));
             const double term = -1.0 / (cd + 1e-4);
             for (int i = 0; i < nd; ++i) acc = acc + term;
@@ -762,6 +806,7 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
     mover_poses<D, NM, 0>(q, (cmover_t)T.movers, mp, mR);
     int cur = -1;
     double gp[3], gmat[9];
+    bool have_rot = true;
     DGeom G;
     if (ONEGEOM) {
         cur = pairs[0].gm;
@@ -782,7 +827,8 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
             cur = pr.gm;
             G = load_geom(geoms + cur);
             const bool second = NM > 1 && G.mover == 1;
-            geom_pose(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp, gmat);
+            geom_pos(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp);
+            have_rot = false;
         }
         int nc = 0;
         if (live && (k >= 64 || ((mymask >> k) & 1ull))) {
@@ -799,14 +845,12 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
                 matmul3(R, pr.omat, om_);
                 op = op_; om = om_;
             }
-            const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
-            const double rg = G.rbound, ro = pr.orbound;
-            bool near = true;
-            if (rg > 0.0 && ro > 0.0) {
-                const double thr = rg + ro + pr.margin;
-                near = !(dot3(dc, dc) > thr * thr);
-            }
-            if (near) {
+            if (pair_near(pr, G.rbound, gp, op, om)) {
+                if (!ONEGEOM && !have_rot) {
+                    const bool second = NM > 1 && G.mover == 1;
+                    geom_rot(second ? mR[NM - 1] : mR[0], G, gmat);
+                    have_rot = true;
+                }
                 int nd = 0;
                 const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
                 if (gfirst) nc = collide<false>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
@@ -1092,8 +1136,11 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
 
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
 // tab: (cp+1) rows of 3 basis values at u = i * (1/cp); Minv: collocation inverse (n x n).
+#ifndef SSPP_TSP_WAVES_PER_EU
+#define SSPP_TSP_WAVES_PER_EU 4
+#endif
 template <int NM, bool ONEGEOM>
-__global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_tsp(
+__global__ __launch_bounds__(kBlock, SSPP_TSP_WAVES_PER_EU) void k_tsp(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
     const double* __restrict__ sigma, const double* __restrict__ vias_in,
@@ -1207,7 +1254,9 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_tsp(
             eval_pt<D, P>(myc, tab + i * P1, span[i], pc);
             aL = aL + dist_nd<D>(pv, pc);
             double c = 0.0;
+#ifndef SSPP_PROF_NOCOLL  // profiling variant only
             point_collide<D, NM, 1, true, ONEGEOM>(pc, a.sc, T, mask, &c);
+#endif
             const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
             const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
             aC = aC + c;
