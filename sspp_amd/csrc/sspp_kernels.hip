@@ -790,6 +790,7 @@ struct SsppC2F {
     int nblk_step;
     long long step_stride;
     int arc_all;   // 0: arc length only for collision-free candidates (+inf otherwise)
+    int hull;      // candidate hull broadphase: 0 off, 1 all candidates, 2 phase-1 survivors
 };
 
 // Pair loop of one waypoint per lane.  All 64 lanes run the (wave-uniform) loop; `live` lanes
@@ -959,7 +960,11 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     // ---- candidate-level broadphase (convex hull of the control points, see pair_may_touch):
     // AABB per (candidate, mover, axis), then one (candidate, pair) test per thread; the mask
     // bits are OR-ed into LDS.
-    if (collide_on && !(a.ablate & 32)) {
+    // hull = 1: every candidate before phase 1; hull = 2 (default): only phase 1's survivors,
+    // before phase 2 — phase 1 stops at the first touching pair anyway, and on robocrane the
+    // all-candidate hull cost more than it saved (measured: 1.11 vs 1.22 G cand/s without it)
+    const int hull = (a.ablate & 32) ? 0 : a.hull;
+    if (collide_on && hull == 1) {
         for (int e = tid; e < cpb * NB; e += NT) {
             const int sl = e / NB, md = e - sl * NB, m = md / 3, d = md - m * 3;
             const int col = 7 * m + d;
@@ -1029,6 +1034,38 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
         __syncthreads();
         const int ns = s_surv[cpb];
+        if (hull == 2 && ns > 0 && np <= 64) {  // the survivors' hull masks (see above)
+            for (int e = tid; e < ns * NB; e += NT) {
+                const int si = e / NB, md = e - si * NB, m = md / 3, d = md - m * 3;
+                const int sl = s_surv[si], col = 7 * m + d;
+                double lo, hi;
+                if (col < D) {
+                    const double* c = s_ctrl + sl * ndof + col;
+                    lo = hi = c[0];
+                    for (int j = 1; j < n; ++j) {
+                        const double v = c[j * D];
+                        lo = v < lo ? v : lo;
+                        hi = v > hi ? v : hi;
+                    }
+                } else {
+                    lo = hi = (double)((cmover_t)TT.movers)[m].qpos0[d];
+                }
+                s_box[sl * 2 * NB + md] = lo;
+                s_box[sl * 2 * NB + NB + md] = hi;
+            }
+            if (tid < ns) s_mask[s_surv[tid]] = 0ull;
+            __syncthreads();
+            for (int e = tid; e < ns * np; e += NT) {
+                const int si = e / np, k = e - si * np, sl = s_surv[si];
+                const DPair pr = load_pair((cpair_t)TT.pairs + k);
+                const DGeom G = load_geom((cgeom_t)TT.geoms + pr.gm);
+                const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
+                const double* bx = s_box + sl * 2 * NB;
+                if (pair_may_touch(pr, G, bx + 3 * m, bx + NB + 3 * m))
+                    atomicOr(s_mask + sl, 1ull << k);
+            }
+            __syncthreads();
+        }
         unsigned long long umask = 0ull;
         for (int i = 0; i < ns; ++i) umask |= s_mask[s_surv[i]];
         const int items = ns * R;
@@ -1389,6 +1426,7 @@ struct sspp_job {
     // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
     int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16, nt2 = 256;
     int arc_all = 0;           // arc length for every candidate (else collision-free only)
+    int hull = 2;              // c2f hull broadphase (SSPP_HULL: 0 off, 1 all, 2 survivors)
     size_t lds2 = 0;
     double* d_otab = nullptr;  // collision rows in coarse-to-fine order
     int* d_ospan = nullptr;
@@ -1829,6 +1867,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     if (j->npert < 0) j->npert = 0;
     { const char* e = getenv("SSPP_KERNEL"); j->c2f = e ? atoi(e) != 0 : 1; }
     { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : (j->c2f ? 1 : 0); }
+    { const char* e = getenv("SSPP_HULL"); j->hull = e ? atoi(e) : 2; }
     {
         // defaults measured on MI355X (robocrane, 8 steps/launch, 4 streams): one-wave
         // workgroups of 8 candidates x 8 phase-1 lanes — 1.12 G cand/s vs 0.69 G for 256 x 16
@@ -2014,6 +2053,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         c.nblk_step = nblk;
         c.step_stride = step_stride;
         c.arc_all = j->arc_all;
+        c.hull = j->hull;
         e = j->p == 3 ? dispatch_c2f_p<3>(c, j, o, nblk * steps, st) : dispatch_c2f_p<2>(c, j, o, nblk * steps, st);
     } else {
         e = j->p == 3 ? dispatch_sspp_p<3>(k, j, o, nblk, st) : dispatch_sspp_p<2>(k, j, o, nblk, st);

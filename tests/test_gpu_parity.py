@@ -320,3 +320,19 @@ def test_config4_full_size_shards(robocrane):
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, ctrl, W)
     np.testing.assert_array_equal(f[sub], feas_o)
     assert arc_err(a[sub], arc_o) <= COST_TOL
+
+
+@pytest.mark.parametrize("hull", ["0", "1", "2"])
+def test_hull_modes_identical(robocrane, monkeypatch, hull):
+    """The candidate hull broadphase is exact: off / before phase 1 / survivors only give the
+    same per-candidate results, equal to the oracle."""
+    import sspp_amd as S
+    _, scene, oscene = robocrane
+    monkeypatch.setenv("SSPP_HULL", hull)
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=2048)
+    r = run_sspp(job, 2048, first=4096)
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 128)
+    np.testing.assert_array_equal(r["feasible"], feas_o)
+    assert arc_err(r["arc"], arc_o) <= COST_TOL
+    assert r["best"][1] == (O.argmin(arc_o, feas_o)[0] + 4096 if feas_o.any() else -1)
