@@ -793,6 +793,13 @@ struct SsppC2F {
     int hull;      // candidate hull broadphase: 0 off, 1 all candidates, 2 phase-1 survivors
 };
 
+#ifdef SSPP_C2F_STATS  // profiling builds only (tools/build_variant.sh stats -DSSPP_C2F_STATS)
+__device__ unsigned long long g_c2f_stats[16];
+#define C2F_STAT(i, v) do { const unsigned long long v_ = (v); if ((threadIdx.x & 63) == 0 && v_) atomicAdd(&g_c2f_stats[i], v_); } while (0)
+#else
+#define C2F_STAT(i, v) do { } while (0)
+#endif
+
 // Pair loop of one waypoint per lane.  All 64 lanes run the (wave-uniform) loop; `live` lanes
 // test the pairs of their own mask.  gbits = the lanes of this lane's candidate within the
 // wave: when any of them touches, all of them stop (returns true for the group).  flag: the
@@ -846,7 +853,9 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
                 matmul3(R, pr.omat, om_);
                 op = op_; om = om_;
             }
-            if (pair_near(pr, G.rbound, gp, op, om)) {
+            const bool nr = pair_near(pr, G.rbound, gp, op, om);
+            C2F_STAT(2, __popcll(__ballot(nr)));
+            if (nr) {
                 if (!ONEGEOM && !have_rot) {
                     const bool second = NM > 1 && G.mover == 1;
                     geom_rot(second ? mR[NM - 1] : mR[0], G, gmat);
@@ -858,6 +867,8 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
                 else nc = collide<false>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
             }
         }
+        C2F_STAT(flag ? 4 : 0, 1);                          // wave pair iterations (phase 2 / 1)
+        C2F_STAT(flag ? 5 : 1, __popcll(__ballot(live && (k >= 64 || ((mymask >> k) & 1ull)))));
         if (__ballot(nc > 0) & gbits) { ghit = true; live = false; }
         if (flag && live && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
             live = false;
@@ -1034,6 +1045,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
         __syncthreads();
         const int ns = s_surv[cpb];
+        if (tid == 0) C2F_STAT(6, ns);
         if (hull == 2 && ns > 0 && np <= 64) {  // the survivors' hull masks (see above)
             for (int e = tid; e < ns * NB; e += NT) {
                 const int si = e / NB, md = e - si * NB, m = md / 3, d = md - m * 3;
@@ -1154,8 +1166,10 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
     }
     __syncthreads();
+    if (tid == 0) C2F_STAT(7, nvalid);
     if (tid < nvalid) {
         const long long c = cand0 + tid;
+        if (s_feas[tid]) C2F_STAT(8, 0);
         arc[c] = s_arc[tid];
         feasible[c] = (unsigned char)(s_feas[tid] != 0);
     }
@@ -2294,6 +2308,18 @@ extern "C" int sspp_best_reduce_steps(const sspp_best* d_parts, int R, int G, ss
     if (e != hipSuccess) return hip_fail(e, "k_argmin_steps launch");
     return SSPP_OK;
 }
+
+#ifdef SSPP_C2F_STATS
+extern "C" int sspp_debug_c2f_stats(unsigned long long* out, int reset) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c2f_stats), sizeof(unsigned long long) * 16);
+    if (reset) {
+        unsigned long long z[16] = {0};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_c2f_stats), z, sizeof z);
+    }
+    return 0;
+}
+#endif
 
 extern "C" int sspp_device_count(int* n) {
     int c = 0;

@@ -336,3 +336,34 @@ def test_hull_modes_identical(robocrane, monkeypatch, hull):
     np.testing.assert_array_equal(r["feasible"], feas_o)
     assert arc_err(r["arc"], arc_o) <= COST_TOL
     assert r["best"][1] == (O.argmin(arc_o, feas_o)[0] + 4096 if feas_o.any() else -1)
+
+
+@pytest.mark.parametrize("goal", [0, 3, 5])
+def test_gripper_tsp_matches_oracle(cuda, goal):
+    """Multi-geom mover (robocrane gripper: 7 collidable geoms, k_tsp<1, false>, lazy geom
+    rotation, exact plane cull): per-candidate L / C_nf / C_wf / cost and status vs the oracle
+    on the device's own via sets; the multi-goal bench scenarios (BASELINE configs[4])."""
+    import sspp_amd as S
+    import torch
+    import bench
+    model = S.Model(ROBOCRANE)
+    body = model.body_id("gripper_collision_with_block/")
+    scene = S.Scene(model, 1, body)
+    oscene = O.Scene(mjcf_ref.load(ROBOCRANE), 1, body)
+    start, end = (np.array(x) for x in bench.MULTIGOAL[goal])
+    B, cp = 3000, 96
+    mean = (start + 0.5 * (end - start)).reshape(1, 4)
+    sigma = np.array([[0.15, 0.15, 0.15, 0.5]])
+    job = S.TspJob(scene, start, end, 1, cp, mean=mean, sigma=sigma, lo=bench.MG_LO,
+                   hi=bench.MG_HI, max_batch=B)
+    out = job.alloc(B, with_vias=True)
+    job.sample_score(0, B, out["L"], out["Cnf"], out["Cwf"], out["status"], out["cost"],
+                     out["best"], vias_out=out["vias"])
+    torch.cuda.synchronize()
+    vias = _np(out["vias"])
+    L, Cnf, Cwf, st, cost = O.tsp_score(oscene, start, end, vias, cp)
+    np.testing.assert_array_equal(_np(out["status"]), st)
+    for a, b in ((out["L"], L), (out["Cnf"], Cnf), (out["Cwf"], Cwf), (out["cost"], cost)):
+        assert np.abs(_np(a) - b).max() <= 1e-9
+    assert 0 < st.sum() < B  # both outcomes present
+    assert S.decode_best(out["best"])[1] == O.tsp_best(cost, st)[0]
