@@ -36,8 +36,7 @@ namespace {
 constexpr int kCesThreads = 512;   // 8 waves: 256 VGPRs per lane, no scratch spills in the serial chain
 constexpr int kCesWaves = kCesThreads / 64;
 constexpr int kMaxVias = 32;
-constexpr int kEliteCap = 8192;  // LDS: 8192 x (8 B key + 4 B slot) = 96 KiB
-constexpr int kLdsKeys = 12288;   // success keys staged in LDS up to this many slots (96 KiB)
+constexpr int kEliteCap = 8192;  // LDS of k_ces_update: 8192 x (8 B weight + 4 B slot) = 96 KiB
 
 struct CesHdr {
     int nfixed;      // fixed slots (mean set [+ forwarded best]) of the current iteration
@@ -52,7 +51,6 @@ struct CesHdr {
 
 struct CesK {
     int K, nslots, samples, cap;
-    int prof;  // profiling only (SSPP_CES_PROF=n): stop after phase n (1 count, 2 select, 3 sort, 4 weights)
     double frac, inc, dec, sigma_floor, var_beta, mean_lr, sd_min, sd_max, dist_z_min, z_min;
     double lo[4], hi[4];
 };
@@ -90,55 +88,6 @@ __device__ __forceinline__ double wrap_diff(double a, double b, double mn, doubl
     while (d > 0.5 * range) d -= range;
     while (d < -0.5 * range) d += range;
     return d;
-}
-
-// exclusive block scan of a 0/1 flag; *total receives the block's count (all threads call)
-__device__ __forceinline__ int block_scan_flag(bool f, int* s_w, int* total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const unsigned long long m = __ballot(f);
-    const int in_wave = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) s_w[w] = __popcll(m);
-    __syncthreads();
-    int before = 0, tot = 0;
-    for (int k = 0; k < kCesWaves; ++k) {
-        const int v = s_w[k];
-        before += k < w ? v : 0;
-        tot += v;
-    }
-    __syncthreads();
-    *total = tot;
-    return before + in_wave;
-}
-
-__device__ __forceinline__ int block_sum_int(int v, int* s_w) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
-    __syncthreads();
-    int t = 0;
-    for (int w = 0; w < kCesWaves; ++w) t += s_w[w];
-    __syncthreads();
-    return t;
-}
-template <bool MIN>
-__device__ __forceinline__ unsigned long long block_ext_u64(unsigned long long v, unsigned long long* s) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const unsigned long long o = __shfl_xor(v, off, 64);
-        v = MIN ? (o < v ? o : v) : (o > v ? o : v);
-    }
-    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
-    __syncthreads();
-    unsigned long long t = s[0];
-    for (int w = 1; w < kCesWaves; ++w) t = MIN ? (s[w] < t ? s[w] : t) : (s[w] > t ? s[w] : t);
-    __syncthreads();
-    return t;
-}
-__device__ __forceinline__ unsigned long long block_min_u64(unsigned long long v, unsigned long long* s) {
-    return block_ext_u64<true>(v, s);
-}
-__device__ __forceinline__ unsigned long long block_max_u64(unsigned long long v, unsigned long long* s) {
-    return block_ext_u64<false>(v, s);
 }
 
 // canonical block sum (or_canon_sum with kCesThreads = 512 lanes): per-wave xor butterfly, then the wave
@@ -191,184 +140,90 @@ __global__ __launch_bounds__(128) void k_ces_begin(CesK c, int iterate, CesReset
     }
 }
 
-// Elite selection + Distribution::update + best pick + adapt, one workgroup.
-__global__ __launch_bounds__(kCesThreads) void k_ces_update(
-    CesK c, const double* __restrict__ cost, const unsigned char* __restrict__ status,
-    const double* __restrict__ vias, const double* __restrict__ LT, const double* __restrict__ LH,
-    CesHdr* h, double* mean, double* sigma, double* lbest, int* elite_out) {
-    __shared__ unsigned long long s_key[kLdsKeys];   // all keys, then the elites' keys, then weights
-    __shared__ int s_idx[kEliteCap];
-    __shared__ int s_hist[512];
-    __shared__ int s_w[kCesWaves];
-    __shared__ int s_sel[8];
-    __shared__ double s_red[4 * kCesWaves];
-    __shared__ unsigned long long s_u64[kCesWaves];
-    __shared__ double s_ms[2 * 4 * kMaxVias];  // mean | sigma
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int nslots = c.nslots;
-    // success keys (kNoKey = not a success): staged in LDS once when they fit, else re-read
-    const bool in_lds = nslots <= kLdsKeys;
-    int nmine = 0;
-    unsigned long long kmin = kNoKey, kmax = 0ull;
-#pragma unroll 1
-    for (int i = tid; i < nslots; i += kCesThreads) {
-        unsigned long long key = kNoKey;
-        if (status[i]) key = okey(cost[i]);
-        if (in_lds) s_key[i] = key;
-        if (key != kNoKey) {
-            ++nmine;
-            kmin = key < kmin ? key : kmin;
-            kmax = key > kmax ? key : kmax;
+// ---- elite selection by rank counting (three launches, no sort, no host round trip) ----
+// The elites are the successes of rank < k in the (cost, slot) order — EliteSelector::select's
+// partial_sort with ties to the lowest slot.  Ranks are counted tile against tile
+// over the whole chip (k_ces_rank: rank[s] += #{j in key tile : (key_j, j) < (key_s, s)}), then
+// each success is scattered to by_rank[rank[s]] (k_ces_scatter).  rank[] and the success
+// counter are re-armed by the kernels that consume them (zeroed once at creation).
+constexpr int kRankTile = 256;
+__global__ __launch_bounds__(kRankTile) void k_ces_rank(int nslots, const double* __restrict__ cost,
+                                                        const unsigned char* __restrict__ status,
+                                                        int* rank, int* nsucc) {
+    __shared__ unsigned long long s_k[kRankTile];
+    const int ts = blockIdx.x, tk = blockIdx.y, tid = threadIdx.x;
+    const int j0 = tk * kRankTile, s = ts * kRankTile + tid, j = j0 + tid;
+    s_k[tid] = (j < nslots && status[j]) ? okey(cost[j]) : kNoKey;  // kNoKey pads the last tile
+    const unsigned long long ks = (s < nslots && status[s]) ? okey(cost[s]) : kNoKey;
+    __syncthreads();
+    if (tk == 0) {  // success count, one atomic per wave
+        const unsigned long long m = __ballot(ks != kNoKey);
+        if ((tid & 63) == 0 && m) atomicAdd(nsucc, (int)__popcll(m));
+    }
+    if (ks == kNoKey) return;
+    // (key_j, j) < (key_s, s) over the tile; padding entries (kNoKey) never count because
+    // ks < kNoKey.  Entries are LDS broadcasts (every lane reads the same address), unrolled so
+    // the reads pipeline.
+    int cnt = 0;
+    const int d = s - j0;  // entries q < d have a lower slot than s
+    if (j0 + kRankTile <= nslots) {
+#pragma unroll 16
+        for (int q = 0; q < kRankTile; ++q) {
+            const unsigned long long kj = s_k[q];
+            cnt += (kj < ks) || (kj == ks && q < d);
+        }
+    } else {  // last, partial tile
+        const int jn = nslots - j0;
+        for (int q = 0; q < jn; ++q) {
+            const unsigned long long kj = s_k[q];
+            cnt += (kj < ks) || (kj == ks && q < d);
         }
     }
-    // the distribution, needed at the end, is fetched now (its latency hides under the selection)
+    if (cnt) atomicAdd(rank + s, cnt);
+}
+__global__ __launch_bounds__(256) void k_ces_scatter(int nslots, const double* __restrict__ cost,
+                                                     const unsigned char* __restrict__ status,
+                                                     int* rank, int* by_rank) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= nslots) return;
+    if (status[s] && okey(cost[s]) != kNoKey) by_rank[rank[s]] = s;
+    rank[s] = 0;  // re-armed for the next update
+}
+
+// Distribution::update + best pick + adapt on the ranked elites, one workgroup.
+__global__ __launch_bounds__(kCesThreads) void k_ces_update(
+    CesK c, const double* __restrict__ cost, const int* __restrict__ by_rank,
+    int* nsucc_p, const double* __restrict__ vias,
+    const double* __restrict__ LT, const double* __restrict__ LH, CesHdr* h, double* mean,
+    double* sigma, double* lbest, int* elite_out) {
+    __shared__ double s_wt[kEliteCap];
+    __shared__ int s_idx[kEliteCap];
+    __shared__ double s_red[4 * kCesWaves];
+    __shared__ double s_ms[2 * 4 * kMaxVias];  // mean | sigma
+    const int tid = threadIdx.x;
     const int K = c.K, KD = 4 * K;
     for (int e = tid; e < 2 * KD; e += kCesThreads) s_ms[e] = e < KD ? mean[e] : sigma[e - KD];
-    const int nsucc = block_sum_int(nmine, s_w);  // (its barriers publish s_key and s_ms)
+    const int nsucc = *nsucc_p;
     if (nsucc == 0) {  // adapt(false)
-        if (tid < c.K * 4) sigma[tid] = clamp_sd(sigma[tid] * c.inc, c);
+        if (tid < KD) sigma[tid] = clamp_sd(sigma[tid] * c.inc, c);
         if (tid == 0) { h->nsucc = 0; h->nelite = 0; h->best_slot = -1; h->best_cost = INFINITY; h->iter++; }
         return;
     }
     const int k = (int)((double)nsucc * c.frac) < 1 ? 1 : (int)((double)nsucc * c.frac);
-    if (c.prof == 1) return;
-    kmin = block_min_u64(kmin, s_u64);
-    kmax = block_max_u64(kmax, s_u64);
-    auto key_at = [&](int i) -> unsigned long long {
-        if (in_lds) return s_key[i];
-        return status[i] ? okey(cost[i]) : kNoKey;
-    };
-
-    // ---- radix select of the k-th smallest key among successes, 8 bits per pass, starting
-    // below the bytes every success key shares (they agree above the top bit of min ^ max)
-    unsigned long long prefix = 0ull, pmask = 0ull;
-    int kk = k;
-    const int top = kmin == kmax ? -1 : (63 - __clzll((long long)(kmin ^ kmax))) >> 3;
-    if (top >= 0 && top < 7) {
-        pmask = ~0ull << (8 * (top + 1));
-        prefix = kmin & pmask;
-    }
-    for (int b = tid; b < 512; b += kCesThreads) s_hist[b] = 0;
+    for (int j = tid; j < k; j += kCesThreads) s_idx[j] = by_rank[j];
     __syncthreads();
-    int eq_cnt = nsucc;  // keys equal to the selected prefix so far (all, before any pass)
-#pragma unroll 1
-    for (int pass = top; pass >= 0; --pass) {
-        int* hist = s_hist + 256 * (pass & 1);  // double-buffered: the other half is cleared
-        const int sh = 8 * pass;                // while wave 0 scans this one
-#pragma unroll 1
-        for (int base = 0; base < nslots; base += kCesThreads) {  // uniform trip count
-            const int i = base + tid;
-            const unsigned long long key = i < nslots ? key_at(i) : kNoKey;
-            bool act = key != kNoKey && (key & pmask) == prefix;
-            const unsigned bin = (unsigned)((key >> sh) & 255ull);
-            // wave-aggregated increments: the high bytes of the keys mostly coincide, so
-            // per-lane LDS atomics on one bin would serialise the whole wave
-            for (unsigned long long m = __ballot(act); m; m = __ballot(act)) {
-                const int leader = __ffsll((long long)m) - 1;
-                const unsigned lb = __shfl(bin, leader, 64);
-                const unsigned long long same = __ballot(act && bin == lb);
-                if (lane == leader) atomicAdd(&hist[lb], __popcll(same));
-                if (bin == lb) act = false;
-            }
-        }
-        __syncthreads();
-        if (wv == 0) {  // inclusive scan of 4 bins per lane, first bin reaching kk
-            int v[4], sum = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { v[q] = hist[4 * lane + q]; sum += v[q]; }
-            int inc = sum;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int o = __shfl_up(inc, off, 64);
-                if (lane >= off) inc += o;
-            }
-            const unsigned long long hit = __ballot(inc >= kk);
-            const int first = __ffsll((long long)hit) - 1;
-            if (lane == first) {
-                int cum = inc - sum, b = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (cum + v[q] >= kk) { b = q; break; }
-                    cum += v[q];
-                }
-                s_sel[2 * (pass & 1)] = 4 * lane + b;
-                s_sel[2 * (pass & 1) + 1] = kk - cum;
-                s_sel[4 + (pass & 1)] = v[b];
-            }
-        } else {
-            int* other = s_hist + 256 * ((pass & 1) ^ 1);
-            for (int b = tid - 64; b < 256; b += kCesThreads - 64) other[b] = 0;
-        }
-        __syncthreads();
-        prefix |= (unsigned long long)s_sel[2 * (pass & 1)] << sh;
-        pmask |= 0xFFull << sh;
-        kk = s_sel[2 * (pass & 1) + 1];
-        eq_cnt = s_sel[4 + (pass & 1)];
-    }
-    const unsigned long long T = top < 0 ? kmin : prefix;
-    const int need_eq = kk;  // elites with key == T, lowest slots first
-    if (c.prof == 2) return;
-
-    // ---- ordered compaction of the elites (slot order) into s_key / s_idx — in place when
-    // the keys are in LDS: a chunk's keys are read before the scan's barrier and written to
-    // positions <= their own index — then a bitonic sort on (key, slot)
-    int eq_seen = 0, nsel = 0;
-#pragma unroll 1
-    for (int base = 0; base < nslots; base += kCesThreads) {
-        const int i = base + tid;
-        const unsigned long long key = i < nslots ? key_at(i) : kNoKey;
-        const bool ok = key != kNoKey;
-        int eq_tot = 0, eq_rank = 0;
-        if (need_eq < eq_cnt)  // uniform: only a tie at the threshold needs the slot order
-            eq_rank = eq_seen + block_scan_flag(ok && key == T, s_w, &eq_tot);
-        const bool sel = ok && (key < T || (key == T && eq_rank < need_eq));
-        int sel_tot;
-        const int pos = nsel + block_scan_flag(sel, s_w, &sel_tot);
-        if (sel) { s_key[pos] = key; s_idx[pos] = i; }
-        eq_seen += eq_tot;
-        nsel += sel_tot;
-    }
-    __syncthreads();
-    int P = 1;
-    while (P < k) P <<= 1;
-    for (int i = k + tid; i < P; i += kCesThreads) { s_key[i] = ~0ull; s_idx[i] = INT_MAX; }
-    __syncthreads();
-    for (int size = 2; size <= P; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = tid; t < (P >> 1); t += kCesThreads) {
-                const int lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
-                const bool up = (lo & size) == 0;
-                const unsigned long long ka = s_key[lo], kb = s_key[hi];
-                const int ia = s_idx[lo], ib = s_idx[hi];
-                const bool gt = ka > kb || (ka == kb && ia > ib);
-                if (gt == up) { s_key[lo] = kb; s_key[hi] = ka; s_idx[lo] = ib; s_idx[hi] = ia; }
-            }
-            // With stride <= 64 the pairs of wave w lie in entries [128 w, 128 w + 128) (t runs
-            // over 64 consecutive values, a multiple of stride), so consecutive stages that both
-            // have stride <= 64 touch wave-private data: a wave-level fence is enough.  After
-            // stride 1 the next stage starts a new size (stride = size): full barrier.
-            if (stride > 1 && stride <= 64) {
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-            } else {
-                __syncthreads();
-            }
-        }
-    }
+    if (tid == 0) *nsucc_p = 0;  // re-armed for the next update (every thread has read it)
 
     // ---- CES log weights (tsp_elites.h:24-32): w_j = log(k + 0.5) - log(j + 1), normalised.
     // Every sum below is the canonical 512-lane order of or_canon_sum(x, n, 512): thread t
     // accumulates j = t, t + 512, ... in order, xor butterfly per wave, waves in order.
-    if (c.prof == 3) return;
     const double lk = LH[k];
     double a = 0.0;
     for (int j = tid; j < k; j += kCesThreads) a = a + (lk - LT[j + 1]);
     const double sumw = block_sum(a, s_red);
-    double* s_wt = reinterpret_cast<double*>(s_key);
     for (int j = tid; j < k; j += kCesThreads) s_wt[j] = (lk - LT[j + 1]) / sumw;
     __syncthreads();
 
-    if (c.prof == 4) return;
     // ---- Distribution::update (tsp_distribution.h:52-83) + adapt(true), via by via: every
     // thread gathers its elites' 4 coordinates once per pass, all 512 lanes reduce
     const bool cache = k <= 2 * kCesThreads;  // each thread's <= 2 elites stay in registers
@@ -433,7 +288,7 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
         }
     }
 
-    // ---- best = first minimum in slot order (std::min_element): the sort's first entry
+    // ---- best = first minimum in slot order (std::min_element): rank 0
     const int b = s_idx[0];
     for (int e = tid; e < KD; e += kCesThreads) lbest[e] = vias[(long long)b * KD + e];
     for (int j = tid; j < k; j += kCesThreads) elite_out[j] = s_idx[j];
@@ -501,6 +356,9 @@ struct sspp_ces {
     double *d_L = nullptr, *d_Cnf = nullptr, *d_Cwf = nullptr, *d_cost = nullptr, *d_vias = nullptr;
     unsigned char* d_status = nullptr;
     int* d_elite = nullptr;
+    int* d_rank = nullptr;     // [n_slots] rank of each success in the (cost, slot) order
+    int* d_by_rank = nullptr;  // [n_slots] slot of rank r
+    int* d_nsucc = nullptr;
     double *d_LT = nullptr, *d_LH = nullptr;
 };
 
@@ -512,8 +370,6 @@ static CesK ces_k(const sspp_ces* p) {
     c.sd_min = p->cfg.stddev_min; c.sd_max = p->cfg.stddev_max;
     c.dist_z_min = p->cfg.dist_z_min; c.z_min = p->cfg.z_min;
     for (int i = 0; i < 4; ++i) { c.lo[i] = p->lo[i]; c.hi[i] = p->hi[i]; }
-    static const int prof = [] { const char* e = getenv("SSPP_CES_PROF"); return e ? atoi(e) : 0; }();
-    c.prof = prof;
     return c;
 }
 
@@ -525,7 +381,8 @@ void sspp_ces_free(sspp_ces* p) {
     for (void* q : {(void*)p->d_hdr, (void*)p->d_mean, (void*)p->d_sigma, (void*)p->d_lbest,
                     (void*)p->d_fixed, (void*)p->d_L, (void*)p->d_Cnf, (void*)p->d_Cwf,
                     (void*)p->d_cost, (void*)p->d_vias, (void*)p->d_status, (void*)p->d_elite,
-                    (void*)p->d_LT, (void*)p->d_LH})
+                    (void*)p->d_LT, (void*)p->d_LH, (void*)p->d_rank, (void*)p->d_by_rank,
+                    (void*)p->d_nsucc})
         if (q) (void)hipFree(q);
     delete p;
 }
@@ -579,6 +436,9 @@ int sspp_ces_create(const sspp_scene* scene, const sspp_ces_config* cfg, int wor
         (e = hipMalloc((void**)&p->d_vias, sizeof(double) * ns * kd)) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_status, ns)) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_elite, sizeof(int) * cap)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_rank, sizeof(int) * ns)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_by_rank, sizeof(int) * ns)) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_nsucc, sizeof(int))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_LT, sizeof(double) * LT.size())) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_LH, sizeof(double) * LH.size())) != hipSuccess ||
         (e = hipMemcpy(p->d_LT, LT.data(), sizeof(double) * LT.size(), hipMemcpyHostToDevice)) != hipSuccess ||
@@ -587,7 +447,9 @@ int sspp_ces_create(const sspp_scene* scene, const sspp_ces_config* cfg, int wor
         (e = hipMemset(p->d_lbest, 0, sizeof(double) * kd)) != hipSuccess ||
         (e = hipMemset(p->d_mean, 0, sizeof(double) * kd)) != hipSuccess ||
         (e = hipMemset(p->d_sigma, 0, sizeof(double) * kd)) != hipSuccess ||
-        (e = hipMemset(p->d_status, 0, ns)) != hipSuccess) {
+        (e = hipMemset(p->d_status, 0, ns)) != hipSuccess ||
+        (e = hipMemset(p->d_rank, 0, sizeof(int) * ns)) != hipSuccess ||
+        (e = hipMemset(p->d_nsucc, 0, sizeof(int))) != hipSuccess) {
         rc = hip_err(e, "sspp_ces_create allocation");
         sspp_ces_free(p);
         return rc;
@@ -657,8 +519,14 @@ int sspp_ces_eval(sspp_ces* p, int rank, void* stream) {
 int sspp_ces_update(sspp_ces* p, void* stream) {
     sspp::clear_error();
     if (!p) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_update: null planner");
-    hipLaunchKernelGGL(k_ces_update, dim3(1), dim3(kCesThreads), 0, (hipStream_t)stream, ces_k(p),
-                       p->d_cost, p->d_status, p->d_vias, p->d_LT, p->d_LH, p->d_hdr, p->d_mean,
+    const int nt = (p->nslots + kRankTile - 1) / kRankTile;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_ces_rank, dim3(nt, nt), dim3(kRankTile), 0, st, p->nslots, p->d_cost,
+                       p->d_status, p->d_rank, p->d_nsucc);
+    hipLaunchKernelGGL(k_ces_scatter, dim3(nt), dim3(256), 0, st, p->nslots, p->d_cost, p->d_status,
+                       p->d_rank, p->d_by_rank);
+    hipLaunchKernelGGL(k_ces_update, dim3(1), dim3(kCesThreads), 0, st, ces_k(p), p->d_cost,
+                       p->d_by_rank, p->d_nsucc, p->d_vias, p->d_LT, p->d_LH, p->d_hdr, p->d_mean,
                        p->d_sigma, p->d_lbest, p->d_elite);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "k_ces_update launch");

@@ -1,1 +1,4 @@
-for n in 1 2 3 4 0; do SSPP_CES_PROF=$n bash tools/gpu_trace.sh trp$n python3 $GRAFT_REPO_ROOT/tools/ces_timing.py 50 0 | grep k_ces_update | sed "s/^/prof $n 50: /"; SSPP_CES_PROF=$n bash tools/gpu_trace.sh trq$n python3 $GRAFT_REPO_ROOT/tools/ces_timing.py 4096 0 | grep k_ces_update | sed "s/^/prof $n 4096: /"; done
+# CES kernel durations (rocprofv3) at a few sizes: bash tools/gpu_cesprof.sh
+for n in "50 0" "4096 0" "16384 3"; do
+  bash tools/gpu_trace.sh trc python3 $GRAFT_REPO_ROOT/tools/ces_timing.py $n | grep k_ces | sed "s/^/[$n] /"
+done
