@@ -295,15 +295,26 @@ __device__ __forceinline__ void mover_poses(const double* q, cmover_t movers,
             for (int k = 0; k < 7; ++k)
                 qp[k] = (7 * m + k < D) ? q[(7 * m + k < D) ? 7 * m + k : 0] : (double)movers[m].qpos0[k];
         } else {
+#ifndef SSPP_YAW_GENERIC
+            // yaw_to_quat (utility.h:198-206): q = (cos h, 0, 0, sin h) — a rotation about z.
+            // normalize4 + quat2mat written out for x = y = +0: every entry equals the generic
+            // formula's (sums with exact zeros), except the sign of the four zero entries,
+            // which only ever enter products and sums with non-zero terms
+            const double half = q[3] * 0.5;
+            double w = cos(half), z = sin(half);
+            const double nn = sqrt(fma(z, z, w * w));
+            if (nn < kMinVal) { w = 1.0; z = 0.0; }
+            else if (fabs(nn - 1.0) > kMinVal) { const double inv = 1.0 / nn; w *= inv; z *= inv; }
+            const double q00 = w * w, q33 = z * z, q03 = w * z;
+            double* R = mR[m];
+            R[0] = q00 - q33; R[1] = 2.0 * (0.0 - q03); R[2] = 0.0;
+            R[3] = 2.0 * (0.0 + q03); R[4] = q00 - q33; R[5] = 0.0;
+            R[6] = 0.0; R[7] = 0.0; R[8] = q00 + q33;
+            mp[m][0] = q[0]; mp[m][1] = q[1]; mp[m][2] = q[2];
+            continue;
+#else
             double half = q[3] * 0.5;
             qp[0] = q[0]; qp[1] = q[1]; qp[2] = q[2];
-#ifdef SSPP_YAW_SINCOS
-            double sh, ch;
-            sincos(half, &sh, &ch);
-            qp[3] = ch; qp[4] = 0.0; qp[5] = 0.0; qp[6] = sh;
-#elif defined(SSPP_PROF_NOTRIG)  // profiling variant only: wrong poses, timing of the rest
-            qp[3] = 1.0 - half * half; qp[4] = 0.0; qp[5] = 0.0; qp[6] = half;
-#else
             qp[3] = cos(half); qp[4] = 0.0; qp[5] = 0.0; qp[6] = sin(half);
 #endif
         }
@@ -339,6 +350,26 @@ __device__ __forceinline__ void geom_rot(const double* R, const DGeom& G, double
     } else {
 #pragma unroll
         for (int k = 0; k < 9; ++k) gm[k] = R[k];
+    }
+}
+
+// Geom pose from a mover rotation about z (R[2] = R[5] = R[6] = R[7] = 0, MODE 1): the
+// generic dot products with those zero terms dropped (each dropped term adds an exact zero).
+template <bool ZR>
+__device__ __forceinline__ void geom_pos_t(const double* P, const double* R, const DGeom& G, double* gp) {
+    if (!ZR) { geom_pos(P, R, G, gp); return; }
+    gp[0] = P[0] + fma(R[1], G.pos[1], R[0] * G.pos[0]);
+    gp[1] = P[1] + fma(R[4], G.pos[1], R[3] * G.pos[0]);
+    gp[2] = P[2] + R[8] * G.pos[2];
+}
+template <bool ZR>
+__device__ __forceinline__ void geom_rot_t(const double* R, const DGeom& G, double* gm) {
+    if (!ZR || !G.relrot) { geom_rot(R, G, gm); return; }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        gm[j] = fma(R[1], G.mat[3 + j], R[0] * G.mat[j]);
+        gm[3 + j] = fma(R[4], G.mat[3 + j], R[3] * G.mat[j]);
+        gm[6 + j] = R[8] * G.mat[6 + j];
     }
 }
 
@@ -381,10 +412,12 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
     double gp[3], gmat[9];
     bool have_rot = true;  // multi-geom movers: a geom's rotation is formed at its first near pair
     DGeom G;
+    constexpr bool ZR = MODE == 1;  // yaw-only mover rotation
     if (ONEGEOM) {  // every pair shares one moving geom: pose once, mover pose dies here
         cur = pairs[0].gm;
         G = load_geom(geoms + cur);
-        geom_pose(mp[0], mR[0], G, gp, gmat);
+        geom_pos_t<ZR>(mp[0], mR[0], G, gp);
+        geom_rot_t<ZR>(mR[0], G, gmat);
     }
     const int np = sc.npairs;
     for (int k = 0; k < np; ++k) {
@@ -400,7 +433,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             cur = pr.gm;
             G = load_geom(geoms + cur);
             const bool second = NM > 1 && G.mover == 1;
-            geom_pos(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp);
+            geom_pos_t<ZR>(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp);
             have_rot = false;
         }
         double op_[3], om_[9];
@@ -421,7 +454,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
         if (near) {
             if (!ONEGEOM && !have_rot) {
                 const bool second = NM > 1 && G.mover == 1;
-                geom_rot(second ? mR[NM - 1] : mR[0], G, gmat);
+                geom_rot_t<ZR>(second ? mR[NM - 1] : mR[0], G, gmat);
                 have_rot = true;
             }
             const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
