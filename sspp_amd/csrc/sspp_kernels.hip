@@ -1330,12 +1330,21 @@ __global__ __launch_bounds__(kBlock, SSPP_TSP_WAVES_PER_EU) void k_tsp(
     const unsigned long long mask = hull_mask<D, NM, 1>(myc, n, a.sc.npairs, (cpair_t)T.pairs,
                                                         (cgeom_t)T.geoms, (cmover_t)T.movers);
     double aL = 0.0, aC = 0.0, aW = 0.0;
+    // cp <= lpc: one waypoint per lane, so s((i-1)du) is the previous lane's s(i du); take it
+    // by shuffle (bit-identical: same eval_pt inputs) except on a wave's first lane
+    const bool one_pass = cp <= lpc;
     if (valid) {
         for (int j = lane; j < cp; j += lpc) {
             const int i = j + 1;
             double pv[4], pc[4];
-            eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
             eval_pt<D, P>(myc, tab + i * P1, span[i], pc);
+            if (one_pass) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pc[d], 1, 64);
+                if ((tid & 63) == 0) eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
+            } else {
+                eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
+            }
             aL = aL + dist_nd<D>(pv, pc);
             double c = 0.0;
 #ifndef SSPP_PROF_NOCOLL  // profiling variant only
