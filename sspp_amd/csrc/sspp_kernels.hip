@@ -1171,13 +1171,17 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
                 }
             }
         } else {
-            // the few collision-free candidates: one chord per thread over the workgroup
+            // the few collision-free candidates: one chord per thread over the workgroup; a
+            // chord's first point is the previous lane's second point (same candidate when
+            // j > 0), taken by shuffle: bit-identical to evaluating it again
             for (int it = tid; it < nl * nch; it += NT) {
                 const int si = it / nch, j = it - si * nch, sl = s_list[si];
                 const double* myc = s_ctrl + sl * ndof;
                 double qa[D], qb[D];
-                eval_pt<D, P>(myc, atab + j * P1, aspan[j], qa);
                 eval_pt<D, P>(myc, atab + (j + 1) * P1, aspan[j + 1], qb);
+#pragma unroll
+                for (int d = 0; d < D; ++d) qa[d] = __shfl_up(qb[d], 1, 64);
+                if (j == 0 || (tid & 63) == 0) eval_pt<D, P>(myc, atab + j * P1, aspan[j], qa);
                 s_chord[sl * nch + j] = dist_nd<D>(qa, qb);
             }
         }
