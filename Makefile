@@ -32,7 +32,7 @@ $(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(OBJDIR)/sspp_kernels.o $(OBJDIR)/ces.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o
+$(LIB): $(OBJDIR)/sspp_kernels.o $(OBJDIR)/ces.o $(OBJDIR)/planner.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 

@@ -51,9 +51,11 @@ def parse():
     ap.add_argument("--roofline-launches", type=int, default=200)
     ap.add_argument("--streams", type=int, default=4,
                     help="independent batches in flight (one job + stream/graph branch each)")
-    ap.add_argument("--mode", default="native", choices=["native", "eager"],
+    ap.add_argument("--mode", default="native", choices=["native", "eager", "dropin"],
                     help="native: the C++ step executor enqueues --chunk steps per call "
-                         "(robocrane); eager: one Python-level launch per step")
+                         "(robocrane); eager: one Python-level launch per step; dropin: "
+                         "per-call latency of the reference's entry point "
+                         "_sspp.SamplingPathPlanner7.plan (src/sspp_bindings.cpp:43-50)")
     ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--steps-per-launch", type=int, default=8,
                     help="native mode: independent steps (each its own B candidates, outputs and "
@@ -213,8 +215,7 @@ def cpu_baseline(args, ctx, B, device):
     from oracle import mjcf_ref
     from oracle import oracle as O
     import sspp_amd as S
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
-        min(16, os.cpu_count() or 1)
+    threads = cpu_threads(args)
     model = mjcf_ref.load(ctx["scene_path"])
     if ctx["kind"] == "multigoal":
         return cpu_baseline_multigoal(args, ctx, model, threads)
@@ -257,17 +258,56 @@ def cpu_baseline(args, ctx, B, device):
                   max_abs_cost_diff=float(np.abs(arc_c[fin] - arc_g[fin]).max()) if fin.any() else 0.0,
                   feasible_identical=bool(np.array_equal(feas_c, feas_g)),
                   argmin_identical=bool(O.argmin(arc_c, feas_c)[0] == O.argmin(arc_g, feas_g)[0]))
-    # timed: successive batches (sampling included, as in the GPU step) for ~cpu_seconds
-    done, batch, t0 = 0, 0, time.perf_counter()
+    # timed: successive batches (sampling included, as in the GPU step) for ~cpu_seconds; the
+    # sampler (single-threaded oracle call) and the scorer (OpenMP over candidates) are timed
+    # separately as well, so their rates can be told apart
+    done, batch, t_smp, t_scr, t0 = 0, 0, 0.0, 0.0, time.perf_counter()
     while time.perf_counter() - t0 < args.cpu_seconds:
-        run_on(sample((batch + 1) * B, B))
+        ta = time.perf_counter()
+        c = sample((batch + 1) * B, B)
+        tb = time.perf_counter()
+        run_on(c)
+        t_smp += tb - ta
+        t_scr += time.perf_counter() - tb
         done += B
         batch += 1
     dt = time.perf_counter() - t0
     return dict(value=done / dt, unit="candidate paths scored/s", cores=threads, kind="port",
                 sample="%d candidates (%d batches of %d, sampling included) in %.1f s; "
                        "OpenMP schedule(dynamic,1) over candidates" % (done, batch, B, dt),
-                parity=parity)
+                scoring_only_value=done / t_scr, sampling_only_value=done / t_smp,
+                sampling_threads=1, **cpu_info(), parity=parity)
+
+
+def cpu_threads(args):
+    """Threads of the CPU baseline: --cpu-threads, else OMP_NUM_THREADS (the GPU box sets it to
+    its CPU share), else every CPU this process may run on."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env:
+        return env
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return dict(cpu_model=model, host_cpus=os.cpu_count(), affinity_cpus=aff,
+                omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
 
 
 def cpu_baseline_multigoal(args, ctx, model, threads):
@@ -300,11 +340,135 @@ def cpu_baseline_multigoal(args, ctx, model, threads):
     dt = time.perf_counter() - t0
     return dict(value=done / dt, unit="candidate paths scored/s (full CES iterations)", cores=threads,
                 kind="port", sample="%d CES iterations of goal 0 (%d candidates) in %.1f s" % (it, done, dt),
-                parity=parity)
+                **cpu_info(), parity=parity)
+
+
+def native_runner(args, ctx, B, world, rank, device, on_chunk=None):
+    """The timed loop's step protocol (robocrane).  The C++ step executor enqueues G steps per
+    call, round robin over --streams streams (one job each): step t scores global ids
+    (t * world + rank) * B + [0, B), so the candidate set does not depend on the rank count.
+    With several ranks each chunk's G per-step argmin records (32 B each) go through ONE
+    all-gather on the main stream and are reduced per step on the device (lowest cost, lowest
+    id).  on_chunk(records) receives each chunk's per-step global records (tests)."""
+    import torch
+    import sspp_amd as S
+    ns = args.streams
+    G = max(1, args.chunk)
+    main = torch.cuda.current_stream()
+    streams = [main] + [torch.cuda.Stream(device) for _ in range(ns - 1)]
+    ex = ctx["make_executor"](streams, args.steps_per_launch)
+    best = torch.zeros((G, 4), dtype=torch.int64, device=device)
+    gbufs = {}
+    counter = [0]
+
+    def gbuf(g):
+        if g not in gbufs:
+            gbufs[g] = (torch.zeros((world, g, 4), dtype=torch.int64, device=device),
+                        torch.zeros((g, 4), dtype=torch.int64, device=device))
+        return gbufs[g]
+
+    # prime every branch before warmup: one launch per stream, so no stream sees its first
+    # work inside the timed region (ids past any timed step's; results discarded)
+    ex.enqueue(ns * args.steps_per_launch, 1 << 40, world * B, None)
+    torch.cuda.synchronize()
+
+    def run_steps(k):
+        while k > 0:
+            g = min(G, k)
+            if world > 1:
+                for st in streams[1:]:
+                    st.wait_stream(main)
+            ex.enqueue(g, (counter[0] * world + rank) * B, world * B, best[:g])
+            rec = best[:g]
+            if world > 1:
+                for st in streams[1:]:
+                    main.wait_stream(st)
+                gat, gout = gbuf(g)
+                S.all_gather_records(gat, best[:g])
+                S.reduce_best_steps(gat, gout)
+                rec = gout
+            if on_chunk is not None:
+                on_chunk(rec)
+            counter[0] += g
+            k -= g
+    return run_steps
+
+
+def run_dropin(args):
+    """Latency of the drop-in entry point, SamplingPathPlanner7.plan(start, end, sigma, limits,
+    sample_count, check_points, init_points) on the robocrane workload (BASELINE configs[1]):
+    host call -> initializePath -> device sampling + scoring + argmin -> compaction of the
+    feasible candidates into pinned memory -> Python list of Spline7.  Inputs are host arrays,
+    as the reference's callers pass them."""
+    import torch
+    from sspp import _sspp
+    import sspp_amd as S
+    planner = _sspp.SamplingPathPlanner7(os.path.join(S.SCENE_DIR, "robocrane.xml"))
+    start = np.array([0.5, 0.15, 0.136, 0.707, 0.0, 0.0, 0.707])
+    end = np.array([0.5, -0.05, 0.136, 0.707, 0.0, 0.0, 0.707])
+    B, W, n = args.batch or 4096, args.waypoints, 10
+    limits = np.ones(7)
+    # plan() prints one line per call (include/sspp.h:221): keep it off the JSON line's stdout
+    sys.stdout.flush()
+    saved = os.dup(1)
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(devnull, 1)
+    try:
+        for _ in range(args.warmup):
+            planner.plan(start, end, 0.08, limits, B, W, n)
+        lat, nfeas = [], []
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ta = time.perf_counter()
+            ok, paths = planner.plan(start, end, 0.08, limits, B, W, n)
+            lat.append(time.perf_counter() - ta)
+            nfeas.append(len(paths))
+        total = time.perf_counter() - t0
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(devnull)
+    # one executor step of the same shape for comparison: a single 4096-candidate launch on an
+    # idle stream (isolated: no overlap with other steps), HIP events
+    model = S.Model(os.path.join(S.SCENE_DIR, "robocrane.xml"))
+    u = np.array([i / (n - 1) for i in range(n)])
+    knots, ctrl0 = S.interpolate(np.array([(1 - t) * start + t * end for t in u]), 3, u)
+    job = S.SsppJob(S.Scene(model, 0, 7), knots, 3, ctrl0, 0.08, limits, W, max_batch=B)
+    out = job.alloc(B, device="cuda")
+    for i in range(20):
+        job.sample_score(i * B, B, out["arc"], out["feasible"], out["best"])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ks = []
+    for i in range(50):
+        e0.record()
+        job.sample_score((100 + i) * B, B, out["arc"], out["feasible"], out["best"])
+        e1.record()
+        torch.cuda.synchronize()
+        ks.append(e0.elapsed_time(e1) * 1e3)
+    lat_us = np.array(lat) * 1e6
+    line = {
+        "metric": "drop-in SamplingPathPlanner7.plan per-call latency (robocrane, 4096 x 128)",
+        "value": float(np.median(lat_us)), "unit": "us/plan (median)", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "higher_is_better": False,
+        "candidates_per_s": B * args.steps / total,
+        "latency_us": {"median": float(np.median(lat_us)), "p10": float(np.percentile(lat_us, 10)),
+                       "p90": float(np.percentile(lat_us, 90)), "mean": float(lat_us.mean())},
+        "feasible_per_plan": float(np.mean(nfeas)),
+        "isolated_step_kernel_us": float(np.median(ks)),
+        "dtype": "f64", "data": "synthetic (on-device Philox candidates around a linear init spline)",
+        "config": {"workload": "robocrane SamplingPathPlanner7.plan(start, end, 0.08, ones(7), %d, %d, %d)"
+                               % (B, W, n), "call": "_sspp (pybind11) -> sspp_planner_plan (C ABI)"},
+    }
+    print(json.dumps(line))
 
 
 def main():
     args = parse()
+    if args.mode == "dropin":
+        run_dropin(args)
+        return
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -327,39 +491,7 @@ def main():
     if "run_steps" in ctx:
         run_steps = ctx["run_steps"]
     elif native:
-        # The C++ step executor enqueues G steps per call, round robin over ns streams (one job
-        # each): step t scores global ids (t * world + rank) * B + [0, B), so the candidate set
-        # does not depend on the rank count.  With several ranks each chunk's G per-step argmin
-        # records go through ONE all-gather (bucketed) and are reduced per step on the device.
-        G = max(1, args.chunk)
-        main = torch.cuda.current_stream()
-        streams = [main] + [torch.cuda.Stream(device) for _ in range(ns - 1)]
-        ex = ctx["make_executor"](streams, args.steps_per_launch)
-        best = torch.zeros((G, 4), dtype=torch.int64, device=device)
-        gbufs = {}
-        counter = [0]
-
-        def gbuf(g):
-            if g not in gbufs:
-                gbufs[g] = (torch.zeros((world, g, 4), dtype=torch.int64, device=device),
-                            torch.zeros((g, 4), dtype=torch.int64, device=device))
-            return gbufs[g]
-
-        def run_steps(k):
-            while k > 0:
-                g = min(G, k)
-                if world > 1:
-                    for st in streams[1:]:
-                        st.wait_stream(main)
-                ex.enqueue(g, (counter[0] * world + rank) * B, world * B, best[:g])
-                if world > 1:
-                    for st in streams[1:]:
-                        main.wait_stream(st)
-                    gat, gout = gbuf(g)
-                    dist.all_gather_into_tensor(gat, best[:g])
-                    S.reduce_best_steps(gat, gout)
-                counter[0] += g
-                k -= g
+        run_steps = native_runner(args, ctx, B, world, rank, device)
     else:
         streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device) for _ in range(ns - 1)]
         gathered = [torch.zeros((world, 4), dtype=torch.int64, device=device) for _ in range(ns)]
@@ -375,7 +507,7 @@ def main():
             with torch.cuda.stream(streams[lane]):
                 step(first, local_best[lane], lane, streams[lane])
                 if world > 1:
-                    dist.all_gather_into_tensor(gathered[lane], local_best[lane])
+                    S.all_gather_records(gathered[lane], local_best[lane])
                     S.reduce_best_device(gathered[lane], gbest[lane], stream=streams[lane])
 
         def run_steps(k):
@@ -425,8 +557,10 @@ def main():
 
     if rank == 0:
         total = args.steps * B * world
-        if ctx["kind"] == "multigoal":  # every goal's list, whatever the rank count
-            total = args.steps * (ctx["samples"] + 2) * len(MULTIGOAL)
+        if ctx["kind"] == "multigoal":
+            # every goal's mean set + samples, whatever the rank count; the forwarded best
+            # (and, before the first success, the padding slot in its place) is not counted
+            total = args.steps * (ctx["samples"] + 1) * len(MULTIGOAL)
         value = total / elapsed
         exec_per, exec_src, ach_exec = None, None, None
         ff = os.path.join(ROOT, "profiles", "fp64_latest.json")

@@ -262,12 +262,42 @@ int sspp_ces_set_state(sspp_ces* ces, const double* mean, const double* sigma,
                        const double* last_best, int has_best /* -1 = keep */);
 void sspp_ces_free(sspp_ces* ces);
 
+/* Re-target a SamplingPathPlanner job (same knots, dof, check_points) to new initial control
+ * points / sigma / limits / seed: asynchronous uploads on `stream` (the job keeps the host
+ * staging alive until its next update).  Used by the cached drop-in planner below.         */
+int sspp_job_update_sspp(sspp_job* job, const double* init_ctrl /* [n][D] */, double sigma,
+                         const double* limits /* [D] */, uint64_t seed, void* stream);
+
+/* ---- drop-in planner: SamplingPathPlanner<N> state kept on the device across calls ----
+ * One object per `_sspp.SamplingPathPlannerN` (src/sspp_bindings.cpp:24-50): it owns a HIP
+ * stream, the job of the last plan() shape (init_points, check_points, capacity) and the
+ * device / pinned buffers, so a plan() call is: initializePath on the host, an asynchronous
+ * job update, one scoring launch, one compaction launch that writes the feasible candidates
+ * (ids, arc lengths, control points — in candidate order) straight into pinned host memory,
+ * and one stream synchronisation.  Not re-entrant per object (as the reference's planner).
+ *   sspp_planner_plan  <- SamplingPathPlanner::plan (include/sspp.h:194-225): writes
+ *     knots [init_points+4], *n_feasible, feasible ids / arc / ctrl [n_feasible][n][D]
+ *     (caller buffers sized for sample_count) and the argmin record.
+ *   sspp_planner_score <- checkCollision / computeArcLength / findBestPath on host splines
+ *     sharing one knot vector (include/sspp.h:132-192); with_collision = 0: arc length only. */
+typedef struct sspp_planner sspp_planner;
+int sspp_planner_create(const sspp_scene* scene, int dof, sspp_planner** out);
+int sspp_planner_plan(sspp_planner* p, const double* start, const double* end, double sigma,
+                      const double* limits, int sample_count, int check_points, int init_points,
+                      uint64_t seed, int64_t first_id, double* knots_out, int64_t* n_feasible,
+                      int64_t* feasible_ids, double* feasible_arc, double* feasible_ctrl,
+                      sspp_best* best_out);
+int sspp_planner_score(sspp_planner* p, const double* knots, int degree,
+                       const double* ctrl /* [B][n][D] */, int64_t B, int n, int W, int with_collision,
+                       double* arc_out, uint8_t* feasible_out, sspp_best* best_out);
+void sspp_planner_free(sspp_planner* p);
+
 /* ---- step executor: a planning loop's back-to-back batches in one call ----
  * Enqueues nsteps independent SamplingPathPlanner steps (each = one plan() batch of B
  * candidates: sampleWithNoise + checkCollision + computeArcLength + findBestPath,
  * include/sspp.h:194-225).  Step i scores candidate ids [first_id + i * step_stride, ... + B)
  * and writes its own argmin record to d_best[i] (nullable).  Steps are grouped
- * steps_per_launch (1..16) to a kernel launch — each step keeps its own workgroups, outputs and
+ * steps_per_launch (1..64) to a kernel launch — each step keeps its own workgroups, outputs and
  * argmin — and launch l goes to branch l % nbranch: jobs[b] (distinct jobs: each owns its argmin
  * counters), streams[b], scratch outputs d_arc[b] / d_feasible[b] of steps_per_launch * B
  * entries.  Asynchronous.                                                                  */

@@ -129,6 +129,13 @@ SIGNATURES = {
                                        C.POINTER(C.c_uint8), C.POINTER(Best)]),
     "sspp_sample_ctrl_host": (C.c_int, [_d, _i, _d, _i, _i, C.c_double, _d, C.c_uint64, _i64,
                                         _i64, _d]),
+    "sspp_job_update_sspp": (C.c_int, [_vp, _d, C.c_double, _d, C.c_uint64, _vp]),
+    "sspp_planner_create": (C.c_int, [_vp, _i, C.POINTER(_vp)]),
+    "sspp_planner_plan": (C.c_int, [_vp, _d, _d, C.c_double, _d, _i, _i, _i, C.c_uint64, _i64, _d,
+                                    C.POINTER(_i64), C.POINTER(_i64), _d, _d, C.POINTER(Best)]),
+    "sspp_planner_score": (C.c_int, [_vp, _d, _i, _d, _i64, _i, _i, _i, _d, C.POINTER(C.c_uint8),
+                                     C.POINTER(Best)]),
+    "sspp_planner_free": (None, [_vp]),
     "sspp_ces_create": (C.c_int, [_vp, C.POINTER(CesConfig), _i, C.POINTER(_vp)]),
     "sspp_ces_get_info": (C.c_int, [_vp, C.POINTER(CesInfo)]),
     "sspp_ces_begin": (C.c_int, [_vp, _d, _d, _i, _vp]),

@@ -209,7 +209,8 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
         if (tid == 0) { h->nsucc = 0; h->nelite = 0; h->best_slot = -1; h->best_cost = INFINITY; h->iter++; }
         return;
     }
-    const int k = (int)((double)nsucc * c.frac) < 1 ? 1 : (int)((double)nsucc * c.frac);
+    int k = (int)((double)nsucc * c.frac) < 1 ? 1 : (int)((double)nsucc * c.frac);
+    if (k > nsucc) k = nsucc;  // frac <= 1 is enforced at creation; never read past the ranks
     for (int j = tid; j < k; j += kCesThreads) s_idx[j] = by_rank[j];
     __syncthreads();
     if (tid == 0) *nsucc_p = 0;  // re-armed for the next update (every thread has read it)
@@ -396,7 +397,10 @@ int sspp_ces_create(const sspp_scene* scene, const sspp_ces_config* cfg, int wor
         return sspp::set_error(SSPP_E_INVAL, "total_points must be in [3, 34] (1..32 via points)");
     if (cfg->samples < 0 || cfg->checks < 1) return sspp::set_error(SSPP_E_INVAL, "samples >= 0, checks >= 1");
     if (world < 1) return sspp::set_error(SSPP_E_INVAL, "world must be >= 1");
-    if (!(cfg->elite_fraction >= 0.0)) return sspp::set_error(SSPP_E_INVAL, "elite_fraction must be >= 0");
+    // tsp_elites.h:15-19 partial_sorts the first max(1, int(n * frac)) of n candidates: frac > 1
+    // would sort past the end (undefined behaviour in the reference), so it is rejected here
+    if (!(cfg->elite_fraction >= 0.0 && cfg->elite_fraction <= 1.0))
+        return sspp::set_error(SSPP_E_INVAL, "elite_fraction must be in [0, 1]");
     const long long maxslots = (long long)cfg->samples + 2;
     long long cap = (long long)((double)maxslots * cfg->elite_fraction);
     if (cap < 1) cap = 1;
@@ -449,6 +453,7 @@ int sspp_ces_create(const sspp_scene* scene, const sspp_ces_config* cfg, int wor
         (e = hipMemset(p->d_sigma, 0, sizeof(double) * kd)) != hipSuccess ||
         (e = hipMemset(p->d_status, 0, ns)) != hipSuccess ||
         (e = hipMemset(p->d_rank, 0, sizeof(int) * ns)) != hipSuccess ||
+        (e = hipMemset(p->d_by_rank, 0, sizeof(int) * ns)) != hipSuccess ||
         (e = hipMemset(p->d_nsucc, 0, sizeof(int))) != hipSuccess) {
         rc = hip_err(e, "sspp_ces_create allocation");
         sspp_ces_free(p);

@@ -1,0 +1,285 @@
+// planner.hip — the cached drop-in SamplingPathPlanner behind `_sspp.SamplingPathPlannerN`.
+//
+// Reference: the planner object of include/sspp.h:20-245, bound at src/sspp_bindings.cpp:24-50.
+// The reference keeps its MuJoCo model and one mjData per OpenMP thread for the planner's
+// lifetime (initializeDataCopies, include/sspp.h:235-244); here the planner keeps, per object:
+// a HIP stream, the job of the last plan() shape (its basis tables, pair table and argmin
+// counters stay on the device), the candidate buffers, and pinned host memory that the
+// compaction kernel writes the feasible candidates into.  A plan() call is therefore
+//   initializePath (host, µs) -> sspp_job_update_sspp (3 small async copies)
+//   -> k_sspp_c2f (sample + score + fused argmin) -> k_compact_feasible -> stream sync
+// with no allocation, no device-wide synchronisation and no copy of infeasible candidates
+// (plan() returns only the feasible splines, include/sspp.h:215-216).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "model.h"
+
+namespace {
+
+constexpr int kCompactThreads = 1024;
+
+// Pinned-memory header the compaction kernel fills (host reads it after the stream sync).
+struct CompactHdr {
+    long long count;
+    long long pad;
+    sspp_best best;
+};
+
+// Stable compaction of the feasible candidates in candidate order (findBestPath's input,
+// include/sspp.h:215-216): one workgroup walks the batch in chunks of 1024; a chunk's
+// positions come from wave ballots + per-wave prefix counts in LDS; the feasible rows are then
+// copied cooperatively.  Outputs go to pinned host memory (written once, read after the sync).
+__global__ __launch_bounds__(kCompactThreads) void k_compact_feasible(
+    const unsigned char* __restrict__ feas, const double* __restrict__ arc,
+    const double* __restrict__ ctrl, long long B, int nd, const sspp_best* __restrict__ best,
+    CompactHdr* hdr, long long* ids, double* arc_out, double* ctrl_out) {
+    __shared__ int s_wave[kCompactThreads / 64 + 1];
+    __shared__ int s_pos[kCompactThreads];
+    __shared__ long long s_base;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    for (long long c0 = 0; c0 < B; c0 += kCompactThreads) {
+        const long long i = c0 + tid;
+        const bool f = i < B && feas[i] != 0;
+        const unsigned long long m = __ballot(f);
+        if (lane == 0) s_wave[w] = __popcll(m);
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int k = 0; k < kCompactThreads / 64; ++k) { const int t = s_wave[k]; s_wave[k] = acc; acc += t; }
+            s_wave[kCompactThreads / 64] = acc;
+        }
+        __syncthreads();
+        const int nf = s_wave[kCompactThreads / 64];
+        const long long base = s_base;
+        if (f) {
+            const int pos = s_wave[w] + __popcll(m & ((1ull << lane) - 1ull));
+            s_pos[pos] = tid;
+            ids[base + pos] = i;
+            arc_out[base + pos] = arc[i];
+        }
+        __syncthreads();
+        for (long long e = tid; e < (long long)nf * nd; e += kCompactThreads) {
+            const int r = (int)(e / nd), k = (int)(e - (long long)r * nd);
+            ctrl_out[(base + r) * nd + k] = ctrl[(c0 + s_pos[r]) * nd + k];
+        }
+        __syncthreads();
+        if (tid == 0) s_base = base + nf;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        hdr->count = s_base;
+        hdr->best = *best;
+    }
+}
+
+int hipck(hipError_t e, const char* what) {
+    if (e == hipSuccess) return SSPP_OK;
+    return sspp::set_error(SSPP_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+struct Dev {
+    T* p = nullptr;
+    size_t n = 0;
+    ~Dev() { if (p) (void)hipFree(p); }
+    int reserve(size_t count) {
+        if (count <= n) return SSPP_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr; n = 0;
+        hipError_t e = hipMalloc((void**)&p, sizeof(T) * (count ? count : 1));
+        if (e != hipSuccess) return sspp::set_error(SSPP_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        n = count;
+        return SSPP_OK;
+    }
+};
+
+template <class T>
+struct Pinned {
+    T* p = nullptr;
+    size_t n = 0;
+    ~Pinned() { if (p) (void)hipHostFree(p); }
+    int reserve(size_t count) {
+        if (count <= n) return SSPP_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr; n = 0;
+        hipError_t e = hipHostMalloc((void**)&p, sizeof(T) * (count ? count : 1),
+                                     hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return sspp::set_error(SSPP_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        n = count;
+        return SSPP_OK;
+    }
+    T* dev() const {
+        void* d = nullptr;
+        return hipHostGetDevicePointer(&d, p, 0) == hipSuccess ? (T*)d : nullptr;
+    }
+};
+
+struct JobRef {
+    sspp_job* j = nullptr;
+    ~JobRef() { reset(); }
+    void reset() { if (j) sspp_job_free(j); j = nullptr; }
+};
+
+}  // namespace
+
+struct sspp_planner {
+    const sspp_scene* scene = nullptr;
+    int D = 0;
+    hipStream_t stream = nullptr;
+    // plan(): job of the last shape
+    JobRef plan_job;
+    int plan_n = 0, plan_W = 0;
+    int64_t plan_cap = 0;
+    Dev<double> d_arc, d_ctrl;
+    Dev<unsigned char> d_feas;
+    Dev<sspp_best> d_best;
+    Pinned<CompactHdr> h_hdr;
+    Pinned<long long> h_ids;
+    Pinned<double> h_arc, h_ctrl;
+    // score(): job keyed on (knots, n, W, collision)
+    JobRef score_job;
+    std::vector<double> score_knots;
+    int score_W = 0, score_coll = -1;
+    int64_t score_cap = 0;
+    Pinned<double> h_in;
+    Pinned<double> h_sarc;
+    Pinned<unsigned char> h_sfeas;
+    Pinned<sspp_best> h_sbest;
+    Dev<double> d_in;
+    ~sspp_planner() {
+        plan_job.reset();
+        score_job.reset();
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+extern "C" int sspp_planner_create(const sspp_scene* scene, int dof, sspp_planner** out) {
+    sspp::clear_error();
+    if (!out || dof < 1 || dof > 16) return sspp::set_error(SSPP_E_INVAL, "sspp_planner_create: bad argument");
+    auto* p = new sspp_planner();
+    p->scene = scene;
+    p->D = dof;
+    hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete p;
+        return hipck(e, "hipStreamCreate");
+    }
+    *out = p;
+    return SSPP_OK;
+}
+
+extern "C" void sspp_planner_free(sspp_planner* p) { delete p; }
+
+extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const double* end, double sigma,
+                                 const double* limits, int sample_count, int check_points,
+                                 int init_points, uint64_t seed, int64_t first_id, double* knots_out,
+                                 int64_t* n_feasible, int64_t* feasible_ids, double* feasible_arc,
+                                 double* feasible_ctrl, sspp_best* best_out) {
+    sspp::clear_error();
+    if (!p || !start || !end || !limits || !knots_out || !n_feasible || !best_out)
+        return sspp::set_error(SSPP_E_INVAL, "sspp_planner_plan: null argument");
+    const int n = init_points, D = p->D, deg = 3;
+    if (sample_count < 1) return sspp::set_error(SSPP_E_INVAL, "sample_count must be >= 1");
+    if (n < deg + 1) return sspp::set_error(SSPP_E_INVAL, "init_points must be >= 4 for a cubic spline");
+    if (check_points < 2) return sspp::set_error(SSPP_E_INVAL, "check_points must be >= 2");
+    // initializePath (include/sspp.h:82-97): linear via points at t_i = i / (n - 1)
+    std::vector<double> u((size_t)n), pts((size_t)n * D), ctrl0((size_t)n * D);
+    for (int i = 0; i < n; ++i) {
+        const double t = (double)i / (n - 1);
+        u[i] = t;
+        for (int d = 0; d < D; ++d) pts[(size_t)i * D + d] = (1 - t) * start[d] + t * end[d];
+    }
+    if (sspp::interpolate(pts.data(), n, D, deg, u.data(), knots_out, ctrl0.data()) != 0)
+        return sspp::set_error(SSPP_E_INVAL, "initializePath: interpolation failed");
+    int rc;
+    const size_t nd = (size_t)n * D;
+    const int64_t B = sample_count;
+    if (!p->plan_job.j || p->plan_n != n || p->plan_W != check_points || B > p->plan_cap) {
+        p->plan_job.reset();
+        sspp_sspp_args a{};
+        a.knots = knots_out; a.degree = deg; a.init_ctrl = ctrl0.data(); a.n_ctrl = n; a.dof = D;
+        a.sigma = sigma; a.limits = limits; a.check_points = check_points; a.seed = seed;
+        if ((rc = sspp_job_create_sspp(p->scene, &a, B, &p->plan_job.j))) return rc;
+        p->plan_n = n; p->plan_W = check_points; p->plan_cap = B;
+        if ((rc = p->d_arc.reserve(B)) || (rc = p->d_feas.reserve(B)) || (rc = p->d_best.reserve(1)) ||
+            (rc = p->d_ctrl.reserve(B * nd)) || (rc = p->h_hdr.reserve(1)) || (rc = p->h_ids.reserve(B)) ||
+            (rc = p->h_arc.reserve(B)) || (rc = p->h_ctrl.reserve(B * nd))) {
+            p->plan_job.reset();
+            return rc;
+        }
+    } else if ((rc = sspp_job_update_sspp(p->plan_job.j, ctrl0.data(), sigma, limits, seed, p->stream))) {
+        return rc;
+    }
+    if ((rc = sspp_job_sample_score(p->plan_job.j, first_id, B, p->d_arc.p, p->d_feas.p, p->d_ctrl.p,
+                                    p->d_best.p, p->stream)))
+        return rc;
+    CompactHdr* hh = p->h_hdr.dev();
+    long long* hi = p->h_ids.dev();
+    double* ha = p->h_arc.dev();
+    double* hc = p->h_ctrl.dev();
+    if (!hh || !hi || !ha || !hc) return sspp::set_error(SSPP_E_HIP, "hipHostGetDevicePointer failed");
+    hipLaunchKernelGGL(k_compact_feasible, dim3(1), dim3(kCompactThreads), 0, p->stream, p->d_feas.p,
+                       p->d_arc.p, p->d_ctrl.p, (long long)B, (int)nd, p->d_best.p, hh, hi, ha, hc);
+    if ((rc = hipck(hipGetLastError(), "k_compact_feasible launch"))) return rc;
+    if ((rc = hipck(hipStreamSynchronize(p->stream), "plan"))) return rc;
+    const long long cnt = p->h_hdr.p->count;
+    *n_feasible = cnt;
+    *best_out = p->h_hdr.p->best;
+    if (feasible_ids) std::memcpy(feasible_ids, p->h_ids.p, sizeof(long long) * cnt);
+    if (feasible_arc) std::memcpy(feasible_arc, p->h_arc.p, sizeof(double) * cnt);
+    if (feasible_ctrl) std::memcpy(feasible_ctrl, p->h_ctrl.p, sizeof(double) * cnt * nd);
+    return SSPP_OK;
+}
+
+extern "C" int sspp_planner_score(sspp_planner* p, const double* knots, int degree, const double* ctrl,
+                                  int64_t B, int n, int W, int with_collision, double* arc_out,
+                                  uint8_t* feasible_out, sspp_best* best_out) {
+    sspp::clear_error();
+    if (!p || !knots || !ctrl || B < 1 || n < degree + 1) return sspp::set_error(SSPP_E_INVAL, "sspp_planner_score: bad argument");
+    const int D = p->D;
+    const size_t nd = (size_t)n * D;
+    const int nk = n + degree + 1;
+    const int coll = with_collision && p->scene ? 1 : 0;
+    int rc;
+    const bool same = p->score_job.j && p->score_W == W && p->score_coll == coll && B <= p->score_cap &&
+                      (int)p->score_knots.size() == nk &&
+                      std::memcmp(p->score_knots.data(), knots, sizeof(double) * nk) == 0;
+    if (!same) {
+        p->score_job.reset();
+        std::vector<double> ones((size_t)D, 1.0);
+        sspp_sspp_args a{};
+        a.knots = knots; a.degree = degree; a.init_ctrl = ctrl; a.n_ctrl = n; a.dof = D;
+        a.sigma = 0.0; a.limits = ones.data(); a.check_points = W; a.seed = 0;
+        if ((rc = sspp_job_create_sspp(coll ? p->scene : nullptr, &a, B, &p->score_job.j))) return rc;
+        p->score_knots.assign(knots, knots + nk);
+        p->score_W = W; p->score_coll = coll; p->score_cap = B;
+        if ((rc = p->d_in.reserve(B * nd)) || (rc = p->h_in.reserve(B * nd)) || (rc = p->h_sarc.reserve(B)) ||
+            (rc = p->h_sfeas.reserve(B)) || (rc = p->h_sbest.reserve(1)) || (rc = p->d_arc.reserve(B)) ||
+            (rc = p->d_feas.reserve(B)) || (rc = p->d_best.reserve(1))) {
+            p->score_job.reset();
+            return rc;
+        }
+    }
+    std::memcpy(p->h_in.p, ctrl, sizeof(double) * B * nd);
+    if ((rc = hipck(hipMemcpyAsync(p->d_in.p, p->h_in.p, sizeof(double) * B * nd, hipMemcpyHostToDevice,
+                                   p->stream), "copy splines")))
+        return rc;
+    if ((rc = sspp_job_score_ctrl(p->score_job.j, p->d_in.p, 0, B, p->d_arc.p, p->d_feas.p, p->d_best.p,
+                                  p->stream)))
+        return rc;
+    if ((rc = hipck(hipMemcpyAsync(p->h_sarc.p, p->d_arc.p, sizeof(double) * B, hipMemcpyDeviceToHost, p->stream), "copy arc")) ||
+        (rc = hipck(hipMemcpyAsync(p->h_sfeas.p, p->d_feas.p, (size_t)B, hipMemcpyDeviceToHost, p->stream), "copy feasible")) ||
+        (rc = hipck(hipMemcpyAsync(p->h_sbest.p, p->d_best.p, sizeof(sspp_best), hipMemcpyDeviceToHost, p->stream), "copy best")) ||
+        (rc = hipck(hipStreamSynchronize(p->stream), "score")))
+        return rc;
+    if (arc_out) std::memcpy(arc_out, p->h_sarc.p, sizeof(double) * B);
+    if (feasible_out) std::memcpy(feasible_out, p->h_sfeas.p, (size_t)B);
+    if (best_out) *best_out = *p->h_sbest.p;
+    return SSPP_OK;
+}

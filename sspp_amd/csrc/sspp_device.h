@@ -146,6 +146,10 @@ SSPP_HD void basis_funcs(double u, int p, int span, const double* knots, double*
     }
 }
 
+// rare, register-hungry narrowphase paths stay out of line so they do not raise the VGPR
+// count (and so lower the occupancy) of the kernels' hot pair loops
+#define SSPP_HDNI __host__ __device__ inline __attribute__((noinline))
+
 // ---------------------------------------------------------------- narrowphase
 // Each returns the contact count (dist < margin); *nd = contacts with dist < -1e-3.
 SSPP_HD int col_plane_box(const double* pp, const double* pm, const double* bp, const double* bm,
@@ -298,37 +302,382 @@ SSPP_HD bool sat_box_box(const double* pa, const double* ma, const double* ea, c
     return true;
 }
 
-// cylinder (A) vs box (B) over the 7 finite axes {box faces, cylinder axis, axis x box edges}.
-SSPP_HD bool sat_cyl_box(const double* pa, const double* ma, const double* sz, const double* pb,
-                         const double* mb, const double* eb, double thr) {
-    double a[3], Bc[3][3];
-    col3(ma, 2, a);
+// Box-box contact manifold (TaskSpacePlanner cost, Collision.h:89-101 adds one term per
+// contact; MuJoCo's box-box collider reports up to 8).  Restated MuJoCo-style:
+// the SAT axis of least penetration decides; an edge-edge axis (separation above every face
+// axis by more than 1e-12) gives one contact; a face axis makes that face the reference face
+// and the most anti-parallel face of the other box the incident face, which is clipped against
+// the reference face's four side planes (Sutherland-Hodgman, <= 8 points): one contact per
+// clipped point, dist = -(depth below the reference face).  Returns the contacts with
+// dist < -1e-3, at least 1: it is called only when the SAT depth exceeds 1e-3, and no clipped
+// point is deeper than the SAT depth along the reference normal.
+SSPP_HDNI int box_box_deep_count(const double* pa, const double* ma, const double* ea,
+                                                const double* pb, const double* mb, const double* eb) {
+    double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
+    for (int j = 0; j < 3; ++j) { col3(ma, j, A[j]); col3(mb, j, Bc[j]); }
+    T[0] = pb[0] - pa[0]; T[1] = pb[1] - pa[1]; T[2] = pb[2] - pa[2];
+    for (int i = 0; i < 3; ++i) {
+        t[i] = dot3(A[i], T);
+        for (int j = 0; j < 3; ++j) { R[i][j] = dot3(A[i], Bc[j]); AR[i][j] = fabs(R[i][j]); }
+    }
+    double best_face = -1e300, best_edge = -1e300;
+    int fi = 0;
+    for (int i = 0; i < 3; ++i) {  // faces of A
+        const double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
+        const double sep = fabs(t[i]) - (ea[i] + rb);
+        if (sep > best_face) { best_face = sep; fi = i; }
+    }
+    for (int j = 0; j < 3; ++j) {  // faces of B
+        const double pr = fabs(fma(t[2], R[2][j], fma(t[1], R[1][j], t[0] * R[0][j])));
+        const double ra = fma(ea[2], AR[2][j], fma(ea[1], AR[1][j], ea[0] * AR[0][j]));
+        const double sep = pr - (ra + eb[j]);
+        if (sep > best_face) { best_face = sep; fi = 3 + j; }
+    }
+    for (int i = 0; i < 3; ++i) {  // edge x edge
+        for (int j = 0; j < 3; ++j) {
+            const double v0 = R[0][j], v1 = R[1][j], v2 = R[2][j];
+            double L[3];
+            if (i == 0) { L[0] = 0.0; L[1] = -v2; L[2] = v1; }
+            else if (i == 1) { L[0] = v2; L[1] = 0.0; L[2] = -v0; }
+            else { L[0] = -v1; L[1] = v0; L[2] = 0.0; }
+            const double len2 = dot3(L, L);
+            if (len2 < 1e-12) continue;
+            const double pr = fabs(dot3(t, L));
+            const double ra = fma(ea[2], fabs(L[2]), fma(ea[1], fabs(L[1]), ea[0] * fabs(L[0])));
+            double rb = 0.0;
+            for (int k = 0; k < 3; ++k) {
+                const double bk[3] = {R[0][k], R[1][k], R[2][k]};
+                rb = fma(eb[k], fabs(dot3(bk, L)), rb);
+            }
+            const double sep = (pr - (ra + rb)) / sqrt(len2);
+            if (sep > best_edge) best_edge = sep;
+        }
+    }
+    if (best_edge > best_face + 1e-12) return 1;
+    const bool refA = fi < 3;
+    const int f = refA ? fi : fi - 3;
+    const double* pR = refA ? pa : pb;
+    const double* pI = refA ? pb : pa;
+    const double* eR = refA ? ea : eb;
+    const double* eI = refA ? eb : ea;
+    double RA[3][3], IA[3][3];
+    for (int j = 0; j < 3; ++j)
+        for (int i = 0; i < 3; ++i) { RA[j][i] = refA ? A[j][i] : Bc[j][i]; IA[j][i] = refA ? Bc[j][i] : A[j][i]; }
+    double n[3] = {RA[f][0], RA[f][1], RA[f][2]};
+    const double dRI[3] = {pI[0] - pR[0], pI[1] - pR[1], pI[2] - pR[2]};
+    if (dot3(dRI, n) < 0.0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+    int k = 0;
+    double kb = -1.0;
+    for (int kk = 0; kk < 3; ++kk) {
+        const double v = fabs(dot3(IA[kk], n));
+        if (v > kb) { kb = v; k = kk; }
+    }
+    const double sg = dot3(IA[k], n) > 0.0 ? -eI[k] : eI[k];
+    const int k1 = k == 2 ? 0 : k + 1, k2 = k == 0 ? 2 : k - 1;
+    double poly[8][3], tmp[8][3];
+    for (int v = 0; v < 4; ++v) {  // incident face corners, cyclic
+        const double c1 = (v == 0 || v == 3) ? eI[k1] : -eI[k1];
+        const double c2 = (v < 2) ? eI[k2] : -eI[k2];
+        for (int i = 0; i < 3; ++i)
+            poly[v][i] = fma(c2, IA[k2][i], fma(c1, IA[k1][i], fma(sg, IA[k][i], pI[i])));
+    }
+    int np = 4;
+#pragma unroll 1
+    for (int pl = 0; pl < 4 && np > 0; ++pl) {  // side planes of the reference face
+        const int ta = (pl < 2) ? (f == 2 ? 0 : f + 1) : (f == 0 ? 2 : f - 1);
+        const double side = (pl & 1) ? -1.0 : 1.0;
+        double dist_prev = 0.0;
+        int m = 0;
+#pragma unroll 1
+        for (int v = 0; v < np; ++v) {
+            const double* P = poly[v];
+            const double* Q = poly[v + 1 < np ? v + 1 : 0];
+            const double dp[3] = {P[0] - pR[0], P[1] - pR[1], P[2] - pR[2]};
+            const double dq[3] = {Q[0] - pR[0], Q[1] - pR[1], Q[2] - pR[2]};
+            const double hp = side * dot3(dp, RA[ta]) - eR[ta];
+            const double hq = side * dot3(dq, RA[ta]) - eR[ta];
+            (void)dist_prev;
+            if (hp <= 0.0) { for (int i = 0; i < 3; ++i) tmp[m][i] = P[i]; ++m; }
+            if ((hp <= 0.0) != (hq <= 0.0)) {
+                const double w = hp / (hp - hq);
+                for (int i = 0; i < 3; ++i) tmp[m][i] = fma(w, Q[i] - P[i], P[i]);
+                ++m;
+            }
+        }
+        np = m;
+        for (int v = 0; v < np; ++v)
+            for (int i = 0; i < 3; ++i) poly[v][i] = tmp[v][i];
+    }
+    const double off = dot3(pR, n) + eR[f];
+    int nd = 0;
+    for (int v = 0; v < np; ++v) {
+        const double depth = off - dot3(poly[v], n);
+        if (-depth < kDeep) ++nd;
+    }
+    return nd > 0 ? nd : 1;
+}
+
+// ---------------------------------------------------------------- cylinder-box, exact
+// The signed distance of two convex bodies is the maximum over directions n of their
+// separation along n (negative: minus the penetration depth), attained at the normal of the
+// closest feature pair.  A cylinder has a cap disc, a lateral surface and two rim circles; a
+// box has faces, edges and vertices.  Every feature pair that can be closest has its normal
+// in one of these families:
+//   (a) box face normals b_k           (b) the cylinder axis a      (c) a x b_k
+//   (d) perp_a(w - c) for each box vertex w (lateral surface vs vertex or vertical edge)
+//   (f) w - (rim point nearest w), both rims (rim circle vs vertex, separated bodies)
+//   (e) rim circle vs box edge: the common normal of a circle and a line = the normal of the
+//       rim's projection along the edge (an ellipse) at its point nearest the projected edge
+//       (Eberly's robust bisection); for a penetration depth also the ellipse's other
+//       locally-nearest point (the deepest point of the Minkowski difference can be one).
+// Every direction gives a lower bound of the signed distance, so "dist < thr" is exact when
+// no candidate separates by >= thr.  (a)-(c) are the finite SAT axes and go first; the rest
+// runs only when those cannot separate.
+struct CylBox {
+    double a[3];     // cylinder axis (world)
+    double T[3];     // box centre - cylinder centre
+    double B[3][3];  // box axes (rows)
+    double e[3];     // box half extents
+    double R, H;     // cylinder radius, half height
+};
+
+SSPP_HD CylBox make_cylbox(const double* pa, const double* ma, const double* sz, const double* pb,
+                           const double* mb, const double* eb) {
+    CylBox c;
+    col3(ma, 2, c.a);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) col3(mb, j, Bc[j]);
-    double T[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+    for (int j = 0; j < 3; ++j) { col3(mb, j, c.B[j]); c.e[j] = eb[j]; }
+    c.T[0] = pb[0] - pa[0]; c.T[1] = pb[1] - pa[1]; c.T[2] = pb[2] - pa[2];
+    c.R = sz[0]; c.H = sz[1];
+    return c;
+}
+
+// true iff the separation along L (any length) is >= thr
+SSPP_HD bool cb_sep(const CylBox& c, const double* L, double thr) {
+    const double len2 = dot3(L, L);
+    if (!(len2 > 1e-30)) return false;
+    const double aL = dot3(c.a, L);
+    const double rr = len2 - aL * aL;
+    const double rc = fma(c.H, fabs(aL), c.R * sqrt(rr > 0.0 ? rr : 0.0));
+    double rb = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) rb = fma(c.e[k], fabs(dot3(c.B[k], L)), rb);
+    const double num = fabs(dot3(c.T, L)) - (rc + rb);
+    return thr == 0.0 ? num >= 0.0 : num >= thr * sqrt(len2);
+}
+
+// families (a)-(c): box faces, cylinder axis, axis x box edges
+SSPP_HD bool cb_base_sep(const CylBox& c, double thr) {
 #pragma unroll
     for (int ax = 0; ax < 7; ++ax) {
         double L[3];
-        if (ax < 3) { L[0] = Bc[ax][0]; L[1] = Bc[ax][1]; L[2] = Bc[ax][2]; }
-        else if (ax == 3) { L[0] = a[0]; L[1] = a[1]; L[2] = a[2]; }
+        if (ax < 3) { L[0] = c.B[ax][0]; L[1] = c.B[ax][1]; L[2] = c.B[ax][2]; }
+        else if (ax == 3) { L[0] = c.a[0]; L[1] = c.a[1]; L[2] = c.a[2]; }
         else {
-            const double* b = Bc[ax - 4];
-            L[0] = a[1] * b[2] - a[2] * b[1];
-            L[1] = a[2] * b[0] - a[0] * b[2];
-            L[2] = a[0] * b[1] - a[1] * b[0];
+            const double* b = c.B[ax - 4];
+            L[0] = c.a[1] * b[2] - c.a[2] * b[1];
+            L[1] = c.a[2] * b[0] - c.a[0] * b[2];
+            L[2] = c.a[0] * b[1] - c.a[1] * b[0];
+            if (dot3(L, L) < 1e-20) continue;  // edge parallel to the axis: family (d)
         }
-        double len2 = dot3(L, L);
-        if (len2 < 1e-12) continue;
-        double aL = dot3(a, L);
-        double rr = len2 - aL * aL;
-        double rc = fma(sz[1], fabs(aL), sz[0] * sqrt(rr > 0.0 ? rr : 0.0));
-        double rb = 0.0;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) rb = fma(eb[k], fabs(dot3(Bc[k], L)), rb);
-        double num = fabs(dot3(T, L)) - (rc + rb);
-        if (thr == 0.0 ? num >= 0.0 : num >= thr * sqrt(len2)) return false;
+        if (cb_sep(c, L, thr)) return true;
     }
-    return true;
+    return false;
+}
+
+// Eberly's F(s) = (r0 z0 / (s + r0))^2 + (z1 / (s + 1))^2 - 1
+SSPP_HD double ell_F(double r0, double z0, double z1, double s) {
+    const double t0 = (r0 * z0) / (s + r0), t1 = z1 / (s + 1.0);
+    return fma(t1, t1, t0 * t0) - 1.0;
+}
+// bisection for the root of F on (lo, hi) with sign(F(lo)) = sgn_lo (midpoint until it hits an end)
+SSPP_HD double ell_bisect(double r0, double z0, double z1, double lo, double hi, double sgn_lo) {
+    double s = lo;
+    for (int i = 0; i < 256; ++i) {
+        s = 0.5 * (lo + hi);
+        if (s == lo || s == hi) break;
+        const double g = ell_F(r0, z0, z1, s);
+        if (g == 0.0) break;
+        if ((g > 0.0) == (sgn_lo > 0.0)) lo = s; else hi = s;
+    }
+    return s;
+}
+// nearest point (x0, x1) of the ellipse x0^2/e0^2 + x1^2/e1^2 = 1 (e0 >= e1 > 0) to (y0, y1) >= 0
+SSPP_HDNI void ellipse_q1(double e0, double e1, double y0, double y1, double* x0, double* x1) {
+    if (y1 > 0.0) {
+        if (y0 > 0.0) {
+            const double z0 = y0 / e0, z1 = y1 / e1;
+            const double g = fma(z1, z1, z0 * z0) - 1.0;
+            if (g != 0.0) {
+                const double q = e0 / e1, r0 = q * q, n0 = r0 * z0;
+                const double hi = g < 0.0 ? 0.0 : sqrt(fma(z1, z1, n0 * n0)) - 1.0;
+                const double s = ell_bisect(r0, z0, z1, z1 - 1.0, hi, 1.0);
+                *x0 = (r0 * y0) / (s + r0);
+                *x1 = y1 / (s + 1.0);
+            } else {
+                *x0 = y0; *x1 = y1;
+            }
+        } else {
+            *x0 = 0.0; *x1 = e1;
+        }
+    } else {
+        const double num = e0 * y0, den = e0 * e0 - e1 * e1;
+        if (num < den) {
+            const double xd = num / den;
+            *x0 = e0 * xd;
+            *x1 = e1 * sqrt(1.0 - xd * xd);
+        } else {
+            *x0 = e0; *x1 = 0.0;
+        }
+    }
+}
+
+// family (e) axis from an ellipse point (x, y) in the (u1, u2) frame: the ellipse normal
+SSPP_HD bool cb_ell_axis(const CylBox& c, const double* u1, const double* u2, double x, double y,
+                         double e0, double e1, double thr) {
+    const double nx = x / (e0 * e0), ny = y / (e1 * e1);
+    const double L[3] = {fma(ny, u2[0], nx * u1[0]), fma(ny, u2[1], nx * u1[1]), fma(ny, u2[2], nx * u1[2])};
+    return cb_sep(c, L, thr);
+}
+
+// The ellipse's other locally-nearest points to p = (px, py) (penetration depth only): the
+// roots of F on (-r0, -1), where F is convex — its minimiser by bisection on F', then one
+// bisection on each side when the minimum is negative; exact-zero coordinates by hand.
+SSPP_HDNI bool cb_ell_other(const CylBox& c, const double* u1, const double* u2, double px, double py,
+                          double e0, double e1, double thr) {
+    const double y0 = fabs(px), y1 = fabs(py), sx = px < 0.0 ? -1.0 : 1.0, sy = py < 0.0 ? -1.0 : 1.0;
+    const double den = e0 * e0 - e1 * e1;
+    if (y1 == 0.0) {  // on the major axis: (+-e0, 0) and the off-axis pair
+        if (cb_ell_axis(c, u1, u2, e0, 0.0, e0, e1, thr)) return true;
+        if (e0 * y0 < den) {
+            const double xd = (e0 * y0) / den, x0 = sx * e0 * xd, x1 = e1 * sqrt(1.0 - xd * xd);
+            if (cb_ell_axis(c, u1, u2, x0, x1, e0, e1, thr) || cb_ell_axis(c, u1, u2, x0, -x1, e0, e1, thr))
+                return true;
+        }
+        return false;
+    }
+    if (y0 == 0.0) {  // on the minor axis: (0, +-e1) and the off-axis pair
+        if (cb_ell_axis(c, u1, u2, 0.0, e1, e0, e1, thr)) return true;
+        if (e1 * y1 < den) {
+            const double x1 = -sy * (e1 * e1 * y1) / den, t = x1 / e1;
+            const double x0 = e0 * sqrt(1.0 - t * t);
+            if (cb_ell_axis(c, u1, u2, x0, x1, e0, e1, thr) || cb_ell_axis(c, u1, u2, -x0, x1, e0, e1, thr))
+                return true;
+        }
+        return false;
+    }
+    const double z0 = y0 / e0, z1 = y1 / e1, q = e0 / e1, r0 = q * q, n0 = r0 * z0;
+    // minimiser of F on (-r0, -1): root of D(s) = n0^2/(s+r0)^3 + z1^2/(s+1)^3 (D < 0 left of it)
+    double lo = -r0, hi = -1.0, s = lo;
+    for (int i = 0; i < 256; ++i) {
+        s = 0.5 * (lo + hi);
+        if (s == lo || s == hi) break;
+        const double a0 = s + r0, a1 = s + 1.0;
+        const double D = (n0 * n0) / (a0 * a0 * a0) + (z1 * z1) / (a1 * a1 * a1);
+        if (D > 0.0) lo = s; else if (D < 0.0) hi = s; else break;
+    }
+    if (!(ell_F(r0, z0, z1, s) < 0.0)) return false;
+    const double sa = ell_bisect(r0, z0, z1, -r0, s, 1.0);
+    const double sb = ell_bisect(r0, z0, z1, s, -1.0, -1.0);
+    const double ss[2] = {sa, sb};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double x0 = sx * ((r0 * y0) / (ss[k] + r0)), x1 = sy * (y1 / (ss[k] + 1.0));
+        if (cb_ell_axis(c, u1, u2, x0, x1, e0, e1, thr)) return true;
+    }
+    return false;
+}
+
+// families (d), (f) and (e); all_roots adds (e)'s non-global critical points
+SSPP_HDNI bool cb_ext_sep(const CylBox& c, double thr, bool all_roots) {
+#pragma unroll 1
+    for (int v = 0; v < 8; ++v) {  // (d), (f): box vertices
+        const double s0 = (v & 1) ? c.e[0] : -c.e[0], s1 = (v & 2) ? c.e[1] : -c.e[1],
+                     s2 = (v & 4) ? c.e[2] : -c.e[2];
+        double w[3], u[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) w[i] = fma(s2, c.B[2][i], fma(s1, c.B[1][i], fma(s0, c.B[0][i], c.T[i])));
+        const double z = dot3(c.a, w);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) u[i] = w[i] - z * c.a[i];
+        const double uu = dot3(u, u);
+        if (!(uu > 1e-30)) continue;
+        if (cb_sep(c, u, thr)) return true;
+        const double f = 1.0 - c.R / sqrt(uu);
+#pragma unroll 1
+        for (int r = 0; r < 2; ++r) {
+            const double dz = z - (r ? c.H : -c.H);
+            const double L[3] = {fma(dz, c.a[0], f * u[0]), fma(dz, c.a[1], f * u[1]), fma(dz, c.a[2], f * u[2])};
+            if (cb_sep(c, L, thr)) return true;
+        }
+    }
+#pragma unroll 1
+    for (int j = 0; j < 3; ++j) {  // (e): rim circles vs box edges along b_j
+        const double* e = c.B[j];
+        double u1[3] = {c.a[1] * e[2] - c.a[2] * e[1], c.a[2] * e[0] - c.a[0] * e[2], c.a[0] * e[1] - c.a[1] * e[0]};
+        const double S2 = dot3(u1, u1);
+        if (S2 < 1e-20) continue;  // edge parallel to the axis: family (d)
+        const double iS = 1.0 / sqrt(S2);
+        u1[0] *= iS; u1[1] *= iS; u1[2] *= iS;
+        const double u2[3] = {e[1] * u1[2] - e[2] * u1[1], e[2] * u1[0] - e[0] * u1[2], e[0] * u1[1] - e[1] * u1[0]};
+        const double e0 = c.R, e1 = c.R * fabs(dot3(c.a, e));
+        const int k1 = j == 2 ? 0 : j + 1, k2 = j == 0 ? 2 : j - 1;
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q) {
+            const double s1 = (q & 1) ? c.e[k1] : -c.e[k1], s2 = (q & 2) ? c.e[k2] : -c.e[k2];
+            double w0[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) w0[i] = fma(s2, c.B[k2][i], fma(s1, c.B[k1][i], c.T[i]));
+#pragma unroll 1
+            for (int r = 0; r < 2; ++r) {
+                const double hs = r ? c.H : -c.H;
+                const double d[3] = {w0[0] - hs * c.a[0], w0[1] - hs * c.a[1], w0[2] - hs * c.a[2]};
+                const double px = dot3(d, u1), py = dot3(d, u2);
+                if (e1 < 1e-9 * e0) {  // the rim's plane contains the edge: a segment
+                    if (fabs(px) <= e0) continue;  // normal = the axis, family (b)
+                    const double ex = px - (px < 0.0 ? -e0 : e0);
+                    const double L[3] = {fma(py, u2[0], ex * u1[0]), fma(py, u2[1], ex * u1[1]), fma(py, u2[2], ex * u1[2])};
+                    if (cb_sep(c, L, thr)) return true;
+                    continue;
+                }
+                double x0, x1;
+                ellipse_q1(e0, e1, fabs(px), fabs(py), &x0, &x1);
+                if (cb_ell_axis(c, u1, u2, px < 0.0 ? -x0 : x0, py < 0.0 ? -x1 : x1, e0, e1, thr)) return true;
+                if (all_roots && cb_ell_other(c, u1, u2, px, py, e0, e1, thr)) return true;
+            }
+        }
+    }
+    return false;
+}
+
+// dist < thr (thr >= 0: MuJoCo's contact test with margin thr)
+SSPP_HDNI bool cyl_box_ext_touch(const CylBox& c, double thr) { return !cb_ext_sep(c, thr, false); }
+
+// dist < thr < 0 (thr = -1e-3: a deep contact, Collision.h:93), exact.  Shortcuts: a
+// cylinder shrunk by -thr (or a box shrunk by -thr) that still overlaps the other body proves
+// depth > -thr, since (A (-) ball) - B lies inside (A - B) (-) ball.
+SSPP_HDNI bool cyl_box_ext_deep(const CylBox& c, double thr) {
+    const double dl = -thr;
+    if (cb_ext_sep(c, thr, false)) return false;
+    if (c.R > dl && c.H > dl) {
+        CylBox s = c;
+        s.R = c.R - dl; s.H = c.H - dl;
+        if (!cb_base_sep(s, 0.0) && !cb_ext_sep(s, 0.0, false)) return true;
+    }
+    if (c.e[0] > dl && c.e[1] > dl && c.e[2] > dl) {
+        CylBox s = c;
+        s.e[0] = c.e[0] - dl; s.e[1] = c.e[1] - dl; s.e[2] = c.e[2] - dl;
+        if (!cb_base_sep(s, 0.0) && !cb_ext_sep(s, 0.0, false)) return true;
+    }
+    return !cb_ext_sep(c, thr, true);
+}
+
+// cylinder (A) vs box (B): signed distance < thr (thr = margin, or kDeep for a deep contact)
+SSPP_HD bool cyl_box_overlap(const double* pa, const double* ma, const double* sz, const double* pb,
+                             const double* mb, const double* eb, double thr) {
+    const CylBox c = make_cylbox(pa, ma, sz, pb, mb, eb);
+    if (cb_base_sep(c, thr)) return false;
+    return thr < 0.0 ? cyl_box_ext_deep(c, thr) : cyl_box_ext_touch(c, thr);
 }
 
 // Supported narrowphase pair? (types ordered t1 <= t2)
@@ -358,23 +707,23 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
         if (t2 == 5) return col_sphere_cyl(p1, s1[0], p2, m2, s2, margin, nd);
         return 0;
     }
-    if (t1 == 5) {  // cylinder-box
+    if (t1 == 5) {  // cylinder-box: exact signed distance test, one contact (MuJoCo's convex collider)
         if (NEED_DEEP) {
-            int d = (margin >= kDeep) ? (int)sat_cyl_box(p1, m1, s1, p2, m2, s2, kDeep)
-                                      : (int)(sat_cyl_box(p1, m1, s1, p2, m2, s2, margin) &&
-                                              sat_cyl_box(p1, m1, s1, p2, m2, s2, kDeep));
+            int d = (margin >= kDeep) ? (int)cyl_box_overlap(p1, m1, s1, p2, m2, s2, kDeep)
+                                      : (int)(cyl_box_overlap(p1, m1, s1, p2, m2, s2, margin) &&
+                                              cyl_box_overlap(p1, m1, s1, p2, m2, s2, kDeep));
             *nd = d;
             return d;
         }
-        return sat_cyl_box(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;
+        return cyl_box_overlap(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;
     }
-    // box-box
+    // box-box: SAT (exact for boxes) decides contact; the deep count comes from the manifold
     if (NEED_DEEP) {
-        int d = (margin >= kDeep) ? (int)sat_box_box(p1, m1, s1, p2, m2, s2, kDeep)
-                                  : (int)(sat_box_box(p1, m1, s1, p2, m2, s2, margin) &&
-                                          sat_box_box(p1, m1, s1, p2, m2, s2, kDeep));
-        *nd = d;
-        return d;
+        const bool d = (margin >= kDeep) ? sat_box_box(p1, m1, s1, p2, m2, s2, kDeep)
+                                         : (sat_box_box(p1, m1, s1, p2, m2, s2, margin) &&
+                                            sat_box_box(p1, m1, s1, p2, m2, s2, kDeep));
+        *nd = d ? box_box_deep_count(p1, m1, s1, p2, m2, s2) : 0;
+        return *nd;
     }
     return sat_box_box(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;
 }

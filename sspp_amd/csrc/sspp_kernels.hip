@@ -35,7 +35,7 @@ constexpr int kBlock = 256;
 #define SSPP_SCORE_WAVES_PER_EU 4  // min waves per SIMD (4 -> <=128 VGPRs; measured best on gfx950)
 #endif
 constexpr int kMaxMovers = 2;
-constexpr int kMaxSteps = 16;  // steps per launch (k_sspp_c2f)
+constexpr int kMaxSteps = 64;  // steps per launch (k_sspp_c2f)
 
 struct KScene {
     int npairs;
@@ -911,7 +911,7 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
 }
 
 #ifndef SSPP_C2F_WAVES_PER_EU
-#define SSPP_C2F_WAVES_PER_EU 1
+#define SSPP_C2F_WAVES_PER_EU 3  // also bounds the out-of-line narrowphase callees (their budget is the callers' minimum)
 #endif
 template <int D, int NM, int P, bool ONEGEOM, int NT>
 __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
@@ -1492,6 +1492,9 @@ struct sspp_job {
     int* d_ospan = nullptr;
     DPair* d_pairs = nullptr;  // this job's pair table (closest-to-the-mean-path first)
     ArgminSync* d_sync = nullptr;  // sharded arrival counters of the fused argmin [kMaxSteps]
+    std::vector<double> h_knots;   // host copies: the knot vector, and the staging of
+    std::vector<double> h_stage;   // sspp_job_update_sspp's asynchronous uploads (init | limits)
+    std::vector<DPair> h_pairs;
     double start[4], end[4], lo[4], hi[4];
     double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
 };
@@ -1893,7 +1896,9 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
         return sspp::set_error(SSPP_E_UNSUPPORTED, "dof must be one of 1,2,3,4,6,7,9");
     if (p < 2 || p > 3) return sspp::set_error(SSPP_E_UNSUPPORTED, "GPU scorer supports spline degree 2 or 3");
     if (n < p + 1) return sspp::set_error(SSPP_E_INVAL, "need at least degree + 1 control points");
-    if (W < 2 || W > 1 << 20) return sspp::set_error(SSPP_E_INVAL, "check_points must be >= 2");
+    // W = 1 is checkCollision(num_samples = 1): u = 0 and 1 (include/sspp.h:134-137); its arc
+    // grid is the single point u = 0 (no chord, arc length 0)
+    if (W < 1 || W > 1 << 20) return sspp::set_error(SSPP_E_INVAL, "check_points must be >= 1");
     if (max_batch < 1) return sspp::set_error(SSPP_E_INVAL, "max_batch must be >= 1");
     if (scene && (scene->mode != SSPP_MODE_QPOS || scene->dof != D))
         return sspp::set_error(SSPP_E_INVAL, "scene was not bound for this dof");
@@ -1901,6 +1906,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     j->kind = 0; j->scene = scene; j->D = D; j->p = p; j->n = n; j->W = W;
     j->nknots = n + p + 1; j->sigma = a->sigma; j->seed = a->seed; j->max_batch = max_batch;
     j->arc_all = a->arc_all ? 1 : 0;
+    j->h_knots.assign(a->knots, a->knots + j->nknots);
     j->nm = scene ? (int)scene->movers.size() : 1;
     if (j->nm < 1) j->nm = 1;
     j->lpc = lanes_for(W - 1);
@@ -1915,7 +1921,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     const int64_t nblk = (max_batch + j->cpb - 1) / j->cpb;
     std::vector<double> us;
     for (int i = 0; i <= W; ++i) us.push_back((double)i / W);            // collision grid
-    for (int i = 0; i < W; ++i) us.push_back((double)i / (W - 1));       // arc-length grid
+    for (int i = 0; i < W; ++i) us.push_back(W > 1 ? (double)i / (W - 1) : 0.0);  // arc-length grid
     if ((rc = upload(&j->d_knots, a->knots, (size_t)j->nknots)) ||
         (rc = upload_basis(us, p, a->knots, j->nknots, &j->d_tab, &j->d_span)) ||
         (rc = upload(&j->d_init, a->init_ctrl, (size_t)n * D)) ||
@@ -1968,7 +1974,10 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc sampler buffer");
     }
     // one record per workgroup: at most max_batch workgroups per step whatever the layout
-    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * std::max<int64_t>(nblk, max_batch) * kMaxSteps) != hipSuccess ||
+    // one record per workgroup and step: k_sspp has nblk workgroups per batch (one step per
+    // launch), k_sspp_c2f ceil(max_batch / cpb2) per step and up to kMaxSteps steps per launch
+    const int64_t nrec = std::max<int64_t>(nblk, ((max_batch + j->cpb2 - 1) / j->cpb2) * kMaxSteps);
+    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nrec) != hipSuccess ||
         hipMalloc((void**)&j->d_sync, sizeof(ArgminSync) * kMaxSteps) != hipSuccess ||
         hipMemset(j->d_sync, 0, sizeof(ArgminSync) * kMaxSteps) != hipSuccess) {
         sspp_job_free(j);
@@ -2028,6 +2037,9 @@ template <int D, int NM, int P>
 static hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
                              hipStream_t st) {
     if (j->nt2 == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
+#ifdef SSPP_DEV_ONLY  // variant builds for experiments: robocrane shape only (fast compile)
+    return hipErrorInvalidValue;
+#endif
     if (j->nt2 == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st);
     return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
 }
@@ -2035,6 +2047,10 @@ static hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs
 template <int P>
 static hipError_t dispatch_c2f_p(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
                                  hipStream_t st) {
+#ifdef SSPP_DEV_ONLY
+    if (P == 3 && j->nm == 1 && j->D == 7) return launch_c2f<7, 1, P>(k, j, o, nblk, st);
+    return hipErrorInvalidValue;
+#endif
     if (j->nm == 2) {
         if (j->D == 9) return launch_c2f<9, 2, P>(k, j, o, nblk, st);
         return hipErrorInvalidValue;
@@ -2054,6 +2070,9 @@ static hipError_t dispatch_c2f_p(const SsppC2F& k, const sspp_job* j, const Sspp
 template <int P>
 static hipError_t dispatch_sspp_p(const SsppK& k, const sspp_job* j, const SsppPtrs& o, int nblk,
                                   hipStream_t st) {
+#ifdef SSPP_DEV_ONLY
+    return hipErrorInvalidValue;
+#endif
     if (j->nm == 2) {
         if (j->D == 9) return launch_sspp<9, 2, P>(k, j, o, nblk, st);
         return hipErrorInvalidValue;
@@ -2090,7 +2109,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     k.arc_all = j->arc_all;
     SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
     if (steps < 1 || steps > kMaxSteps || (steps > 1 && (!j->c2f || d_ctrl || (j->npert > 0 && !j->insample))))
-        return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..16, coarse-to-fine kernel with in-kernel sampling only");
+        return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..64, coarse-to-fine kernel with in-kernel sampling only");
     const int cpb = j->c2f ? j->cpb2 : j->cpb;
     const int nblk = (int)((B + cpb - 1) / cpb);
     hipStream_t st = (hipStream_t)stream;
@@ -2125,6 +2144,32 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
 extern "C" int sspp_job_sample_score(sspp_job* j, int64_t first_id, int64_t B, double* d_arc,
                           uint8_t* d_feasible, double* d_ctrl_out, sspp_best* d_best, void* stream) {
     return run_sspp(j, nullptr, first_id, B, d_arc, d_feasible, d_ctrl_out, d_best, stream);
+}
+
+// Re-target a SamplingPathPlanner job to another plan() call with the same knots, dof and
+// check_points (the drop-in planner caches one job per shape): the initial control points,
+// sigma, limits and seed change; the per-job pair order is recomputed for the new mean path.
+// Uploads are asynchronous on `stream` from job-owned host copies (valid until the next update).
+extern "C" int sspp_job_update_sspp(sspp_job* j, const double* init_ctrl, double sigma,
+                                    const double* limits, uint64_t seed, void* stream) {
+    sspp::clear_error();
+    if (!j || j->kind != 0 || !init_ctrl || !limits) return sspp::set_error(SSPP_E_INVAL, "sspp_job_update_sspp: bad argument");
+    const size_t nd = (size_t)j->n * j->D;
+    hipStream_t st = (hipStream_t)stream;
+    j->h_stage.assign(init_ctrl, init_ctrl + nd);
+    j->h_stage.insert(j->h_stage.end(), limits, limits + j->D);
+    j->sigma = sigma;
+    j->seed = seed;
+    HIPCHK(hipMemcpyAsync(j->d_init, j->h_stage.data(), sizeof(double) * nd, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(j->d_limits, j->h_stage.data() + nd, sizeof(double) * j->D, hipMemcpyHostToDevice, st));
+    if (j->d_pairs && j->scene && !j->h_knots.empty()) {
+        const char* po = getenv("SSPP_PAIR_ORDER");
+        j->h_pairs = (po && atoi(po) == 0) ? j->scene->pairs
+                                           : pairs_for_job(j->scene, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D);
+        HIPCHK(hipMemcpyAsync(j->d_pairs, j->h_pairs.data(), sizeof(DPair) * j->h_pairs.size(),
+                              hipMemcpyHostToDevice, st));
+    }
+    return SSPP_OK;
 }
 
 extern "C" int sspp_job_score_ctrl(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B,
@@ -2333,7 +2378,7 @@ extern "C" int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void*
             if (jobs[c] == jobs[b]) return sspp::set_error(SSPP_E_INVAL, "branches need distinct jobs");
     }
     const int S = steps_per_launch;
-    if (S < 1 || S > kMaxSteps) return sspp::set_error(SSPP_E_INVAL, "steps_per_launch must be in [1, 16]");
+    if (S < 1 || S > kMaxSteps) return sspp::set_error(SSPP_E_INVAL, "steps_per_launch must be in [1, 64]");
     for (int i = 0, l = 0; i < nsteps; i += S, ++l) {
         const int b = l % nbranch, s = std::min(S, nsteps - i);
         const int rc = run_sspp(jobs[b], nullptr, first_id + (int64_t)i * step_stride, B, d_arc[b],

@@ -58,11 +58,12 @@ struct Spline {
         for (int d = 0; d < N; ++d)
             for (int j = 0; j < nn; ++j) ctrl[(size_t)d * nn + j] = c[(size_t)j * N + d];
     }
-    std::vector<double> eval(double u) const {
+    // Eigen's Matrix<double, N, 1> reaches Python as a numpy array of shape (N,)
+    py::array_t<double> eval(double u) const {
         if (ctrl.empty()) throw std::runtime_error("evaluate on an empty spline");
-        std::vector<double> out(N);
+        py::array_t<double> out((ssize_t)N);
         std::vector<double> c = ctrl_nd();
-        ck(sspp_spline_eval(knots.data(), (int)knots.size(), 3, c.data(), N, u, out.data()),
+        ck(sspp_spline_eval(knots.data(), (int)knots.size(), 3, c.data(), N, u, out.mutable_data()),
            "evaluate");
         return out;
     }
@@ -108,6 +109,9 @@ public:
         return true;
     }
 
+    // The device state (scene tables, the job of the last plan() shape, candidate buffers,
+    // pinned staging) lives in one sspp_planner per object; a call allocates nothing on the
+    // device and copies back only the feasible candidates (sspp_hip.h, sspp_planner_plan).
     py::tuple plan(py::array_t<double, py::array::forcecast> start,
                    py::array_t<double, py::array::forcecast> end, double sigma,
                    py::array_t<double, py::array::forcecast> limits, int sample_count,
@@ -116,40 +120,50 @@ public:
         if (sample_count < 1) throw py::value_error("sample_count must be >= 1");
         if (init_points < 4) throw py::value_error("init_points must be >= 4");
         if (check_points < 2) throw py::value_error("check_points must be >= 2");
-        ensure_scene();
+        ensure_planner();
         const int n = init_points;
-        std::vector<double> knots(n + 4), ctrl((size_t)sample_count * n * N), arc(sample_count);
-        std::vector<uint8_t> feas(sample_count);
+        const size_t nd = (size_t)n * N;
+        knots_buf_.resize(n + 4);
+        if (ids_buf_.size() < (size_t)sample_count) {
+            ids_buf_.resize(sample_count);
+            arc_buf_.resize(sample_count);
+        }
+        if (ctrl_buf_.size() < (size_t)sample_count * nd) ctrl_buf_.resize((size_t)sample_count * nd);
         sspp_best best{};
+        int64_t nf = 0;
         int rc;
         {
             py::gil_scoped_release nogil;
-            rc = sspp_plan_sspp(scene_.get(), N, a.data(), b.data(), sigma, l.data(), sample_count,
-                                check_points, init_points, seed, knots.data(), ctrl.data(),
-                                feas.data(), arc.data(), &best);
+            rc = sspp_planner_plan(planner_.get(), a.data(), b.data(), sigma, l.data(), sample_count,
+                                   check_points, init_points, seed, 0, knots_buf_.data(), &nf,
+                                   ids_buf_.data(), arc_buf_.data(), ctrl_buf_.data(), &best);
         }
         ck(rc, "plan");
         py::list paths;
-        for (int i = 0; i < sample_count; ++i) {
-            if (!feas[i]) continue;
+        for (int64_t k = 0; k < nf; ++k) {
             Spline<N> s;
-            s.set_from_nd(knots.data(), (int)knots.size(), ctrl.data() + (size_t)i * n * N, n);
+            s.set_from_nd(knots_buf_.data(), (int)knots_buf_.size(), ctrl_buf_.data() + (size_t)k * nd, n);
             paths.append(py::cast(std::move(s)));
         }
         std::cout << "Sampled " << sample_count << " splines. Successful paths found: "
                   << best.count << std::endl;
         bool found = best.index >= 0;
         if (found) {
-            path_.set_from_nd(knots.data(), (int)knots.size(),
-                              ctrl.data() + (size_t)best.index * n * N, n);
+            // the winner is one of the compacted rows (ids ascending)
+            for (int64_t k = 0; k < nf; ++k) {
+                if (ids_buf_[(size_t)k] != best.index) continue;
+                path_.set_from_nd(knots_buf_.data(), (int)knots_buf_.size(), ctrl_buf_.data() + (size_t)k * nd, n);
+                break;
+            }
         }
         last_best_cost = best.cost;
         last_best_index = best.index;
+        last_feasible_ids.assign(ids_buf_.begin(), ids_buf_.begin() + nf);
         return py::make_tuple(found, paths);
     }
 
-    std::vector<double> evaluate(double u) const { return path_.eval(u); }
-    std::vector<double> evaluate_s(const Spline<N>& s, double u) const { return s.eval(u); }
+    py::array_t<double> evaluate(double u) const { return path_.eval(u); }
+    py::array_t<double> evaluate_s(const Spline<N>& s, double u) const { return s.eval(u); }
 
     Spline<N> sampleWithNoise(const Spline<N>& init, double sigma,
                               py::array_t<double, py::array::forcecast> limits, py::object generator) {
@@ -168,9 +182,11 @@ public:
         return s;
     }
 
+    // include/sspp.h:132-150 checks u = i / num_samples for i = 0..num_samples (num_samples >= 1)
     bool checkCollision(const Spline<N>& s, int num_samples, py::object /*data*/) {
-        if (num_samples < 2) throw py::value_error("num_samples must be >= 2");
-        ensure_scene();
+        if (num_samples < 1) throw py::value_error("num_samples must be >= 1");
+        if (s.ctrl.empty()) throw py::value_error("checkCollision on an empty spline");
+        ensure_planner();
         double arc;
         uint8_t feas;
         sspp_best best;
@@ -178,8 +194,8 @@ public:
         int rc;
         {
             py::gil_scoped_release nogil;
-            rc = sspp_score_ctrl_host(scene_.get(), s.knots.data(), 3, c.data(), 1, s.n(), N,
-                                      num_samples, &arc, &feas, &best);
+            rc = sspp_planner_score(planner_.get(), s.knots.data(), 3, c.data(), 1, s.n(), num_samples, 1,
+                                    &arc, &feas, &best);
         }
         ck(rc, "checkCollision");
         return feas == 0;
@@ -187,12 +203,14 @@ public:
 
     double computeArcLength(const Spline<N>& s, int check_points) {
         if (check_points < 2) throw py::value_error("check_points must be >= 2");
+        if (s.ctrl.empty()) throw py::value_error("computeArcLength on an empty spline");
+        ensure_planner();
         double arc;
         uint8_t feas;
         sspp_best best;
         std::vector<double> c = s.ctrl_nd();
-        ck(sspp_score_ctrl_host(nullptr, s.knots.data(), 3, c.data(), 1, s.n(), N, check_points,
-                                &arc, &feas, &best), "computeArcLength");
+        ck(sspp_planner_score(planner_.get(), s.knots.data(), 3, c.data(), 1, s.n(), check_points, 0,
+                              &arc, &feas, &best), "computeArcLength");
         return arc;
     }
 
@@ -211,8 +229,9 @@ public:
             std::vector<double> arc(paths.size());
             std::vector<uint8_t> feas(paths.size());
             sspp_best b;
-            ck(sspp_score_ctrl_host(nullptr, f.knots.data(), 3, all.data(), (int64_t)paths.size(),
-                                    f.n(), N, check_points, arc.data(), feas.data(), &b),
+            ensure_planner();
+            ck(sspp_planner_score(planner_.get(), f.knots.data(), 3, all.data(), (int64_t)paths.size(),
+                                  f.n(), check_points, 0, arc.data(), feas.data(), &b),
                "findBestPath");
             best = b.cost; bi = b.index;
         } else {
@@ -235,21 +254,31 @@ public:
     uint64_t seed = 0x5EED;
     double last_best_cost = INFINITY;
     int64_t last_best_index = -1;
+    std::vector<int64_t> last_feasible_ids;  // candidate ids of the last plan()'s paths
 
 private:
     struct ModelDel { void operator()(sspp_model* m) const { sspp_model_free(m); } };
     struct SceneDel { void operator()(sspp_scene* s) const { sspp_scene_free(s); } };
+    struct PlannerDel { void operator()(sspp_planner* p) const { sspp_planner_free(p); } };
 
-    void ensure_scene() {
-        if (scene_) return;
-        sspp_scene* s = nullptr;
-        ck(sspp_scene_create(model_.get(), SSPP_MODE_QPOS, N, 0, &s), "scene");
-        scene_.reset(s);
+    void ensure_planner() {
+        if (planner_) return;
+        if (!scene_) {
+            sspp_scene* s = nullptr;
+            ck(sspp_scene_create(model_.get(), SSPP_MODE_QPOS, N, 0, &s), "scene");
+            scene_.reset(s);
+        }
+        sspp_planner* p = nullptr;
+        ck(sspp_planner_create(scene_.get(), N, &p), "planner");
+        planner_.reset(p);
     }
 
     std::string xml_path_;
     std::unique_ptr<sspp_model, ModelDel> model_;
     std::unique_ptr<sspp_scene, SceneDel> scene_;
+    std::unique_ptr<sspp_planner, PlannerDel> planner_;  // declared after scene_: freed first
+    std::vector<double> knots_buf_, arc_buf_, ctrl_buf_;
+    std::vector<int64_t> ids_buf_;
     Spline<N> path_;
 };
 
@@ -287,7 +316,8 @@ void bind(py::module& m, const std::string& planner_name, const std::string& spl
              py::arg("sample_count") = 50, py::arg("check_points") = 50, py::arg("init_points") = 10)
         .def_readwrite("seed", &P::seed)
         .def_readonly("last_best_cost", &P::last_best_cost)
-        .def_readonly("last_best_index", &P::last_best_index);
+        .def_readonly("last_best_index", &P::last_best_index)
+        .def_readonly("last_feasible_ids", &P::last_feasible_ids);
 }
 
 }  // namespace

@@ -381,9 +381,13 @@ class CesPlanner:
         self.update(stream)
 
     def _exchange(self, stream=None):
-        """All-gather every rank's slot records (one RCCL collective), then unpack them into
-        this rank's planner so the update sees the whole candidate list."""
-        import torch.distributed as dist
+        """All-gather every rank's slot records (one collective), then unpack them into this
+        rank's planner so the update sees the whole candidate list.
+
+        Pack, gather and unpack are all ordered on `stream`: the collective is issued with
+        `stream` as torch's current stream (RCCL orders its work after the current stream's
+        and makes the current stream wait for the result), so a planner driven on a
+        non-default stream cannot gather before the pack or unpack before the gather."""
         torch = _torch()
         rec = 5 + 4 * self.K
         if getattr(self, "_xbuf", None) is None:
@@ -391,9 +395,10 @@ class CesPlanner:
             self._xbuf = (torch.empty(self.spr * rec, dtype=torch.float64, device=dev),
                           torch.empty(self.world * self.spr * rec, dtype=torch.float64, device=dev))
         local, full = self._xbuf
-        check(lib().sspp_ces_pack(self._h, self.rank, _ptr(local), _stream(stream)), "ces pack")
-        dist.all_gather_into_tensor(full, local, group=self.group)
-        check(lib().sspp_ces_unpack(self._h, _ptr(full), _stream(stream)), "ces unpack")
+        with torch.cuda.stream(torch_stream(stream)):
+            check(lib().sspp_ces_pack(self._h, self.rank, _ptr(local), _stream(stream)), "ces pack")
+            all_gather_records(full, local, self.group)
+            check(lib().sspp_ces_unpack(self._h, _ptr(full), _stream(stream)), "ces unpack")
 
     def plan(self, start, end, iterate=False, iterations=1, stream=None):
         """iterations x plan(start, end, iterate) without host synchronisation (world == 1)."""
@@ -431,6 +436,31 @@ class CesPlanner:
         check(lib().sspp_ces_set_state(self._h, *ptrs, int(has_best)), "ces set_state")
 
 
+def torch_stream(stream):
+    """A torch stream object for `stream` (None = current, raw hipStream_t int = external)."""
+    torch = _torch()
+    if stream is None:
+        return torch.cuda.current_stream()
+    if isinstance(stream, int):
+        return torch.cuda.ExternalStream(stream)
+    return stream
+
+
+def all_gather_records(out, local, group=None):
+    """all_gather_into_tensor of device records on torch's current stream.  RCCL ("nccl")
+    gathers device memory directly over xGMI; a gloo group (the CPU tests' backend) is staged
+    through host memory, in the same stream order."""
+    import torch.distributed as dist
+    torch = _torch()
+    if dist.get_backend(group) == "gloo":
+        host = local.cpu()  # waits for the current stream's work on `local`
+        gathered = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(gathered, host, group=group)
+        out.copy_(gathered)
+        return
+    dist.all_gather_into_tensor(out, local, group=group)
+
+
 def reduce_best_steps(parts, out, stream=None):
     """parts: (R, G, 4) int64 device tensor of per-rank step records -> out (G, 4)."""
     R, G = parts.shape[0], parts.shape[1]
@@ -444,5 +474,6 @@ def device_count():
     return n.value if rc == 0 else 0
 
 
-__all__ = ["Model", "Scene", "SsppJob", "TspJob", "CesPlanner", "SsppSteps", "reduce_best_steps", "interpolate", "spline_eval", "best_tensor",
+__all__ = ["Model", "Scene", "SsppJob", "TspJob", "CesPlanner", "SsppSteps", "reduce_best_steps", "all_gather_records",
+           "torch_stream", "interpolate", "spline_eval", "best_tensor",
            "decode_best", "reduce_best", "reduce_best_device", "device_count", "DEFAULT_SEED", "math"]

@@ -16,6 +16,7 @@ from oracle import oracle as O
 from tests.conftest import SCENES
 
 STACKING = os.path.join(SCENES, "stacking.xml")
+ROBOCRANE = os.path.join(SCENES, "robocrane.xml")
 LO, HI = (-0.5, -0.5, 0.0, -1.6), (0.5, 0.5, 0.6, 1.6)
 
 
@@ -281,3 +282,65 @@ def test_tsp_module_surface(cuda):
     with pytest.raises(RuntimeError):
         _tsp.TaskSpacePlanner(STACKING, "no_such_body")
     assert _tsp.__backend__ == "hip-gfx950" and "sspp._tsp" in sys.modules
+
+
+@pytest.mark.gpu
+def test_config5_multigoal_full_size_each_iteration(cuda):
+    """BASELINE configs[4] at its stated size: the gripper TaskSpacePlanner (7 collidable geoms)
+    on robocrane.xml, 4096 sampled via sets x 128 checks, all 8 bench goals, 3 CES iterations
+    each (tsp_planner.h:72-145).  Per iteration, against the oracle on the device's own via sets:
+    status identical, costs <= 1e-9, then elites / best slot / mean / sigma bit-identical."""
+    import bench
+    import sspp_amd as S
+    model = S.Model(ROBOCRANE)
+    body = model.body_id("gripper_collision_with_block/")
+    scene = S.Scene(model, 1, body)
+    osc = O.Scene(mjcf_ref.load(ROBOCRANE), 1, body)
+    lo, hi = bench.MG_LO, bench.MG_HI
+    samples, checks = 4096, 128
+    seen_success = 0
+    for g, (st, en) in enumerate(bench.MULTIGOAL):
+        st, en = np.array(st), np.array(en)
+        pl = S.CesPlanner(scene, sample_count=samples, check_points=checks, init_points=3,
+                          limits_min=lo, limits_max=hi, seed=S.DEFAULT_SEED + g)
+        prev = None
+        for t in range(3):
+            if prev is None:
+                m_in, s_in = O.ces_reset(st, en, 3, lo=lo, hi=hi)
+                lb_in, hb_in = np.zeros((1, 4)), False
+            else:
+                m_in, s_in, lb_in, hb_in = prev["mean"], prev["sigma"], prev["last_best"], prev["has_best"]
+            pl.step(st, en, iterate=t > 0)
+            r = pl.read()
+            nfx = 2 if (t > 0 and hb_in) else 1
+            assert r["n_fixed"] == nfx and r["n_candidates"] == nfx + samples
+            smp = O.sample_tsp(m_in, s_in, lo, hi, 0.0, S.DEFAULT_SEED + g, t * samples, samples)
+            assert np.abs(r["vias"][nfx:] - smp).max() <= 1e-12
+            L, Cnf, Cwf, stt, cost = O.tsp_score(osc, st, en, r["vias"], checks)
+            np.testing.assert_array_equal(r["status"], stt)
+            fin = np.isfinite(cost)
+            np.testing.assert_array_equal(np.isfinite(r["cost"]), fin)
+            assert np.abs(r["cost"][fin] - cost[fin]).max() <= 1e-9
+            for a, b in ((r["L"], L), (r["C_nf"], Cnf), (r["C_wf"], Cwf)):
+                assert np.abs(a - b).max() <= 1e-9
+            m, s, lb, hb, ns, el, bs = O.ces_update(r["cost"], r["status"], r["vias"], m_in, s_in,
+                                                    lb_in, hb_in, lo=lo, hi=hi)
+            assert r["n_success"] == ns and r["best_slot"] == bs and r["has_best"] == hb
+            np.testing.assert_array_equal(r["elites"], el)
+            np.testing.assert_array_equal(r["mean"], m)
+            np.testing.assert_array_equal(r["sigma"], s)
+            np.testing.assert_array_equal(r["last_best"], lb)
+            seen_success += ns > 0
+            prev = r
+    assert seen_success >= 8  # most goals find collision-free via sets
+
+
+@pytest.mark.gpu
+def test_elite_fraction_above_one_rejected(cuda):
+    """tsp_elites.h:15-19 would partial_sort past the end for frac > 1: rejected at creation."""
+    import sspp_amd as S
+    model = S.Model(STACKING)
+    scene = S.Scene(model, 1, model.body_id("block1"))
+    with pytest.raises(S.SsppError, match="elite_fraction"):
+        S.CesPlanner(scene, sample_count=100, check_points=32, elite_fraction=1.5)
+    S.CesPlanner(scene, sample_count=100, check_points=32, elite_fraction=1.0)  # accepted

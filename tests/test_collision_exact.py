@@ -1,0 +1,174 @@
+"""Exactness of the cylinder-box narrowphase and the box-box contact manifold.
+
+MuJoCo is absent here, so the restated collision rules are pinned by independent
+geometry, not by MuJoCo output:
+
+* cylinder-box: the signed distance of two convex bodies is max over unit directions n of their
+  separation along n.  The reference below evaluates that separation (from the support
+  functions) on a dense Fibonacci sphere and refines the best directions by a shrinking random
+  search — no candidate-axis reasoning at all — and the oracle's contact (dist < margin) and
+  deep-contact (dist < -1e-3, include/Collision.h:93) decisions must agree with it on random
+  oriented pairs, near-threshold cases skipped.
+* box-box: SAT is exact for boxes; the manifold's deep count is checked on hand configurations
+  with known contact polygons and on random pairs (>= 1 exactly when the SAT depth > 1e-3).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from tests.test_collision_known import BOX, CYL, _qmat, contacts
+
+DEEP = -1e-3
+
+
+def _fib_sphere(n):
+    i = np.arange(n) + 0.5
+    phi = np.arccos(1 - 2 * i / n)
+    th = math.pi * (1 + 5 ** 0.5) * i
+    return np.stack([np.cos(th) * np.sin(phi), np.sin(th) * np.sin(phi), np.cos(phi)], 1)
+
+
+def _sep(ns, T, a, H, R, Bm, e):
+    """separation along unit directions ns (M, 3): |T.n| - (h_cyl(n) + h_box(n))"""
+    an = ns @ a
+    perp = np.sqrt(np.maximum(1.0 - an * an, 0.0))
+    return np.abs(ns @ T) - (H * np.abs(an) + R * perp + np.abs(ns @ Bm) @ e)
+
+
+def ref_signed_distance(T, a, H, R, Bm, e, rng, dense=40000, rounds=60):
+    """max over the sphere of the separation: dense sampling + shrinking random refinement"""
+    ns = _fib_sphere(dense)
+    s = _sep(ns, T, a, H, R, Bm, e)
+    top = np.argsort(-s)[:8]
+    best_n, best = ns[top], s[top]
+    scale = 0.05
+    for _ in range(rounds):
+        cand = best_n[:, None, :] + scale * rng.normal(size=(len(best_n), 48, 3))
+        cand /= np.linalg.norm(cand, axis=2, keepdims=True)
+        cs = _sep(cand.reshape(-1, 3), T, a, H, R, Bm, e).reshape(len(best_n), -1)
+        k = cs.argmax(1)
+        better = cs[np.arange(len(best_n)), k] > best
+        best_n[better] = cand[better, k[better]]
+        best[better] = cs[better, k[better]]
+        scale *= 0.75
+    return best.max()
+
+
+def sat7_lower_bound(T, a, H, R, Bm, e):
+    """the 7 finite SAT axes alone (round-1 restatement): a lower bound of the distance"""
+    axes = [Bm[:, k] for k in range(3)] + [a] + [np.cross(a, Bm[:, k]) for k in range(3)]
+    axes = np.array([x / np.linalg.norm(x) for x in axes if np.linalg.norm(x) > 1e-9])
+    return _sep(axes, T, a, H, R, Bm, e).max()
+
+
+def _random_pair(rng):
+    R, H = rng.uniform(0.02, 0.15), rng.uniform(0.02, 0.15)
+    e = rng.uniform(0.02, 0.2, 3)
+    qc, qb = rng.normal(size=4), rng.normal(size=4)
+    qc, qb = qc / np.linalg.norm(qc), qb / np.linalg.norm(qb)
+    d = rng.normal(size=3)
+    d /= np.linalg.norm(d)
+    # centre distance spread around touching (reach along d of both bodies)
+    reach = np.linalg.norm(e) + math.hypot(R, H)
+    T = d * rng.uniform(0.3, 1.05) * reach
+    return R, H, e, qc, qb, T
+
+
+@pytest.mark.parametrize("margin", [0.0, 0.001, 0.01])
+def test_cylinder_box_contact_matches_support_function_reference(margin):
+    rng = np.random.default_rng(7 + int(margin * 1000))
+    n, agree, sat7_wrong, deep_checked = 0, 0, 0, 0
+    for _ in range(450):
+        R, H, e, qc, qb, T = _random_pair(rng)
+        Mc, Mb = _qmat(qc), _qmat(qb)
+        a = Mc[:, 2]
+        dist = ref_signed_distance(T, a, H, R, Mb, e, rng)
+        cont, cost, nd = contacts([(CYL, (R, H, 0), (0, 0, 0), tuple(qc), margin)],
+                                  [(BOX, tuple(e), (0, 0, 0), (1, 0, 0, 0))], T, tuple(qb))
+        if abs(dist - margin) > 1e-6:
+            n += 1
+            agree += (cont > 0) == (dist < margin)
+            sat7_wrong += (sat7_lower_bound(T, a, H, R, Mb, e) < margin) != (dist < margin)
+        if abs(dist - DEEP) > 1e-6:
+            deep_checked += 1
+            assert (nd > 0) == (dist < DEEP), (R, H, e, qc, qb, T, dist)
+    assert n > 400 and agree == n
+    assert deep_checked > 400
+    # the configurations exercise the non-SAT families: the 7-axis test alone errs on some
+    assert sat7_wrong > 0
+
+
+# ---------------------------------------------------------------- box-box manifold
+BIG = (BOX, (0.3, 0.3, 0.1), (0, 0, 0), (1, 0, 0, 0))
+
+
+def _deep(moving_size, pos, quat=(1, 0, 0, 0), static=BIG):
+    return contacts([static], [(BOX, moving_size, (0, 0, 0), (1, 0, 0, 0))], pos, quat)
+
+
+def test_box_box_manifold_face_contacts():
+    # a 45-degree-rotated small box sunk 5 mm into the big box's top face: 4 corners inside
+    q45 = (math.cos(math.pi / 8), 0, 0, math.sin(math.pi / 8))
+    assert _deep((0.05, 0.05, 0.05), (0, 0, 0.145), q45)[2] == 4
+    # sunk only 0.5 mm: in contact, no deep contact
+    n, _, nd = _deep((0.05, 0.05, 0.05), (0, 0, 0.1495), q45)
+    assert (n, nd) == (1, 0)
+    # equal footprints, offset by half a box in y: two incident corners + two clip points
+    eq = (BOX, (0.1, 0.1, 0.1), (0, 0, 0), (1, 0, 0, 0))
+    assert _deep((0.1, 0.1, 0.1), (0, 0.1, 0.195), static=eq)[2] == 4
+    # partly overhanging the big box's edge: corners outside are clipped to the side plane
+    assert _deep((0.05, 0.05, 0.05), (0.28, 0, 0.145))[2] == 4
+
+
+def test_box_box_manifold_tilted_edge_and_edge_edge():
+    # tilted about x so that one bottom edge dips 5 mm deep and the other is above the face
+    ang = 0.2
+    qx = (math.cos(ang / 2), math.sin(ang / 2), 0, 0)
+    e = 0.05
+    low = e * math.cos(ang) + e * math.sin(ang)  # depth of the lowest edge below the centre
+    n, _, nd = _deep((e, e, e), (0, 0, 0.1 + low - 0.005), qx)
+    assert nd == 2
+    # edge against edge: two boxes rotated 45 deg about orthogonal horizontal axes
+    s = math.sqrt(2) * 0.05
+    qa = (math.cos(math.pi / 8), math.sin(math.pi / 8), 0, 0)
+    qb = (math.cos(math.pi / 8), 0, math.sin(math.pi / 8), 0)
+    a = (BOX, (0.05, 0.05, 0.05), (0, 0, 0), qa)
+    n, _, nd = contacts([a], [(BOX, (0.05, 0.05, 0.05), (0, 0, 0), (1, 0, 0, 0))], (0, 0, 2 * s - 0.004), qb)
+    assert (n, nd) == (1, 1)
+    n, _, nd = contacts([a], [(BOX, (0.05, 0.05, 0.05), (0, 0, 0), (1, 0, 0, 0))], (0, 0, 2 * s - 0.0005), qb)
+    assert (n, nd) == (1, 0)
+
+
+def _box_sat_distance(pa, Ma, ea, pb, Mb, eb):
+    """exact signed distance of two boxes: max separation over the 15 SAT axes"""
+    axes = [Ma[:, i] for i in range(3)] + [Mb[:, j] for j in range(3)]
+    axes += [np.cross(Ma[:, i], Mb[:, j]) for i in range(3) for j in range(3)]
+    best = -np.inf
+    T = pb - pa
+    for L in axes:
+        n = np.linalg.norm(L)
+        if n < 1e-6:
+            continue
+        L = L / n
+        best = max(best, abs(T @ L) - (np.abs(Ma.T @ L) @ ea + np.abs(Mb.T @ L) @ eb))
+    return best
+
+
+def test_box_box_manifold_random_pairs():
+    rng = np.random.default_rng(11)
+    checked, multi = 0, 0
+    for _ in range(400):
+        ea, eb = rng.uniform(0.03, 0.2, 3), rng.uniform(0.03, 0.2, 3)
+        qa, qb = rng.normal(size=4), rng.normal(size=4)
+        qa, qb = qa / np.linalg.norm(qa), qb / np.linalg.norm(qb)
+        d = rng.normal(size=3)
+        pb = d / np.linalg.norm(d) * rng.uniform(0.3, 1.0) * (np.linalg.norm(ea) + np.linalg.norm(eb))
+        dist = _box_sat_distance(np.zeros(3), _qmat(qa), ea, pb, _qmat(qb), eb)
+        n, _, nd = contacts([(BOX, ea, (0, 0, 0), qa)], [(BOX, eb, (0, 0, 0), (1, 0, 0, 0))], pb, qb)
+        assert 0 <= nd <= 8
+        if abs(dist - DEEP) > 1e-9:
+            checked += 1
+            assert (nd > 0) == (dist < DEEP)
+        multi += nd > 1
+    assert checked > 390 and multi > 20

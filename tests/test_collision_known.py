@@ -79,7 +79,9 @@ def test_sphere_and_cylinder_on_plane():
 
 def test_box_box_axis_aligned():
     a = (BOX, (0.5, 0.5, 0.5), (0, 0, 0), (1, 0, 0, 0))
-    assert contacts([a], [a], (0.9, 0, 0))[:3:2] == (1, 1)
+    # face against face, 0.1 deep: the clipped manifold has the 4 incident corners, all deep
+    # (n counts the pair: SamplingPathPlanner feasibility only needs n > 0)
+    assert contacts([a], [a], (0.9, 0, 0))[:3:2] == (1, 4)
     assert contacts([a], [a], (0.9995, 0, 0))[:3:2] == (1, 0)  # overlap 5e-4: not deep
     assert contacts([a], [a], (1.0, 0, 0))[0] == 0
     assert contacts([a], [a], (1.1, 0, 0))[0] == 0
@@ -187,6 +189,7 @@ def test_stacking_tsp_cost(robocrane):
     assert s.npairs() == (3, 3)  # block1 vs floor/block2/block3; block2-floor, block3-floor, 2-3
     n, cost, nd = s.contacts(np.array([0.205, 0.0, 0.12, 0.0]))
     assert (n, cost) == (0, 0.0)
-    # overlapping block2 by 50 mm in x: one deep box-box contact, centre distance 0.15
+    # overlapping block2 by 50 mm in x, face to face: the manifold's 4 corners are all deep
+    # (Collision.h:89-101 adds one term per contact), centre distance 0.15
     n, cost, nd = s.contacts(np.array([0.15, 0.0, 0.1, 0.0]))
-    assert nd == 1 and cost == pytest.approx(-1.0 / (0.15 + 1e-4), rel=1e-14)
+    assert nd == 4 and cost == pytest.approx(4 * -1.0 / (0.15 + 1e-4), rel=1e-14)

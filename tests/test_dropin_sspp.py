@@ -100,3 +100,57 @@ def test_other_dofs(sp):
         arc, feas = O.sspp_score(osc, init.knots(), 3, ctrl, 32)
         assert len(paths) == int(feas.sum())
         assert ok == bool(feas.any())
+
+
+def test_evaluate_returns_ndarray(sp):
+    """Eigen Matrix<double, N, 1> returns reach Python as numpy arrays of shape (N,)."""
+    planner = sp.SamplingPathPlanner7(ROBOCRANE)
+    s = sp.Spline7()
+    start = np.array([0.3, 0.2, 0.5, 1, 0, 0, 0])
+    planner.initializePath(start, start + [0.2, 0, 0, 0, 0, 0, 0], s, 7)
+    for v in (planner.evaluate(s, 0.5), s(0.5)):
+        assert isinstance(v, np.ndarray) and v.shape == (7,) and v.dtype == np.float64
+    np.testing.assert_allclose(planner.evaluate(s, 0.0) - start, np.zeros(7), atol=1e-12)
+
+
+def test_check_collision_one_sample(sp):
+    """include/sspp.h:132-150 with num_samples = 1 checks only u = 0 and u = 1."""
+    planner = sp.SamplingPathPlanner7(ROBOCRANE)
+    start = np.array([0.5, 0.15, 0.136, 0.707, 0, 0, 0.707])
+    end = np.array([0.5, -0.05, 0.136, 0.707, 0, 0, 0.707])  # the straight line crosses the bricks
+    s = sp.Spline7()
+    planner.initializePath(start, end, s, 10)
+    assert not planner.checkCollision(s, 1)   # both end points are free
+    assert planner.checkCollision(s, 20)      # the middle is not
+
+
+def test_plan_cached_state_across_shapes(sp, capfd):
+    """The cached device planner (sspp_planner_plan) re-targets its job between calls: every
+    call must still equal the oracle, whatever the shape sequence (same shape, new start/end,
+    new sigma, larger and smaller batches, other init_points / check_points)."""
+    planner = sp.SamplingPathPlanner7(ROBOCRANE)
+    osc = O.Scene(mjcf_ref.load(ROBOCRANE), 0, 7)
+    base_s = np.array([0.5, 0.15, 0.136, 0.707, 0, 0, 0.707])
+    base_e = np.array([0.5, -0.05, 0.136, 0.707, 0, 0, 0.707])
+    calls = [(base_s, base_e, 0.08, 1024, 64, 10), (base_s, base_e, 0.08, 1024, 64, 10),
+             (base_s + [0, 0, 0.05, 0, 0, 0, 0], base_e, 0.12, 1024, 64, 10),
+             (base_s, base_e, 0.08, 3000, 64, 10), (base_s, base_e, 0.05, 700, 64, 10),
+             (base_s, base_e, 0.08, 512, 96, 8), (base_s, base_e, 0.08, 512, 96, 8)]
+    for k, (st, en, sig, B, W, n) in enumerate(calls):
+        planner.seed = 1000 + k
+        ok, paths = planner.plan(st, en, sig, np.ones(7), sample_count=B, check_points=W, init_points=n)
+        init = sp.Spline7()
+        planner.initializePath(st, en, init, n)
+        ctrl = O.sample_sspp(init.ctrls().T.copy(), 3, sig, np.ones(7), planner.seed, 0, B)
+        arc, feas = O.sspp_score(osc, init.knots(), 3, ctrl, W)
+        ids = np.nonzero(feas)[0]
+        assert list(planner.last_feasible_ids) == list(ids)
+        assert len(paths) == len(ids) and ok == bool(len(ids))
+        for s, i in zip(paths, ids):
+            np.testing.assert_allclose(s.ctrls().T, ctrl[i], rtol=0, atol=1e-12)
+        if ok:
+            idx, best = O.argmin(arc, feas)
+            assert planner.last_best_index == idx
+            assert abs(planner.last_best_cost - best) <= 1e-12
+            np.testing.assert_allclose(planner.get_ctrl_pts().T, ctrl[idx], atol=1e-12)
+    capfd.readouterr()
