@@ -57,7 +57,7 @@ def parse():
                          "per-call latency of the reference's entry point "
                          "_sspp.SamplingPathPlanner7.plan (src/sspp_bindings.cpp:43-50)")
     ap.add_argument("--chunk", type=int, default=64)
-    ap.add_argument("--steps-per-launch", type=int, default=8,
+    ap.add_argument("--steps-per-launch", type=int, default=32,
                     help="native mode: independent steps (each its own B candidates, outputs and "
                          "argmin) grouped into one kernel launch")
     a = ap.parse_args()

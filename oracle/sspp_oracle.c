@@ -686,10 +686,12 @@ static int sat_box_box(const double* pa, const double* ma, const double* ea, con
  * term per MuJoCo contact; MuJoCo's box-box collider reports up to 8).  The SAT axis of least
  * penetration decides: an edge-edge axis (separation above every face axis by > 1e-12) gives
  * one contact; a face axis makes that face the reference face and the most anti-parallel face
- * of the other box the incident face, clipped (Sutherland-Hodgman) against the reference
- * face's side planes; each clipped point is a contact with dist = -(depth below the reference
- * face).  Returns the contacts with dist < -1e-3, at least 1 (called only when the SAT depth
- * exceeds 1e-3; no clipped point is deeper than it).  DESIGN.md §4.                        */
+ * of the other box the incident face.  Contacts = vertices of the incident face clipped to the
+ * reference face's rectangle, dist = -(depth below the face): every incident edge's clipped
+ * segment (Liang-Barsky) gives its entry point and, if it leaves early, its exit point, and the
+ * reference corners strictly inside the incident face are vertices too.  Returns the contacts
+ * with dist < -1e-3, at least 1 (called only when the SAT depth exceeds 1e-3; no clipped point
+ * is deeper than it).  DESIGN.md §4.                                                          */
 static int box_box_deep_count(const double* pa, const double* ma, const double* ea,
                               const double* pb, const double* mb, const double* eb) {
     double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
@@ -749,41 +751,59 @@ static int box_box_deep_count(const double* pa, const double* ma, const double* 
     }
     double sg = dot3(IA[k], n) > 0.0 ? -eI[k] : eI[k];
     int k1 = k == 2 ? 0 : k + 1, k2 = k == 0 ? 2 : k - 1;
-    double poly[8][3], tmp[8][3];
+    /* incident corners in the reference face frame: (u, v) along its axes, d = depth */
+    int ta = f == 2 ? 0 : f + 1, tb = f == 0 ? 2 : f - 1;
+    double off = dot3(pR, n) + eR[f];
+    double cu[4], cv[4], cd[4];
     for (int v = 0; v < 4; ++v) {
         double c1 = (v == 0 || v == 3) ? eI[k1] : -eI[k1];
         double c2 = (v < 2) ? eI[k2] : -eI[k2];
-        for (int i = 0; i < 3; ++i)
-            poly[v][i] = fma(c2, IA[k2][i], fma(c1, IA[k1][i], fma(sg, IA[k][i], pI[i])));
+        double P[3], dp[3];
+        for (int i = 0; i < 3; ++i) {
+            P[i] = fma(c2, IA[k2][i], fma(c1, IA[k1][i], fma(sg, IA[k][i], pI[i])));
+            dp[i] = P[i] - pR[i];
+        }
+        cu[v] = dot3(dp, RA[ta]);
+        cv[v] = dot3(dp, RA[tb]);
+        cd[v] = off - dot3(P, n);
     }
-    int np = 4;
-    for (int pl = 0; pl < 4 && np > 0; ++pl) {
-        int ta = (pl < 2) ? (f == 2 ? 0 : f + 1) : (f == 0 ? 2 : f - 1);
-        double side = (pl & 1) ? -1.0 : 1.0;
-        int m = 0;
-        for (int v = 0; v < np; ++v) {
-            const double* P = poly[v];
-            const double* Q = poly[v + 1 < np ? v + 1 : 0];
-            double dp[3] = {P[0] - pR[0], P[1] - pR[1], P[2] - pR[2]};
-            double dq[3] = {Q[0] - pR[0], Q[1] - pR[1], Q[2] - pR[2]};
-            double hp = side * dot3(dp, RA[ta]) - eR[ta];
-            double hq = side * dot3(dq, RA[ta]) - eR[ta];
-            if (hp <= 0.0) { for (int i = 0; i < 3; ++i) tmp[m][i] = P[i]; ++m; }
-            if ((hp <= 0.0) != (hq <= 0.0)) {
-                double w = hp / (hp - hq);
-                for (int i = 0; i < 3; ++i) tmp[m][i] = fma(w, Q[i] - P[i], P[i]);
-                ++m;
+    double eu = eR[ta], ev = eR[tb];
+    int nd = 0;
+    /* each incident edge clipped to the face rectangle (Liang-Barsky, boundary inclusive):
+       its entry point, and its exit point when it leaves early */
+    for (int e = 0; e < 4; ++e) {
+        int e2 = (e + 1) & 3;
+        double du = cu[e2] - cu[e], dv = cv[e2] - cv[e];
+        double t0 = 0.0, t1 = 1.0;
+        int ok = 1;
+        double pp[4] = {-du, du, -dv, dv};
+        double qq[4] = {cu[e] + eu, eu - cu[e], cv[e] + ev, ev - cv[e]};
+        for (int c = 0; c < 4; ++c) {
+            if (pp[c] == 0.0) {
+                if (qq[c] < 0.0) ok = 0;
+            } else {
+                double r = qq[c] / pp[c];
+                if (pp[c] < 0.0) { if (r > t0) t0 = r; }
+                else if (r < t1) t1 = r;
             }
         }
-        np = m;
-        for (int v = 0; v < np; ++v)
-            for (int i = 0; i < 3; ++i) poly[v][i] = tmp[v][i];
+        if (ok && t0 <= t1) {
+            double dd = cd[e2] - cd[e];
+            if (-fma(t0, dd, cd[e]) < DEEP) ++nd;
+            if (t1 < 1.0 && -fma(t1, dd, cd[e]) < DEEP) ++nd;
+        }
     }
-    double off = dot3(pR, n) + eR[f];
-    int nd = 0;
-    for (int v = 0; v < np; ++v) {
-        double depth = off - dot3(poly[v], n);
-        if (-depth < DEEP) ++nd;
+    /* face rectangle corners strictly inside the incident parallelogram */
+    double au = cu[1] - cu[0], av = cv[1] - cv[0], bu = cu[3] - cu[0], bv = cv[3] - cv[0];
+    double det = au * bv - av * bu;
+    for (int q = 0; q < 4; ++q) {
+        double qu = (q & 1) ? eu : -eu, qv = (q & 2) ? ev : -ev;
+        double wu = qu - cu[0], wv = qv - cv[0];
+        double al = (wu * bv - wv * bu) / det, be = (au * wv - av * wu) / det;
+        if (al > 0.0 && al < 1.0 && be > 0.0 && be < 1.0) {
+            double d = fma(be, cd[3] - cd[0], fma(al, cd[1] - cd[0], cd[0]));
+            if (-d < DEEP) ++nd;
+        }
     }
     return nd > 0 ? nd : 1;
 }
@@ -989,29 +1009,74 @@ static int cb_ext_sep(const or_cylbox* c, double thr, int all_roots) {
     return 0;
 }
 
-/* dist < thr < 0, exact; shrunk-body shortcuts ((A (-) ball) - B lies in (A - B) (-) ball) */
-static int cyl_box_ext_deep(const or_cylbox* c, double thr) {
-    double dl = -thr;
-    if (cb_ext_sep(c, thr, 0)) return 0;
+/* Witnesses: they only prove overlap (a separation needs the candidate directions). */
+static int cb_proj_box(const or_cylbox* c, const double* e, const double* x, double* y) {
+    double d[3] = {x[0] - c->T[0], x[1] - c->T[1], x[2] - c->T[2]}, l[3];
+    int in = 1;
+    for (int k = 0; k < 3; ++k) {
+        double t = dot3(c->B[k], d);
+        if (!(t < e[k] && t > -e[k])) in = 0;
+        l[k] = t > e[k] ? e[k] : (t < -e[k] ? -e[k] : t);
+    }
+    for (int i = 0; i < 3; ++i) y[i] = fma(l[2], c->B[2][i], fma(l[1], c->B[1][i], fma(l[0], c->B[0][i], c->T[i])));
+    return in;
+}
+static int cb_proj_cyl(const or_cylbox* c, double R, double H, const double* x, double* y) {
+    double z = dot3(c->a, x);
+    double r[3] = {x[0] - z * c->a[0], x[1] - z * c->a[1], x[2] - z * c->a[2]};
+    double rr = dot3(r, r);
+    int in = rr < R * R && z < H && z > -H;
+    double zc = z > H ? H : (z < -H ? -H : z);
+    double f = rr > R * R ? R / sqrt(rr) : 1.0;
+    for (int i = 0; i < 3; ++i) y[i] = fma(zc, c->a[i], f * r[i]);
+    return in;
+}
+/* dist < thr (thr >= 0): alternating projections, x on the cylinder strictly inside the box
+   or closer than thr to its projection y on the box */
+static int cb_touch_witness(const or_cylbox* c, double thr) {
+    double x[3], y[3] = {c->T[0], c->T[1], c->T[2]};
+    for (int it = 0; it < 3; ++it) {
+        cb_proj_cyl(c, c->R, c->H, y, x);
+        if (cb_proj_box(c, c->e, x, y)) return 1;
+        double d[3] = {x[0] - y[0], x[1] - y[1], x[2] - y[2]};
+        if (thr > 0.0 && dot3(d, d) < thr * thr) return 1;
+    }
+    return 0;
+}
+/* dist < -dl: a point of the cylinder shrunk by dl strictly inside the box, or of the box
+   shrunk by dl strictly inside the cylinder ((A (-) ball) - B lies in (A - B) (-) ball) */
+static int cb_deep_witness(const or_cylbox* c, double dl) {
+    double x[3], y[3];
     if (c->R > dl && c->H > dl) {
-        or_cylbox s = *c;
-        s.R = c->R - dl; s.H = c->H - dl;
-        if (!cb_base_sep(&s, 0.0) && !cb_ext_sep(&s, 0.0, 0)) return 1;
+        y[0] = c->T[0]; y[1] = c->T[1]; y[2] = c->T[2];
+        for (int it = 0; it < 3; ++it) {
+            cb_proj_cyl(c, c->R - dl, c->H - dl, y, x);
+            if (cb_proj_box(c, c->e, x, y)) return 1;
+        }
     }
     if (c->e[0] > dl && c->e[1] > dl && c->e[2] > dl) {
-        or_cylbox s = *c;
-        s.e[0] = c->e[0] - dl; s.e[1] = c->e[1] - dl; s.e[2] = c->e[2] - dl;
-        if (!cb_base_sep(&s, 0.0) && !cb_ext_sep(&s, 0.0, 0)) return 1;
+        double es[3] = {c->e[0] - dl, c->e[1] - dl, c->e[2] - dl};
+        x[0] = 0.0; x[1] = 0.0; x[2] = 0.0;
+        for (int it = 0; it < 3; ++it) {
+            cb_proj_box(c, es, x, y);
+            if (cb_proj_cyl(c, c->R, c->H, y, x)) return 1;
+        }
     }
-    return !cb_ext_sep(c, thr, 1);
+    return 0;
 }
 
-/* cylinder (A) vs box (B): signed distance < thr */
+/* cylinder (A) vs box (B): signed distance < thr; SAT axes, then witnesses, then the
+   remaining candidate directions */
 static int cyl_box_overlap(const double* pa, const double* ma, const double* sz, const double* pb,
                            const double* mb, const double* eb, double thr) {
     or_cylbox c = make_cylbox(pa, ma, sz, pb, mb, eb);
     if (cb_base_sep(&c, thr)) return 0;
-    return thr < 0.0 ? cyl_box_ext_deep(&c, thr) : !cb_ext_sep(&c, thr, 0);
+    if (thr >= 0.0) {
+        if (cb_touch_witness(&c, thr)) return 1;
+        return !cb_ext_sep(&c, thr, 0);
+    }
+    if (cb_deep_witness(&c, -thr)) return 1;
+    return !cb_ext_sep(&c, thr, 1);
 }
 
 /* dispatch; returns contact count, *ndeep deep count, -1 if unsupported */

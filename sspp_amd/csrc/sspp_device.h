@@ -306,12 +306,14 @@ SSPP_HD bool sat_box_box(const double* pa, const double* ma, const double* ea, c
 // contact; MuJoCo's box-box collider reports up to 8).  Restated MuJoCo-style:
 // the SAT axis of least penetration decides; an edge-edge axis (separation above every face
 // axis by more than 1e-12) gives one contact; a face axis makes that face the reference face
-// and the most anti-parallel face of the other box the incident face, which is clipped against
-// the reference face's four side planes (Sutherland-Hodgman, <= 8 points): one contact per
-// clipped point, dist = -(depth below the reference face).  Returns the contacts with
-// dist < -1e-3, at least 1: it is called only when the SAT depth exceeds 1e-3, and no clipped
-// point is deeper than the SAT depth along the reference normal.
-SSPP_HDNI int box_box_deep_count(const double* pa, const double* ma, const double* ea,
+// and the most anti-parallel face of the other box the incident face.  The contacts are the
+// vertices of the incident face clipped to the reference face's rectangle (<= 8), with
+// dist = -(depth below the reference face): every incident edge's clipped segment (Liang-Barsky)
+// gives its entry point and, if it leaves early, its exit point; reference corners strictly
+// inside the incident face are vertices too.  Fixed-size, branch-light, register resident.
+// Returns the contacts with dist < -1e-3, at least 1: it is called only when the SAT depth
+// exceeds 1e-3, and no clipped point is deeper than the SAT depth along the reference normal.
+SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double* ea,
                                                 const double* pb, const double* mb, const double* eb) {
     double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
     for (int j = 0; j < 3; ++j) { col3(ma, j, A[j]); col3(mb, j, Bc[j]); }
@@ -374,45 +376,65 @@ SSPP_HDNI int box_box_deep_count(const double* pa, const double* ma, const doubl
     }
     const double sg = dot3(IA[k], n) > 0.0 ? -eI[k] : eI[k];
     const int k1 = k == 2 ? 0 : k + 1, k2 = k == 0 ? 2 : k - 1;
-    double poly[8][3], tmp[8][3];
-    for (int v = 0; v < 4; ++v) {  // incident face corners, cyclic
+    // incident face corners (cyclic) in the reference face's frame: (u, v) along its two axes,
+    // d = depth below the face
+    const int ta = f == 2 ? 0 : f + 1, tb = f == 0 ? 2 : f - 1;
+    const double off = dot3(pR, n) + eR[f];
+    double cu[4], cv[4], cd[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
         const double c1 = (v == 0 || v == 3) ? eI[k1] : -eI[k1];
         const double c2 = (v < 2) ? eI[k2] : -eI[k2];
-        for (int i = 0; i < 3; ++i)
-            poly[v][i] = fma(c2, IA[k2][i], fma(c1, IA[k1][i], fma(sg, IA[k][i], pI[i])));
+        double P[3], dp[3];
+        for (int i = 0; i < 3; ++i) {
+            P[i] = fma(c2, IA[k2][i], fma(c1, IA[k1][i], fma(sg, IA[k][i], pI[i])));
+            dp[i] = P[i] - pR[i];
+        }
+        cu[v] = dot3(dp, RA[ta]);
+        cv[v] = dot3(dp, RA[tb]);
+        cd[v] = off - dot3(P, n);
     }
-    int np = 4;
-#pragma unroll 1
-    for (int pl = 0; pl < 4 && np > 0; ++pl) {  // side planes of the reference face
-        const int ta = (pl < 2) ? (f == 2 ? 0 : f + 1) : (f == 0 ? 2 : f - 1);
-        const double side = (pl & 1) ? -1.0 : 1.0;
-        double dist_prev = 0.0;
-        int m = 0;
-#pragma unroll 1
-        for (int v = 0; v < np; ++v) {
-            const double* P = poly[v];
-            const double* Q = poly[v + 1 < np ? v + 1 : 0];
-            const double dp[3] = {P[0] - pR[0], P[1] - pR[1], P[2] - pR[2]};
-            const double dq[3] = {Q[0] - pR[0], Q[1] - pR[1], Q[2] - pR[2]};
-            const double hp = side * dot3(dp, RA[ta]) - eR[ta];
-            const double hq = side * dot3(dq, RA[ta]) - eR[ta];
-            (void)dist_prev;
-            if (hp <= 0.0) { for (int i = 0; i < 3; ++i) tmp[m][i] = P[i]; ++m; }
-            if ((hp <= 0.0) != (hq <= 0.0)) {
-                const double w = hp / (hp - hq);
-                for (int i = 0; i < 3; ++i) tmp[m][i] = fma(w, Q[i] - P[i], P[i]);
-                ++m;
+    const double eu = eR[ta], ev = eR[tb];
+    int nd = 0;
+    // the clipped polygon's vertices: each incident edge clipped to the face rectangle
+    // (Liang-Barsky, boundary inclusive) contributes its entry point and, when it leaves the
+    // rectangle early, its exit point ...
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int e2 = (e + 1) & 3;
+        const double du = cu[e2] - cu[e], dv = cv[e2] - cv[e];
+        double t0 = 0.0, t1 = 1.0;
+        bool ok = true;
+        const double pp[4] = {-du, du, -dv, dv};
+        const double qq[4] = {cu[e] + eu, eu - cu[e], cv[e] + ev, ev - cv[e]};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (pp[c] == 0.0) {
+                if (qq[c] < 0.0) ok = false;
+            } else {
+                const double r = qq[c] / pp[c];
+                if (pp[c] < 0.0) { if (r > t0) t0 = r; }
+                else if (r < t1) t1 = r;
             }
         }
-        np = m;
-        for (int v = 0; v < np; ++v)
-            for (int i = 0; i < 3; ++i) poly[v][i] = tmp[v][i];
+        if (ok && t0 <= t1) {
+            const double dd = cd[e2] - cd[e];
+            if (-fma(t0, dd, cd[e]) < kDeep) ++nd;
+            if (t1 < 1.0 && -fma(t1, dd, cd[e]) < kDeep) ++nd;
+        }
     }
-    const double off = dot3(pR, n) + eR[f];
-    int nd = 0;
-    for (int v = 0; v < np; ++v) {
-        const double depth = off - dot3(poly[v], n);
-        if (-depth < kDeep) ++nd;
+    // ... and the face rectangle's corners strictly inside the incident parallelogram
+    const double au = cu[1] - cu[0], av = cv[1] - cv[0], bu = cu[3] - cu[0], bv = cv[3] - cv[0];
+    const double det = au * bv - av * bu;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double qu = (q & 1) ? eu : -eu, qv = (q & 2) ? ev : -ev;
+        const double wu = qu - cu[0], wv = qv - cv[0];
+        const double al = (wu * bv - wv * bu) / det, be = (au * wv - av * wu) / det;
+        if (al > 0.0 && al < 1.0 && be > 0.0 && be < 1.0) {
+            const double d = fma(be, cd[3] - cd[0], fma(al, cd[1] - cd[0], cd[0]));
+            if (-d < kDeep) ++nd;
+        }
     }
     return nd > 0 ? nd : 1;
 }
@@ -589,7 +611,7 @@ SSPP_HDNI bool cb_ell_other(const CylBox& c, const double* u1, const double* u2,
 }
 
 // families (d), (f) and (e); all_roots adds (e)'s non-global critical points
-SSPP_HDNI bool cb_ext_sep(const CylBox& c, double thr, bool all_roots) {
+SSPP_HD bool cb_ext_sep(const CylBox& c, double thr, bool all_roots) {
 #pragma unroll 1
     for (int v = 0; v < 8; ++v) {  // (d), (f): box vertices
         const double s0 = (v & 1) ? c.e[0] : -c.e[0], s1 = (v & 2) ? c.e[1] : -c.e[1],
@@ -651,33 +673,91 @@ SSPP_HDNI bool cb_ext_sep(const CylBox& c, double thr, bool all_roots) {
 }
 
 // dist < thr (thr >= 0: MuJoCo's contact test with margin thr)
-SSPP_HDNI bool cyl_box_ext_touch(const CylBox& c, double thr) { return !cb_ext_sep(c, thr, false); }
+// The same, out of line: kernels that run near their register budget (k_tsp) call this one;
+// the SamplingPathPlanner kernels inline cb_ext_sep (a call there makes the compiler spill the
+// pair loop's SGPRs around it on every iteration).
+SSPP_HDNI bool cb_ext_sep_call(const CylBox& c, double thr, bool all_roots) { return cb_ext_sep(c, thr, all_roots); }
 
-// dist < thr < 0 (thr = -1e-3: a deep contact, Collision.h:93), exact.  Shortcuts: a
-// cylinder shrunk by -thr (or a box shrunk by -thr) that still overlaps the other body proves
-// depth > -thr, since (A (-) ball) - B lies inside (A - B) (-) ball.
-SSPP_HDNI bool cyl_box_ext_deep(const CylBox& c, double thr) {
-    const double dl = -thr;
-    if (cb_ext_sep(c, thr, false)) return false;
+// Witnesses (they only prove overlap; a separation always needs the candidate directions).
+// Nearest point of the box to x, and whether x lies strictly inside it.
+SSPP_HD bool cb_proj_box(const CylBox& c, const double* e, const double* x, double* y) {
+    const double d[3] = {x[0] - c.T[0], x[1] - c.T[1], x[2] - c.T[2]};
+    double l[3];
+    bool in = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double t = dot3(c.B[k], d);
+        if (!(t < e[k] && t > -e[k])) in = false;
+        l[k] = t > e[k] ? e[k] : (t < -e[k] ? -e[k] : t);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) y[i] = fma(l[2], c.B[2][i], fma(l[1], c.B[1][i], fma(l[0], c.B[0][i], c.T[i])));
+    return in;
+}
+// Nearest point of the cylinder (radius R, half height H, at the origin) to x, and whether x
+// lies strictly inside it.
+SSPP_HD bool cb_proj_cyl(const CylBox& c, double R, double H, const double* x, double* y) {
+    const double z = dot3(c.a, x);
+    const double r[3] = {x[0] - z * c.a[0], x[1] - z * c.a[1], x[2] - z * c.a[2]};
+    const double rr = dot3(r, r);
+    const bool in = rr < R * R && z < H && z > -H;
+    const double zc = z > H ? H : (z < -H ? -H : z);
+    const double f = rr > R * R ? R / sqrt(rr) : 1.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) y[i] = fma(zc, c.a[i], f * r[i]);
+    return in;
+}
+// dist < thr (thr >= 0) proven by alternating projections: x on the cylinder strictly inside
+// the box (interiors overlap), or x on the cylinder and y on the box closer than thr.
+SSPP_HD bool cb_touch_witness(const CylBox& c, double thr) {
+    double x[3], y[3] = {c.T[0], c.T[1], c.T[2]};
+#pragma unroll 1
+    for (int it = 0; it < 3; ++it) {
+        cb_proj_cyl(c, c.R, c.H, y, x);
+        if (cb_proj_box(c, c.e, x, y)) return true;
+        const double d[3] = {x[0] - y[0], x[1] - y[1], x[2] - y[2]};
+        if (thr > 0.0 && dot3(d, d) < thr * thr) return true;
+    }
+    return false;
+}
+// dist < -dl proven by a point of the cylinder shrunk by dl strictly inside the box, or of the
+// box shrunk by dl strictly inside the cylinder: (A (-) ball) - B lies in (A - B) (-) ball.
+SSPP_HD bool cb_deep_witness(const CylBox& c, double dl) {
+    double x[3], y[3];
     if (c.R > dl && c.H > dl) {
-        CylBox s = c;
-        s.R = c.R - dl; s.H = c.H - dl;
-        if (!cb_base_sep(s, 0.0) && !cb_ext_sep(s, 0.0, false)) return true;
+        y[0] = c.T[0]; y[1] = c.T[1]; y[2] = c.T[2];
+#pragma unroll 1
+        for (int it = 0; it < 3; ++it) {
+            cb_proj_cyl(c, c.R - dl, c.H - dl, y, x);
+            if (cb_proj_box(c, c.e, x, y)) return true;
+        }
     }
     if (c.e[0] > dl && c.e[1] > dl && c.e[2] > dl) {
-        CylBox s = c;
-        s.e[0] = c.e[0] - dl; s.e[1] = c.e[1] - dl; s.e[2] = c.e[2] - dl;
-        if (!cb_base_sep(s, 0.0) && !cb_ext_sep(s, 0.0, false)) return true;
+        const double es[3] = {c.e[0] - dl, c.e[1] - dl, c.e[2] - dl};
+        x[0] = 0.0; x[1] = 0.0; x[2] = 0.0;
+#pragma unroll 1
+        for (int it = 0; it < 3; ++it) {
+            cb_proj_box(c, es, x, y);
+            if (cb_proj_cyl(c, c.R, c.H, y, x)) return true;
+        }
     }
-    return !cb_ext_sep(c, thr, true);
+    return false;
 }
 
-// cylinder (A) vs box (B): signed distance < thr (thr = margin, or kDeep for a deep contact)
+// cylinder (A) vs box (B): signed distance < thr (thr = margin >= 0, or kDeep for a deep
+// contact).  The 7 SAT axes separate most pairs; overlaps are usually proven by a witness;
+// only what neither settles runs the remaining candidate directions (out of line).
+template <bool OUTLINE>
 SSPP_HD bool cyl_box_overlap(const double* pa, const double* ma, const double* sz, const double* pb,
                              const double* mb, const double* eb, double thr) {
     const CylBox c = make_cylbox(pa, ma, sz, pb, mb, eb);
     if (cb_base_sep(c, thr)) return false;
-    return thr < 0.0 ? cyl_box_ext_deep(c, thr) : cyl_box_ext_touch(c, thr);
+    if (thr >= 0.0) {
+        if (cb_touch_witness(c, thr)) return true;
+        return !(OUTLINE ? cb_ext_sep_call(c, thr, false) : cb_ext_sep(c, thr, false));
+    }
+    if (cb_deep_witness(c, -thr)) return true;
+    return !(OUTLINE ? cb_ext_sep_call(c, thr, true) : cb_ext_sep(c, thr, true));
 }
 
 // Supported narrowphase pair? (types ordered t1 <= t2)
@@ -709,13 +789,13 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
     }
     if (t1 == 5) {  // cylinder-box: exact signed distance test, one contact (MuJoCo's convex collider)
         if (NEED_DEEP) {
-            int d = (margin >= kDeep) ? (int)cyl_box_overlap(p1, m1, s1, p2, m2, s2, kDeep)
-                                      : (int)(cyl_box_overlap(p1, m1, s1, p2, m2, s2, margin) &&
-                                              cyl_box_overlap(p1, m1, s1, p2, m2, s2, kDeep));
+            int d = (margin >= kDeep) ? (int)cyl_box_overlap<true>(p1, m1, s1, p2, m2, s2, kDeep)
+                                      : (int)(cyl_box_overlap<true>(p1, m1, s1, p2, m2, s2, margin) &&
+                                              cyl_box_overlap<true>(p1, m1, s1, p2, m2, s2, kDeep));
             *nd = d;
             return d;
         }
-        return cyl_box_overlap(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;
+        return cyl_box_overlap<false>(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;
     }
     // box-box: SAT (exact for boxes) decides contact; the deep count comes from the manifold
     if (NEED_DEEP) {

@@ -101,12 +101,12 @@ Spline spline_through(const std::vector<Point>& pts) {
     return s;
 }
 
-struct GradientStep {  // tsp_types.h:231-235 (unused by the CES-only planner)
+struct GradientStep {  // tsp_types.h:18-23 (unused by the CES-only planner)
     Point x{0, 0, 0, 0};
     double f = 0.0;
 };
 
-struct PathCandidate {  // tsp_types.h:238-247
+struct PathCandidate {  // tsp_types.h:25-34
     ViaSet via;
     py::object refined = py::none();
     std::vector<GradientStep> steps;

@@ -454,9 +454,9 @@ def all_gather_records(out, local, group=None):
     torch = _torch()
     if dist.get_backend(group) == "gloo":
         host = local.cpu()  # waits for the current stream's work on `local`
-        gathered = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_gather_into_tensor(gathered, host, group=group)
-        out.copy_(gathered)
+        parts = [torch.empty_like(host) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(parts, host, group=group)
+        out.copy_(torch.stack(parts).view(out.shape))
         return
     dist.all_gather_into_tensor(out, local, group=group)
 

@@ -320,9 +320,10 @@ def test_config5_multigoal_full_size_each_iteration(cuda):
             np.testing.assert_array_equal(r["status"], stt)
             fin = np.isfinite(cost)
             np.testing.assert_array_equal(np.isfinite(r["cost"]), fin)
-            assert np.abs(r["cost"][fin] - cost[fin]).max() <= 1e-9
-            for a, b in ((r["L"], L), (r["C_nf"], Cnf), (r["C_wf"], Cwf)):
-                assert np.abs(a - b).max() <= 1e-9
+            # relative 1e-12: colliding gripper candidates sum hundreds of contact terms, and the
+            # device's control points come from the collocation inverse, not a per-candidate QR
+            for a, b in ((r["cost"][fin], cost[fin]), (r["L"], L), (r["C_nf"], Cnf), (r["C_wf"], Cwf)):
+                assert (np.abs(a - b) <= 1e-12 * np.maximum(1.0, np.abs(b))).all()
             m, s, lb, hb, ns, el, bs = O.ces_update(r["cost"], r["status"], r["vias"], m_in, s_in,
                                                     lb_in, hb_in, lo=lo, hi=hi)
             assert r["n_success"] == ns and r["best_slot"] == bs and r["has_best"] == hb

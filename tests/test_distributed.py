@@ -79,3 +79,40 @@ def test_bench_ids_are_disjoint():
         ids = sorted(x for i in range(3) for r in range(world)
                      for x in range((i * world + r) * B, (i * world + r + 1) * B))
         assert ids == list(range(3 * world * B))
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    from sspp_amd.runtime import all_gather_records
+    # bench.py's chunk records [G][4] -> [world][G][4]; CesPlanner's flat slot records
+    rec = torch.arange(12 * 4, dtype=torch.int64).view(12, 4) + 1000 * rank
+    out = torch.empty((world, 12, 4), dtype=torch.int64)
+    all_gather_records(out, rec)
+    flat = torch.arange(10, dtype=torch.float64) + 0.5 * rank
+    fout = torch.empty(10 * world, dtype=torch.float64)
+    all_gather_records(fout, flat)
+    q.put((rank, out.tolist(), fout.tolist()))
+    dist.destroy_process_group()
+
+
+def test_all_gather_records_gloo_layout():
+    """sspp_amd.all_gather_records on a gloo group (the host-staged path) lays the ranks'
+    records out exactly as RCCL's all_gather_into_tensor does: rank-major."""
+    import torch
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = torch.stack([torch.arange(48, dtype=torch.int64).view(12, 4) + 1000 * r for r in range(world)])
+    wantf = torch.cat([torch.arange(10, dtype=torch.float64) + 0.5 * r for r in range(world)])
+    for r in range(world):
+        assert res[r][0] == want.tolist() and res[r][1] == wantf.tolist()
