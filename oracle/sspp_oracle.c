@@ -682,16 +682,16 @@ static int sat_box_box(const double* pa, const double* ma, const double* ea, con
     return 1;
 }
 
-/* Box-box contact manifold for the TaskSpacePlanner cost (include/Collision.h:89-101 adds one
- * term per MuJoCo contact; MuJoCo's box-box collider reports up to 8).  The SAT axis of least
- * penetration decides: an edge-edge axis (separation above every face axis by > 1e-12) gives
- * one contact; a face axis makes that face the reference face and the most anti-parallel face
- * of the other box the incident face.  Contacts = vertices of the incident face clipped to the
- * reference face's rectangle, dist = -(depth below the face): every incident edge's clipped
- * segment (Liang-Barsky) gives its entry point and, if it leaves early, its exit point, and the
- * reference corners strictly inside the incident face are vertices too.  Returns the contacts
- * with dist < -1e-3, at least 1 (called only when the SAT depth exceeds 1e-3; no clipped point
- * is deeper than it).  DESIGN.md §4.                                                          */
+/* Box-box deep contacts for the TaskSpacePlanner cost (include/Collision.h:89-101 adds one
+ * term per MuJoCo contact with dist < -1e-3; MuJoCo's box-box collider reports up to 8).  One
+ * pass: the 15-axis SAT at thr = -1e-3 exactly as sat_box_box (0 = not deep); then an edge-edge
+ * axis separating by more than every face axis + 1e-12 gives one contact; else the face axis of
+ * least penetration is the reference face, the most anti-parallel face of the other box the
+ * incident face, and the contacts are the vertices of the incident face clipped to the
+ * reference rectangle, dist = -(depth below the reference face): each incident edge clipped by
+ * Liang-Barsky (one reciprocal per direction, boundary inclusive) gives its entry point and, if
+ * it leaves early, its exit point; reference corners strictly inside the incident face are
+ * vertices too.  Returns the count with dist < -1e-3, at least 1.  DESIGN.md §4.             */
 static int box_box_deep_count(const double* pa, const double* ma, const double* ea,
                               const double* pb, const double* mb, const double* eb) {
     double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
@@ -701,19 +701,23 @@ static int box_box_deep_count(const double* pa, const double* ma, const double* 
         t[i] = dot3(A[i], T);
         for (int j = 0; j < 3; ++j) { R[i][j] = dot3(A[i], Bc[j]); AR[i][j] = fabs(R[i][j]); }
     }
-    double best_face = -1e300, best_edge = -1e300;
+    double best_face = -1e300;
     int fi = 0;
     for (int i = 0; i < 3; ++i) {
         double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
         double sep = fabs(t[i]) - (ea[i] + rb);
+        if (sep >= DEEP) return 0;
         if (sep > best_face) { best_face = sep; fi = i; }
     }
     for (int j = 0; j < 3; ++j) {
         double pr = fabs(fma(t[2], R[2][j], fma(t[1], R[1][j], t[0] * R[0][j])));
         double ra = fma(ea[2], AR[2][j], fma(ea[1], AR[1][j], ea[0] * AR[0][j]));
         double sep = pr - (ra + eb[j]);
+        if (sep >= DEEP) return 0;
         if (sep > best_face) { best_face = sep; fi = 3 + j; }
     }
+    int edge = 0;
+    double fthr = best_face + 1e-12;
     for (int i = 0; i < 3; ++i) {
         for (int j = 0; j < 3; ++j) {
             double v[3] = {R[0][j], R[1][j], R[2][j]}, L[3];
@@ -729,11 +733,12 @@ static int box_box_deep_count(const double* pa, const double* ma, const double* 
                 double bk[3] = {R[0][k], R[1][k], R[2][k]};
                 rb = fma(eb[k], fabs(dot3(bk, L)), rb);
             }
-            double sep = (pr - (ra + rb)) / sqrt(len2);
-            if (sep > best_edge) best_edge = sep;
+            double num = pr - (ra + rb), len = sqrt(len2);
+            if (num >= DEEP * len) return 0;
+            edge = edge || num > fthr * len;
         }
     }
-    if (best_edge > best_face + 1e-12) return 1;
+    if (edge) return 1;
     int refA = fi < 3, f = refA ? fi : fi - 3;
     const double *pR = refA ? pa : pb, *pI = refA ? pb : pa;
     const double *eR = refA ? ea : eb, *eI = refA ? eb : ea;
@@ -744,14 +749,11 @@ static int box_box_deep_count(const double* pa, const double* ma, const double* 
     double dRI[3] = {pI[0] - pR[0], pI[1] - pR[1], pI[2] - pR[2]};
     if (dot3(dRI, n) < 0.0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
     int k = 0;
-    double kb = -1.0;
-    for (int kk = 0; kk < 3; ++kk) {
-        double v = fabs(dot3(IA[kk], n));
-        if (v > kb) { kb = v; k = kk; }
-    }
+    double kb = fabs(dot3(IA[0], n));
+    { double v = fabs(dot3(IA[1], n)); if (v > kb) { kb = v; k = 1; } }
+    { double v = fabs(dot3(IA[2], n)); if (v > kb) { kb = v; k = 2; } }
     double sg = dot3(IA[k], n) > 0.0 ? -eI[k] : eI[k];
     int k1 = k == 2 ? 0 : k + 1, k2 = k == 0 ? 2 : k - 1;
-    /* incident corners in the reference face frame: (u, v) along its axes, d = depth */
     int ta = f == 2 ? 0 : f + 1, tb = f == 0 ? 2 : f - 1;
     double off = dot3(pR, n) + eR[f];
     double cu[4], cv[4], cd[4];
@@ -769,23 +771,28 @@ static int box_box_deep_count(const double* pa, const double* ma, const double* 
     }
     double eu = eR[ta], ev = eR[tb];
     int nd = 0;
-    /* each incident edge clipped to the face rectangle (Liang-Barsky, boundary inclusive):
-       its entry point, and its exit point when it leaves early */
     for (int e = 0; e < 4; ++e) {
         int e2 = (e + 1) & 3;
         double du = cu[e2] - cu[e], dv = cv[e2] - cv[e];
         double t0 = 0.0, t1 = 1.0;
         int ok = 1;
-        double pp[4] = {-du, du, -dv, dv};
-        double qq[4] = {cu[e] + eu, eu - cu[e], cv[e] + ev, ev - cv[e]};
-        for (int c = 0; c < 4; ++c) {
-            if (pp[c] == 0.0) {
-                if (qq[c] < 0.0) ok = 0;
-            } else {
-                double r = qq[c] / pp[c];
-                if (pp[c] < 0.0) { if (r > t0) t0 = r; }
-                else if (r < t1) t1 = r;
-            }
+        if (du == 0.0) {
+            ok = ok && !(cu[e] + eu < 0.0) && !(eu - cu[e] < 0.0);
+        } else {
+            double r = 1.0 / du;
+            double a0 = -(cu[e] + eu) * r, a1 = (eu - cu[e]) * r;
+            double lo = du > 0.0 ? a0 : a1, hi = du > 0.0 ? a1 : a0;
+            if (lo > t0) t0 = lo;
+            if (hi < t1) t1 = hi;
+        }
+        if (dv == 0.0) {
+            ok = ok && !(cv[e] + ev < 0.0) && !(ev - cv[e] < 0.0);
+        } else {
+            double r = 1.0 / dv;
+            double b0 = -(cv[e] + ev) * r, b1 = (ev - cv[e]) * r;
+            double lo = dv > 0.0 ? b0 : b1, hi = dv > 0.0 ? b1 : b0;
+            if (lo > t0) t0 = lo;
+            if (hi < t1) t1 = hi;
         }
         if (ok && t0 <= t1) {
             double dd = cd[e2] - cd[e];
@@ -793,13 +800,12 @@ static int box_box_deep_count(const double* pa, const double* ma, const double* 
             if (t1 < 1.0 && -fma(t1, dd, cd[e]) < DEEP) ++nd;
         }
     }
-    /* face rectangle corners strictly inside the incident parallelogram */
     double au = cu[1] - cu[0], av = cv[1] - cv[0], bu = cu[3] - cu[0], bv = cv[3] - cv[0];
-    double det = au * bv - av * bu;
+    double idet = 1.0 / (au * bv - av * bu);
     for (int q = 0; q < 4; ++q) {
         double qu = (q & 1) ? eu : -eu, qv = (q & 2) ? ev : -ev;
         double wu = qu - cu[0], wv = qv - cv[0];
-        double al = (wu * bv - wv * bu) / det, be = (au * wv - av * wu) / det;
+        double al = (wu * bv - wv * bu) * idet, be = (au * wv - av * wu) * idet;
         if (al > 0.0 && al < 1.0 && be > 0.0 && be < 1.0) {
             double d = fma(be, cd[3] - cd[0], fma(al, cd[1] - cd[0], cd[0]));
             if (-d < DEEP) ++nd;
@@ -867,14 +873,21 @@ static double ell_F(double r0, double z0, double z1, double s) {
     double t0 = (r0 * z0) / (s + r0), t1 = z1 / (s + 1.0);
     return fma(t1, t1, t0 * t0) - 1.0;
 }
+/* root of F on (lo, hi), sign(F(lo)) = sgn_lo, F convex + monotone: safeguarded Newton */
 static double ell_bisect(double r0, double z0, double z1, double lo, double hi, double sgn_lo) {
-    double s = lo;
-    for (int i = 0; i < 256; ++i) {
-        s = 0.5 * (lo + hi);
-        if (s == lo || s == hi) break;
-        double g = ell_F(r0, z0, z1, s);
-        if (g == 0.0) break;
-        if ((g > 0.0) == (sgn_lo > 0.0)) lo = s; else hi = s;
+    double n0 = r0 * z0;
+    double s = 0.5 * (lo + hi);
+    for (int i = 0; i < 48; ++i) {
+        double a0 = s + r0, a1 = s + 1.0;
+        double t0 = n0 / a0, t1 = z1 / a1;
+        double f = fma(t1, t1, t0 * t0) - 1.0;
+        if (f == 0.0) break;
+        if ((f > 0.0) == (sgn_lo > 0.0)) lo = s; else hi = s;
+        double fp = -2.0 * ((t0 * t0) / a0 + (t1 * t1) / a1);
+        double sn = s - f / fp;
+        if (!(sn > lo && sn < hi)) sn = 0.5 * (lo + hi);
+        if (sn == s) break;
+        s = sn;
     }
     return s;
 }
@@ -937,13 +950,18 @@ static int cb_ell_other(const or_cylbox* c, const double* u1, const double* u2, 
         return 0;
     }
     double z0 = y0 / e0, z1 = y1 / e1, q = e0 / e1, r0 = q * q, n0 = r0 * z0;
-    double lo = -r0, hi = -1.0, s = lo;
-    for (int i = 0; i < 256; ++i) {
-        s = 0.5 * (lo + hi);
-        if (s == lo || s == hi) break;
+    double lo = -r0, hi = -1.0, s = 0.5 * (lo + hi);
+    for (int i = 0; i < 48; ++i) {
         double a0 = s + r0, a1 = s + 1.0;
-        double D = (n0 * n0) / (a0 * a0 * a0) + (z1 * z1) / (a1 * a1 * a1);
-        if (D > 0.0) lo = s; else if (D < 0.0) hi = s; else break;
+        double q0 = (n0 * n0) / (a0 * a0 * a0), q1 = (z1 * z1) / (a1 * a1 * a1);
+        double D = q0 + q1;
+        if (D == 0.0) break;
+        if (D > 0.0) lo = s; else hi = s;
+        double Dp = -3.0 * (q0 / a0 + q1 / a1);
+        double sn = s - D / Dp;
+        if (!(sn > lo && sn < hi)) sn = 0.5 * (lo + hi);
+        if (sn == s) break;
+        s = sn;
     }
     if (!(ell_F(r0, z0, z1, s) < 0.0)) return 0;
     double ss[2];
@@ -1065,18 +1083,29 @@ static int cb_deep_witness(const or_cylbox* c, double dl) {
     return 0;
 }
 
+/* the candidate search runs in the box's frame (box axes = identity), as on the device */
+static or_cylbox cb_box_frame(const or_cylbox* c) {
+    or_cylbox b;
+    for (int k = 0; k < 3; ++k) {
+        b.T[k] = dot3(c->B[k], c->T);
+        b.a[k] = dot3(c->B[k], c->a);
+        b.e[k] = c->e[k];
+        for (int i = 0; i < 3; ++i) b.B[k][i] = k == i ? 1.0 : 0.0;
+    }
+    b.R = c->R; b.H = c->H;
+    return b;
+}
+
 /* cylinder (A) vs box (B): signed distance < thr; SAT axes, then witnesses, then the
    remaining candidate directions */
 static int cyl_box_overlap(const double* pa, const double* ma, const double* sz, const double* pb,
                            const double* mb, const double* eb, double thr) {
     or_cylbox c = make_cylbox(pa, ma, sz, pb, mb, eb);
     if (cb_base_sep(&c, thr)) return 0;
-    if (thr >= 0.0) {
-        if (cb_touch_witness(&c, thr)) return 1;
-        return !cb_ext_sep(&c, thr, 0);
-    }
-    if (cb_deep_witness(&c, -thr)) return 1;
-    return !cb_ext_sep(&c, thr, 1);
+    int deep = thr < 0.0;
+    if (deep ? cb_deep_witness(&c, -thr) : cb_touch_witness(&c, thr)) return 1;
+    or_cylbox b = cb_box_frame(&c);
+    return !cb_ext_sep(&b, thr, deep);
 }
 
 /* dispatch; returns contact count, *ndeep deep count, -1 if unsupported */
@@ -1112,7 +1141,7 @@ static int collide(int t1, const double* p1, const double* m1, const double* s1,
     if (t1 == OR_GEOM_BOX && t2 == OR_GEOM_BOX) { /* SAT decides; deep count from the manifold */
         int c = sat_box_box(p1, m1, s1, p2, m2, s2, margin);
         if (!c) return 0;
-        *ndeep = sat_box_box(p1, m1, s1, p2, m2, s2, DEEP) ? box_box_deep_count(p1, m1, s1, p2, m2, s2) : 0;
+        *ndeep = box_box_deep_count(p1, m1, s1, p2, m2, s2); /* 0 unless deep (its SAT pass) */
         return 1;
     }
     return -1;

@@ -146,10 +146,6 @@ SSPP_HD void basis_funcs(double u, int p, int span, const double* knots, double*
     }
 }
 
-// rare, register-hungry narrowphase paths stay out of line so they do not raise the VGPR
-// count (and so lower the occupancy) of the kernels' hot pair loops
-#define SSPP_HDNI __host__ __device__ inline __attribute__((noinline))
-
 // ---------------------------------------------------------------- narrowphase
 // Each returns the contact count (dist < margin); *nd = contacts with dist < -1e-3.
 SSPP_HD int col_plane_box(const double* pp, const double* pm, const double* bp, const double* bm,
@@ -302,40 +298,54 @@ SSPP_HD bool sat_box_box(const double* pa, const double* ma, const double* ea, c
     return true;
 }
 
-// Box-box contact manifold (TaskSpacePlanner cost, Collision.h:89-101 adds one term per
-// contact; MuJoCo's box-box collider reports up to 8).  Restated MuJoCo-style:
-// the SAT axis of least penetration decides; an edge-edge axis (separation above every face
-// axis by more than 1e-12) gives one contact; a face axis makes that face the reference face
-// and the most anti-parallel face of the other box the incident face.  The contacts are the
-// vertices of the incident face clipped to the reference face's rectangle (<= 8), with
-// dist = -(depth below the reference face): every incident edge's clipped segment (Liang-Barsky)
-// gives its entry point and, if it leaves early, its exit point; reference corners strictly
-// inside the incident face are vertices too.  Fixed-size, branch-light, register resident.
-// Returns the contacts with dist < -1e-3, at least 1: it is called only when the SAT depth
-// exceeds 1e-3, and no clipped point is deeper than the SAT depth along the reference normal.
+// Box-box deep contacts (TaskSpacePlanner cost: Collision.h:89-101 adds one term per contact
+// with dist < -1e-3, and MuJoCo's box-box collider reports up to 8).  One pass:
+// * the 15-axis SAT at thr = -1e-3 exactly as sat_box_box (returns 0 at the first axis whose
+//   separation reaches it: not deep);
+// * otherwise MuJoCo-style: an edge-edge axis whose separation exceeds every face
+//   axis's by more than 1e-12 gives one contact; else the face axis of least penetration makes
+//   that face the reference face and the most anti-parallel face of the other box the incident
+//   face, and the contacts are the vertices of the incident face clipped to the reference face's
+//   rectangle (<= 8), dist = -(depth below the reference face): every incident edge's clipped
+//   segment (Liang-Barsky, boundary inclusive) gives its entry point and, if it leaves early,
+//   its exit point; reference corners strictly inside the incident face are vertices too.
+// Returns the number of those with dist < -1e-3, at least 1 (no clipped point is deeper than the
+// SAT depth).  Every array is indexed with compile-time indices (run-time choices are selects),
+// so everything stays in registers.
 SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double* ea,
-                                                const double* pb, const double* mb, const double* eb) {
+                               const double* pb, const double* mb, const double* eb) {
     double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
+#pragma unroll
     for (int j = 0; j < 3; ++j) { col3(ma, j, A[j]); col3(mb, j, Bc[j]); }
     T[0] = pb[0] - pa[0]; T[1] = pb[1] - pa[1]; T[2] = pb[2] - pa[2];
+#pragma unroll
     for (int i = 0; i < 3; ++i) {
         t[i] = dot3(A[i], T);
+#pragma unroll
         for (int j = 0; j < 3; ++j) { R[i][j] = dot3(A[i], Bc[j]); AR[i][j] = fabs(R[i][j]); }
     }
-    double best_face = -1e300, best_edge = -1e300;
+    double best_face = -1e300;
     int fi = 0;
+#pragma unroll
     for (int i = 0; i < 3; ++i) {  // faces of A
         const double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
         const double sep = fabs(t[i]) - (ea[i] + rb);
+        if (sep >= kDeep) return 0;
         if (sep > best_face) { best_face = sep; fi = i; }
     }
+#pragma unroll
     for (int j = 0; j < 3; ++j) {  // faces of B
         const double pr = fabs(fma(t[2], R[2][j], fma(t[1], R[1][j], t[0] * R[0][j])));
         const double ra = fma(ea[2], AR[2][j], fma(ea[1], AR[1][j], ea[0] * AR[0][j]));
         const double sep = pr - (ra + eb[j]);
+        if (sep >= kDeep) return 0;
         if (sep > best_face) { best_face = sep; fi = 3 + j; }
     }
+    bool edge = false;  // some edge axis separates by more than best_face + 1e-12
+    const double fthr = best_face + 1e-12;
+#pragma unroll
     for (int i = 0; i < 3; ++i) {  // edge x edge
+#pragma unroll
         for (int j = 0; j < 3; ++j) {
             const double v0 = R[0][j], v1 = R[1][j], v2 = R[2][j];
             double L[3];
@@ -347,75 +357,97 @@ SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double*
             const double pr = fabs(dot3(t, L));
             const double ra = fma(ea[2], fabs(L[2]), fma(ea[1], fabs(L[1]), ea[0] * fabs(L[0])));
             double rb = 0.0;
+#pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const double bk[3] = {R[0][k], R[1][k], R[2][k]};
                 rb = fma(eb[k], fabs(dot3(bk, L)), rb);
             }
-            const double sep = (pr - (ra + rb)) / sqrt(len2);
-            if (sep > best_edge) best_edge = sep;
+            const double num = pr - (ra + rb), len = sqrt(len2);
+            if (num >= kDeep * len) return 0;
+            edge = edge || num > fthr * len;
         }
     }
-    if (best_edge > best_face + 1e-12) return 1;
+    if (edge) return 1;
+    auto pick3 = [](int i, double x0, double x1, double x2) { return i == 0 ? x0 : (i == 1 ? x1 : x2); };
     const bool refA = fi < 3;
     const int f = refA ? fi : fi - 3;
-    const double* pR = refA ? pa : pb;
-    const double* pI = refA ? pb : pa;
-    const double* eR = refA ? ea : eb;
-    const double* eI = refA ? eb : ea;
-    double RA[3][3], IA[3][3];
-    for (int j = 0; j < 3; ++j)
+    double pR[3], pI[3], eR[3], eI[3], RA[3][3], IA[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        pR[j] = refA ? pa[j] : pb[j]; pI[j] = refA ? pb[j] : pa[j];
+        eR[j] = refA ? ea[j] : eb[j]; eI[j] = refA ? eb[j] : ea[j];
+#pragma unroll
         for (int i = 0; i < 3; ++i) { RA[j][i] = refA ? A[j][i] : Bc[j][i]; IA[j][i] = refA ? Bc[j][i] : A[j][i]; }
-    double n[3] = {RA[f][0], RA[f][1], RA[f][2]};
+    }
+    double n[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) n[c] = pick3(f, RA[0][c], RA[1][c], RA[2][c]);
     const double dRI[3] = {pI[0] - pR[0], pI[1] - pR[1], pI[2] - pR[2]};
     if (dot3(dRI, n) < 0.0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+    // incident face: the first most anti-parallel face normal of the other box
     int k = 0;
-    double kb = -1.0;
-    for (int kk = 0; kk < 3; ++kk) {
-        const double v = fabs(dot3(IA[kk], n));
-        if (v > kb) { kb = v; k = kk; }
-    }
-    const double sg = dot3(IA[k], n) > 0.0 ? -eI[k] : eI[k];
+    double kb = fabs(dot3(IA[0], n));
+    { const double v = fabs(dot3(IA[1], n)); if (v > kb) { kb = v; k = 1; } }
+    { const double v = fabs(dot3(IA[2], n)); if (v > kb) { kb = v; k = 2; } }
     const int k1 = k == 2 ? 0 : k + 1, k2 = k == 0 ? 2 : k - 1;
+    const int ta = f == 2 ? 0 : f + 1, tb = f == 0 ? 2 : f - 1;
+    double Ik[3], Ik1[3], Ik2[3], Ta[3], Tb[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        Ik[c] = pick3(k, IA[0][c], IA[1][c], IA[2][c]);
+        Ik1[c] = pick3(k1, IA[0][c], IA[1][c], IA[2][c]);
+        Ik2[c] = pick3(k2, IA[0][c], IA[1][c], IA[2][c]);
+        Ta[c] = pick3(ta, RA[0][c], RA[1][c], RA[2][c]);
+        Tb[c] = pick3(tb, RA[0][c], RA[1][c], RA[2][c]);
+    }
+    const double eIk = pick3(k, eI[0], eI[1], eI[2]), eIk1 = pick3(k1, eI[0], eI[1], eI[2]),
+                 eIk2 = pick3(k2, eI[0], eI[1], eI[2]);
+    const double sg = dot3(Ik, n) > 0.0 ? -eIk : eIk;
     // incident face corners (cyclic) in the reference face's frame: (u, v) along its two axes,
     // d = depth below the face
-    const int ta = f == 2 ? 0 : f + 1, tb = f == 0 ? 2 : f - 1;
-    const double off = dot3(pR, n) + eR[f];
+    const double off = dot3(pR, n) + pick3(f, eR[0], eR[1], eR[2]);
     double cu[4], cv[4], cd[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-        const double c1 = (v == 0 || v == 3) ? eI[k1] : -eI[k1];
-        const double c2 = (v < 2) ? eI[k2] : -eI[k2];
+        const double c1 = (v == 0 || v == 3) ? eIk1 : -eIk1;
+        const double c2 = (v < 2) ? eIk2 : -eIk2;
         double P[3], dp[3];
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
-            P[i] = fma(c2, IA[k2][i], fma(c1, IA[k1][i], fma(sg, IA[k][i], pI[i])));
+            P[i] = fma(c2, Ik2[i], fma(c1, Ik1[i], fma(sg, Ik[i], pI[i])));
             dp[i] = P[i] - pR[i];
         }
-        cu[v] = dot3(dp, RA[ta]);
-        cv[v] = dot3(dp, RA[tb]);
+        cu[v] = dot3(dp, Ta);
+        cv[v] = dot3(dp, Tb);
         cd[v] = off - dot3(P, n);
     }
-    const double eu = eR[ta], ev = eR[tb];
+    const double eu = pick3(ta, eR[0], eR[1], eR[2]), ev = pick3(tb, eR[0], eR[1], eR[2]);
     int nd = 0;
-    // the clipped polygon's vertices: each incident edge clipped to the face rectangle
-    // (Liang-Barsky, boundary inclusive) contributes its entry point and, when it leaves the
-    // rectangle early, its exit point ...
+    // each incident edge clipped to the rectangle |u| <= eu, |v| <= ev (Liang-Barsky with one
+    // reciprocal per direction): its entry point, and its exit point when it leaves early
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int e2 = (e + 1) & 3;
         const double du = cu[e2] - cu[e], dv = cv[e2] - cv[e];
         double t0 = 0.0, t1 = 1.0;
         bool ok = true;
-        const double pp[4] = {-du, du, -dv, dv};
-        const double qq[4] = {cu[e] + eu, eu - cu[e], cv[e] + ev, ev - cv[e]};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (pp[c] == 0.0) {
-                if (qq[c] < 0.0) ok = false;
-            } else {
-                const double r = qq[c] / pp[c];
-                if (pp[c] < 0.0) { if (r > t0) t0 = r; }
-                else if (r < t1) t1 = r;
-            }
+        if (du == 0.0) {
+            ok = ok && !(cu[e] + eu < 0.0) && !(eu - cu[e] < 0.0);
+        } else {
+            const double r = 1.0 / du;
+            const double ta0 = -(cu[e] + eu) * r, ta1 = (eu - cu[e]) * r;  // u = -eu, u = eu
+            const double lo = du > 0.0 ? ta0 : ta1, hi = du > 0.0 ? ta1 : ta0;
+            if (lo > t0) t0 = lo;
+            if (hi < t1) t1 = hi;
+        }
+        if (dv == 0.0) {
+            ok = ok && !(cv[e] + ev < 0.0) && !(ev - cv[e] < 0.0);
+        } else {
+            const double r = 1.0 / dv;
+            const double tb0 = -(cv[e] + ev) * r, tb1 = (ev - cv[e]) * r;
+            const double lo = dv > 0.0 ? tb0 : tb1, hi = dv > 0.0 ? tb1 : tb0;
+            if (lo > t0) t0 = lo;
+            if (hi < t1) t1 = hi;
         }
         if (ok && t0 <= t1) {
             const double dd = cd[e2] - cd[e];
@@ -423,14 +455,14 @@ SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double*
             if (t1 < 1.0 && -fma(t1, dd, cd[e]) < kDeep) ++nd;
         }
     }
-    // ... and the face rectangle's corners strictly inside the incident parallelogram
+    // ... and the rectangle's corners strictly inside the incident parallelogram
     const double au = cu[1] - cu[0], av = cv[1] - cv[0], bu = cu[3] - cu[0], bv = cv[3] - cv[0];
-    const double det = au * bv - av * bu;
+    const double idet = 1.0 / (au * bv - av * bu);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const double qu = (q & 1) ? eu : -eu, qv = (q & 2) ? ev : -ev;
         const double wu = qu - cu[0], wv = qv - cv[0];
-        const double al = (wu * bv - wv * bu) / det, be = (au * wv - av * wu) / det;
+        const double al = (wu * bv - wv * bu) * idet, be = (au * wv - av * wu) * idet;
         if (al > 0.0 && al < 1.0 && be > 0.0 && be < 1.0) {
             const double d = fma(be, cd[3] - cd[0], fma(al, cd[1] - cd[0], cd[0]));
             if (-d < kDeep) ++nd;
@@ -512,20 +544,28 @@ SSPP_HD double ell_F(double r0, double z0, double z1, double s) {
     const double t0 = (r0 * z0) / (s + r0), t1 = z1 / (s + 1.0);
     return fma(t1, t1, t0 * t0) - 1.0;
 }
-// bisection for the root of F on (lo, hi) with sign(F(lo)) = sgn_lo (midpoint until it hits an end)
+// Root of F on (lo, hi) with sign(F(lo)) = sgn_lo, F convex and monotone there: Newton steps
+// safeguarded by the shrinking bracket (bisection whenever a step leaves it), <= 48 iterations.
 SSPP_HD double ell_bisect(double r0, double z0, double z1, double lo, double hi, double sgn_lo) {
-    double s = lo;
-    for (int i = 0; i < 256; ++i) {
-        s = 0.5 * (lo + hi);
-        if (s == lo || s == hi) break;
-        const double g = ell_F(r0, z0, z1, s);
-        if (g == 0.0) break;
-        if ((g > 0.0) == (sgn_lo > 0.0)) lo = s; else hi = s;
+    const double n0 = r0 * z0;
+    double s = 0.5 * (lo + hi);
+#pragma unroll 1
+    for (int i = 0; i < 48; ++i) {
+        const double a0 = s + r0, a1 = s + 1.0;
+        const double t0 = n0 / a0, t1 = z1 / a1;
+        const double f = fma(t1, t1, t0 * t0) - 1.0;
+        if (f == 0.0) break;
+        if ((f > 0.0) == (sgn_lo > 0.0)) lo = s; else hi = s;
+        const double fp = -2.0 * ((t0 * t0) / a0 + (t1 * t1) / a1);
+        double sn = s - f / fp;
+        if (!(sn > lo && sn < hi)) sn = 0.5 * (lo + hi);
+        if (sn == s) break;
+        s = sn;
     }
     return s;
 }
 // nearest point (x0, x1) of the ellipse x0^2/e0^2 + x1^2/e1^2 = 1 (e0 >= e1 > 0) to (y0, y1) >= 0
-SSPP_HDNI void ellipse_q1(double e0, double e1, double y0, double y1, double* x0, double* x1) {
+SSPP_HD void ellipse_q1(double e0, double e1, double y0, double y1, double* x0, double* x1) {
     if (y1 > 0.0) {
         if (y0 > 0.0) {
             const double z0 = y0 / e0, z1 = y1 / e1;
@@ -565,7 +605,7 @@ SSPP_HD bool cb_ell_axis(const CylBox& c, const double* u1, const double* u2, do
 // The ellipse's other locally-nearest points to p = (px, py) (penetration depth only): the
 // roots of F on (-r0, -1), where F is convex — its minimiser by bisection on F', then one
 // bisection on each side when the minimum is negative; exact-zero coordinates by hand.
-SSPP_HDNI bool cb_ell_other(const CylBox& c, const double* u1, const double* u2, double px, double py,
+SSPP_HD bool cb_ell_other(const CylBox& c, const double* u1, const double* u2, double px, double py,
                           double e0, double e1, double thr) {
     const double y0 = fabs(px), y1 = fabs(py), sx = px < 0.0 ? -1.0 : 1.0, sy = py < 0.0 ? -1.0 : 1.0;
     const double den = e0 * e0 - e1 * e1;
@@ -589,14 +629,21 @@ SSPP_HDNI bool cb_ell_other(const CylBox& c, const double* u1, const double* u2,
         return false;
     }
     const double z0 = y0 / e0, z1 = y1 / e1, q = e0 / e1, r0 = q * q, n0 = r0 * z0;
-    // minimiser of F on (-r0, -1): root of D(s) = n0^2/(s+r0)^3 + z1^2/(s+1)^3 (D < 0 left of it)
-    double lo = -r0, hi = -1.0, s = lo;
-    for (int i = 0; i < 256; ++i) {
-        s = 0.5 * (lo + hi);
-        if (s == lo || s == hi) break;
+    // minimiser of F on (-r0, -1): root of the decreasing D(s) = n0^2/(s+r0)^3 + z1^2/(s+1)^3,
+    // safeguarded Newton as in ell_bisect
+    double lo = -r0, hi = -1.0, s = 0.5 * (lo + hi);
+#pragma unroll 1
+    for (int i = 0; i < 48; ++i) {
         const double a0 = s + r0, a1 = s + 1.0;
-        const double D = (n0 * n0) / (a0 * a0 * a0) + (z1 * z1) / (a1 * a1 * a1);
-        if (D > 0.0) lo = s; else if (D < 0.0) hi = s; else break;
+        const double q0 = (n0 * n0) / (a0 * a0 * a0), q1 = (z1 * z1) / (a1 * a1 * a1);
+        const double D = q0 + q1;
+        if (D == 0.0) break;
+        if (D > 0.0) lo = s; else hi = s;
+        const double Dp = -3.0 * (q0 / a0 + q1 / a1);
+        double sn = s - D / Dp;
+        if (!(sn > lo && sn < hi)) sn = 0.5 * (lo + hi);
+        if (sn == s) break;
+        s = sn;
     }
     if (!(ell_F(r0, z0, z1, s) < 0.0)) return false;
     const double sa = ell_bisect(r0, z0, z1, -r0, s, 1.0);
@@ -633,8 +680,8 @@ SSPP_HD bool cb_ext_sep(const CylBox& c, double thr, bool all_roots) {
             if (cb_sep(c, L, thr)) return true;
         }
     }
-#pragma unroll 1
-    for (int j = 0; j < 3; ++j) {  // (e): rim circles vs box edges along b_j
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // (e): rim circles vs box edges along b_j (unrolled: static indices)
         const double* e = c.B[j];
         double u1[3] = {c.a[1] * e[2] - c.a[2] * e[1], c.a[2] * e[0] - c.a[0] * e[2], c.a[0] * e[1] - c.a[1] * e[0]};
         const double S2 = dot3(u1, u1);
@@ -673,11 +720,6 @@ SSPP_HD bool cb_ext_sep(const CylBox& c, double thr, bool all_roots) {
 }
 
 // dist < thr (thr >= 0: MuJoCo's contact test with margin thr)
-// The same, out of line: kernels that run near their register budget (k_tsp) call this one;
-// the SamplingPathPlanner kernels inline cb_ext_sep (a call there makes the compiler spill the
-// pair loop's SGPRs around it on every iteration).
-SSPP_HDNI bool cb_ext_sep_call(const CylBox& c, double thr, bool all_roots) { return cb_ext_sep(c, thr, all_roots); }
-
 // Witnesses (they only prove overlap; a separation always needs the candidate directions).
 // Nearest point of the box to x, and whether x lies strictly inside it.
 SSPP_HD bool cb_proj_box(const CylBox& c, const double* e, const double* x, double* y) {
@@ -744,20 +786,60 @@ SSPP_HD bool cb_deep_witness(const CylBox& c, double dl) {
     return false;
 }
 
+// The candidate-direction search in the box's frame (box axes = identity): the cylinder-box pair
+// then travels as 12 doubles, which fit the argument registers of an out-of-line call.
+SSPP_HD CylBox cb_box_frame(const CylBox& c) {
+    CylBox b;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        b.T[k] = dot3(c.B[k], c.T);
+        b.a[k] = dot3(c.B[k], c.a);
+        b.e[k] = c.e[k];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) b.B[k][i] = k == i ? 1.0 : 0.0;
+    }
+    b.R = c.R; b.H = c.H;
+    return b;
+}
+SSPP_HD bool cb_ext_sep_boxframe(double T0, double T1, double T2, double a0, double a1, double a2,
+                                 double e0, double e1, double e2, double R, double H, double thr,
+                                 bool all_roots) {
+    CylBox b;
+    b.T[0] = T0; b.T[1] = T1; b.T[2] = T2;
+    b.a[0] = a0; b.a[1] = a1; b.a[2] = a2;
+    b.e[0] = e0; b.e[1] = e1; b.e[2] = e2;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) b.B[k][i] = k == i ? 1.0 : 0.0;
+    b.R = R; b.H = H;
+    return cb_ext_sep(b, thr, all_roots);
+}
+// Out of line, for kernels at their register budget (k_tsp): the call happens only for pairs the
+// SAT axes and the witnesses leave undecided.
+__host__ __device__ inline __attribute__((noinline)) bool cb_ext_sep_call(
+    double T0, double T1, double T2, double a0, double a1, double a2, double e0, double e1,
+    double e2, double R, double H, double thr, bool all_roots) {
+    return cb_ext_sep_boxframe(T0, T1, T2, a0, a1, a2, e0, e1, e2, R, H, thr, all_roots);
+}
+
 // cylinder (A) vs box (B): signed distance < thr (thr = margin >= 0, or kDeep for a deep
 // contact).  The 7 SAT axes separate most pairs; overlaps are usually proven by a witness;
-// only what neither settles runs the remaining candidate directions (out of line).
+// only what neither settles runs the remaining candidate directions (in the box's frame;
+// OUTLINE: as a call).
 template <bool OUTLINE>
 SSPP_HD bool cyl_box_overlap(const double* pa, const double* ma, const double* sz, const double* pb,
                              const double* mb, const double* eb, double thr) {
     const CylBox c = make_cylbox(pa, ma, sz, pb, mb, eb);
     if (cb_base_sep(c, thr)) return false;
-    if (thr >= 0.0) {
-        if (cb_touch_witness(c, thr)) return true;
-        return !(OUTLINE ? cb_ext_sep_call(c, thr, false) : cb_ext_sep(c, thr, false));
-    }
-    if (cb_deep_witness(c, -thr)) return true;
-    return !(OUTLINE ? cb_ext_sep_call(c, thr, true) : cb_ext_sep(c, thr, true));
+    const bool deep = thr < 0.0;
+    if (deep ? cb_deep_witness(c, -thr) : cb_touch_witness(c, thr)) return true;
+    const CylBox b = cb_box_frame(c);
+    if (OUTLINE)
+        return !cb_ext_sep_call(b.T[0], b.T[1], b.T[2], b.a[0], b.a[1], b.a[2], b.e[0], b.e[1], b.e[2],
+                                b.R, b.H, thr, deep);
+    return !cb_ext_sep_boxframe(b.T[0], b.T[1], b.T[2], b.a[0], b.a[1], b.a[2], b.e[0], b.e[1], b.e[2],
+                                b.R, b.H, thr, deep);
 }
 
 // Supported narrowphase pair? (types ordered t1 <= t2)
@@ -771,7 +853,9 @@ SSPP_HD bool pair_supported(int t1, int t2) {
 // Narrowphase dispatch.  Geom 1 must be the first by (type, model index), like the oracle.
 // NEED_DEEP=false: returns the contact count (SamplingPathPlanner feasibility needs > 0).
 // NEED_DEEP=true:  only *nd (contacts with dist < -1e-3, Collision.h cost) is meaningful.
-template <bool NEED_DEEP>
+// CB = false compiles out the cylinder-box code (only for scenes without such pairs); OUTLINE
+// calls the rare cylinder-box candidate search out of line.
+template <bool NEED_DEEP, bool CB = true, bool OUTLINE = false>
 SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1, int t2,
                     const double* p2, const double* m2, const double* s2, double margin, int* nd) {
     *nd = 0;
@@ -788,21 +872,20 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
         return 0;
     }
     if (t1 == 5) {  // cylinder-box: exact signed distance test, one contact (MuJoCo's convex collider)
+        if (!CB) return 0;
         if (NEED_DEEP) {
-            int d = (margin >= kDeep) ? (int)cyl_box_overlap<true>(p1, m1, s1, p2, m2, s2, kDeep)
-                                      : (int)(cyl_box_overlap<true>(p1, m1, s1, p2, m2, s2, margin) &&
-                                              cyl_box_overlap<true>(p1, m1, s1, p2, m2, s2, kDeep));
+            int d = (margin >= kDeep) ? (int)cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, kDeep)
+                                      : (int)(cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, margin) &&
+                                              cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, kDeep));
             *nd = d;
             return d;
         }
-        return cyl_box_overlap<false>(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;
+        return cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;
     }
-    // box-box: SAT (exact for boxes) decides contact; the deep count comes from the manifold
+    // box-box: SAT (exact for boxes) decides contact; deep contacts: one pass, SAT + manifold
     if (NEED_DEEP) {
-        const bool d = (margin >= kDeep) ? sat_box_box(p1, m1, s1, p2, m2, s2, kDeep)
-                                         : (sat_box_box(p1, m1, s1, p2, m2, s2, margin) &&
-                                            sat_box_box(p1, m1, s1, p2, m2, s2, kDeep));
-        *nd = d ? box_box_deep_count(p1, m1, s1, p2, m2, s2) : 0;
+        *nd = (margin >= kDeep || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
+                  ? box_box_deep_count(p1, m1, s1, p2, m2, s2) : 0;
         return *nd;
     }
     return sat_box_box(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;

@@ -42,6 +42,7 @@ struct KScene {
     int onegeom;        // every pair shares one moving geom: its pose is computed once
     int static_block;   // sspp: env-env contacts counted and present -> nothing feasible
     double static_cost; // tsp: Collision.h cost of env-env contacts, added per waypoint
+    int cylbox;         // some moving pair is cylinder-box (selects the kernels that carry that code)
 };
 
 // Scene tables are passed as separate __restrict__ kernel arguments: the pair loop is
@@ -399,7 +400,7 @@ __device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const doub
 //   the other waypoints give), or when *stop (the candidate's LDS flag, cleared by another
 //   wave of the same candidate) reads 0.  Returns 0 when no lane has a contact.
 // DEEP=true : returns 0, *cost = sum over deep contacts of -1/(center_dist + 1e-4) + static.
-template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM>
+template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                              unsigned long long mask, double* cost, int* stop = nullptr) {
     static_assert(!ONEGEOM || NM == 1, "single moving geom implies a single mover");
@@ -458,8 +459,8 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                 have_rot = true;
             }
             const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
-            if (gfirst) nc = collide<DEEP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
-            else nc = collide<DEEP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+            if (gfirst) nc = collide<DEEP, CB, DEEP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+            else nc = collide<DEEP, CB, DEEP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
         }
         if (!DEEP) {
             // the loop trip is wave-uniform, so every active lane reaches this vote
@@ -599,22 +600,26 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
 }
 
 // ---------------------------------------------------------------- candidate sampler
-// sampleWithNoise (include/sspp.h:114-130) for candidate ids first_id + [0, B): one thread per
-// (candidate, Box-Muller pair) over the whole chip; writes the perturbed control-point columns
-// j in [p, n-p) as pert[B][npert] with npert = (n-2p)*D, value = init + (sigma * z) * limits[d].
+// sampleWithNoise (include/sspp.h:114-130) for `steps` batches of B candidates, step s covering
+// ids first_id + s * step_stride + [0, B): one thread per (step, candidate, Box-Muller pair) over
+// the whole chip; writes the perturbed control-point columns j in [p, n-p) as
+// pert[steps][B][npert] with npert = (n-2p)*D, value = init + (sigma * z) * limits[d].
+// A separate launch at full occupancy (26 VGPRs, 8 waves/SIMD): the FP64 log/sqrt/sincospi
+// chains are latency-bound, and in the scoring kernel (3 waves/SIMD) they were 40% of its time.
 __global__ __launch_bounds__(kBlock) void k_sample_sspp(
-    unsigned long long seed, long long first_id, long long B, int D, int p, int npert,
-    double sigma, const double* __restrict__ init_ctrl, const double* __restrict__ limits,
-    double* __restrict__ pert) {
+    unsigned long long seed, long long first_id, long long step_stride, long long B, int steps,
+    int D, int p, int npert, double sigma, const double* __restrict__ init_ctrl,
+    const double* __restrict__ limits, double* __restrict__ pert) {
     const int npairs = (npert + 1) >> 1;
     const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= B * npairs) return;
-    const long long b = t / npairs;
-    const int m = (int)(t - b * npairs);
+    if (t >= (long long)steps * B * npairs) return;
+    const long long sb = t / npairs;
+    const int m = (int)(t - sb * npairs);
+    const long long s = sb / B, b = sb - s * B;
     double z0, z1;
-    normal_pair(seed, (unsigned long long)(first_id + b), (unsigned)m, 0u, &z0, &z1);
+    normal_pair(seed, (unsigned long long)(first_id + s * step_stride + b), (unsigned)m, 0u, &z0, &z1);
     const double* base = init_ctrl + p * D;
-    double* out = pert + b * npert;
+    double* out = pert + sb * npert;
     const int k0 = 2 * m, k1 = 2 * m + 1;
     {
         const double noise = (sigma * z0) * limits[k0 % D];
@@ -935,6 +940,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     if (step) {
         arc += step * a.B;
         feasible += step * a.B;
+        if (pert) pert += step * a.B * ((n - 2 * P) * D);
         if (ctrl_out) ctrl_out += step * a.B * ndof;
         part += step * a.nblk_step;
         sync += step;
@@ -1070,11 +1076,11 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
     const int R = a.npts - a.n1;
     if (collide_on && R > 0 && !(a.ablate & 8)) {
-        if (tid == 0) {
-            int ns = 0;
-            for (int s = 0; s < nvalid; ++s)
-                if (s_feas[s]) s_surv[ns++] = s;
-            s_surv[cpb] = ns;
+        if (tid < 64) {  // survivors compacted by one wave ballot (cpb <= 64), in candidate order
+            const bool f = tid < nvalid && s_feas[tid] != 0;
+            const unsigned long long m = __ballot(f);
+            if (f) s_surv[__popcll(m & ((1ull << tid) - 1ull))] = tid;
+            if (tid == 0) s_surv[cpb] = __popcll(m);
         }
         __syncthreads();
         const int ns = s_surv[cpb];
@@ -1144,11 +1150,11 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     if (!(a.ablate & 4)) {
         __syncthreads();
         int* s_list = s_surv;  // phase 2 is done with it
-        if (tid == 0) {
-            int nl = 0;
-            for (int s = 0; s < nvalid; ++s)
-                if (a.arc_all || s_feas[s]) s_list[nl++] = s;
-            s_list[cpb] = nl;
+        if (tid < 64) {  // one wave ballot, candidate order
+            const bool f = tid < nvalid && (a.arc_all || s_feas[tid] != 0);
+            const unsigned long long m = __ballot(f);
+            if (f) s_list[__popcll(m & ((1ull << tid) - 1ull))] = tid;
+            if (tid == 0) s_list[cpb] = __popcll(m);
         }
         __syncthreads();
         const int nl = s_list[cpb];
@@ -1210,14 +1216,20 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         arc[c] = s_arc[tid];
         feasible[c] = (unsigned char)(s_feas[tid] != 0);
     }
+    // block argmin over the workgroup's feasible candidates: one wave, lexicographic (cost, id)
+    // xor butterfly (exact, order independent: the lowest id wins ties like the serial scan)
     BlockBest bb;
-    if (tid == 0) {
-        bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
-        for (int s = 0; s < nvalid; ++s) {
-            if (!s_feas[s]) continue;
-            bb.count++;
-            if (s_arc[s] < bb.cost) { bb.cost = s_arc[s]; bb.idx = first_id + cand0 + s; }
+    if (tid < 64) {
+        const bool f = tid < nvalid && s_feas[tid] != 0;
+        double bc = f ? s_arc[tid] : INFINITY;
+        long long bi = f ? first_id + cand0 + tid : -1;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double oc = __shfl_xor(bc, off, 64);
+            const long long oi = __shfl_xor(bi, off, 64);
+            if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
         }
+        bb.cost = bi < 0 ? INFINITY : bc; bb.idx = bi; bb.count = __popcll(__ballot(f)); bb.pad = 0;
     }
     finish_batch<NT>(bb, part, sync, best, a.nblk_step, blk);
 }
@@ -1227,7 +1239,9 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
 #ifndef SSPP_TSP_WAVES_PER_EU
 #define SSPP_TSP_WAVES_PER_EU 4
 #endif
-template <int NM, bool ONEGEOM>
+// CB: the scene has cylinder-box pairs (without them the exact cylinder-box code is compiled
+// out: it costs registers even when it never runs)
+template <int NM, bool ONEGEOM, bool CB>
 __global__ __launch_bounds__(kBlock, SSPP_TSP_WAVES_PER_EU) void k_tsp(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
@@ -1352,7 +1366,7 @@ __global__ __launch_bounds__(kBlock, SSPP_TSP_WAVES_PER_EU) void k_tsp(
             aL = aL + dist_nd<D>(pv, pc);
             double c = 0.0;
 #ifndef SSPP_PROF_NOCOLL  // profiling variant only
-            point_collide<D, NM, 1, true, ONEGEOM>(pc, a.sc, T, mask, &c);
+            point_collide<D, NM, 1, true, ONEGEOM, CB>(pc, a.sc, T, mask, &c);
 #endif
             const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
             const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
@@ -1480,8 +1494,9 @@ struct sspp_job {
     double* d_mean = nullptr;
     double* d_sigma = nullptr;
     BlockBest* d_part = nullptr;
-    double* d_pert = nullptr;  // sampler output: perturbed columns [max_batch][(n-2p)*D]
+    double* d_pert = nullptr;  // sampler output: perturbed columns [pert_steps][max_batch][(n-2p)*D]
     int npert = 0;
+    int pert_steps = 1;        // steps per launch the sampler buffer holds
     int insample = 0;          // sample inside the scoring kernel (SSPP_INSAMPLE=1)
     // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
     int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16, nt2 = 256;
@@ -1772,6 +1787,10 @@ static KScene kscene(const sspp_scene* s, bool tsp) {
     for (const DPair& p : s->pairs) k.onegeom &= (p.gm == s->pairs[0].gm);
     k.static_block = (!tsp && s->count_static && s->static_contacts > 0) ? 1 : 0;
     k.static_cost = tsp ? s->static_cost : 0.0;
+    for (const DPair& p : s->pairs) {
+        const int tg = s->geoms[p.gm].type;
+        k.cylbox |= (tg == 5 && p.otype == 6) || (tg == 6 && p.otype == 5);
+    }
     return k;
 }
 
@@ -1932,6 +1951,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     j->npert = (n - 2 * p) * D;
     if (j->npert < 0) j->npert = 0;
     { const char* e = getenv("SSPP_KERNEL"); j->c2f = e ? atoi(e) != 0 : 1; }
+    // default: c2f draws inside the scoring kernel (SSPP_INSAMPLE=0: chip-wide k_sample_sspp; measured slower)
     { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : (j->c2f ? 1 : 0); }
     { const char* e = getenv("SSPP_HULL"); j->hull = e ? atoi(e) : 2; }
     {
@@ -1969,7 +1989,11 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
                   sizeof(unsigned long long) * j->cpb2 + sizeof(int) * (2 * j->cpb2 + 1);
         if (j->lds2 > 64 * 1024) j->c2f = 0;
     }
-    if (j->npert > 0 && hipMalloc((void**)&j->d_pert, sizeof(double) * (size_t)max_batch * j->npert) != hipSuccess) {
+    if (j->npert > 0 && !j->insample && j->c2f) {  // room for kMaxSteps steps, capped at 256 MiB
+        const size_t per_step = sizeof(double) * (size_t)max_batch * j->npert;
+        j->pert_steps = (int)std::max<size_t>(1, std::min<size_t>(kMaxSteps, ((size_t)256 << 20) / per_step));
+    }
+    if (j->npert > 0 && hipMalloc((void**)&j->d_pert, sizeof(double) * (size_t)max_batch * j->npert * j->pert_steps) != hipSuccess) {
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc sampler buffer");
     }
@@ -2039,9 +2063,10 @@ static hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs
     if (j->nt2 == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
 #ifdef SSPP_DEV_ONLY  // variant builds for experiments: robocrane shape only (fast compile)
     return hipErrorInvalidValue;
-#endif
+#else
     if (j->nt2 == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st);
     return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
+#endif
 }
 
 template <int P>
@@ -2050,7 +2075,7 @@ static hipError_t dispatch_c2f_p(const SsppC2F& k, const sspp_job* j, const Sspp
 #ifdef SSPP_DEV_ONLY
     if (P == 3 && j->nm == 1 && j->D == 7) return launch_c2f<7, 1, P>(k, j, o, nblk, st);
     return hipErrorInvalidValue;
-#endif
+#else
     if (j->nm == 2) {
         if (j->D == 9) return launch_c2f<9, 2, P>(k, j, o, nblk, st);
         return hipErrorInvalidValue;
@@ -2065,6 +2090,7 @@ static hipError_t dispatch_c2f_p(const SsppC2F& k, const sspp_job* j, const Sspp
         case 9: return launch_c2f<9, 1, P>(k, j, o, nblk, st);
     }
     return hipErrorInvalidValue;
+#endif
 }
 
 template <int P>
@@ -2072,7 +2098,7 @@ static hipError_t dispatch_sspp_p(const SsppK& k, const sspp_job* j, const SsppP
                                   hipStream_t st) {
 #ifdef SSPP_DEV_ONLY
     return hipErrorInvalidValue;
-#endif
+#else
     if (j->nm == 2) {
         if (j->D == 9) return launch_sspp<9, 2, P>(k, j, o, nblk, st);
         return hipErrorInvalidValue;
@@ -2087,6 +2113,7 @@ static hipError_t dispatch_sspp_p(const SsppK& k, const sspp_job* j, const SsppP
         case 9: return launch_sspp<9, 1, P>(k, j, o, nblk, st);
     }
     return hipErrorInvalidValue;
+#endif
 }
 
 static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B, double* d_arc,
@@ -2108,16 +2135,17 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     k.insample = j->insample;
     k.arc_all = j->arc_all;
     SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
-    if (steps < 1 || steps > kMaxSteps || (steps > 1 && (!j->c2f || d_ctrl || (j->npert > 0 && !j->insample))))
-        return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..64, coarse-to-fine kernel with in-kernel sampling only");
+    if (steps < 1 || steps > kMaxSteps || (steps > 1 && (!j->c2f || d_ctrl || (j->npert > 0 && !j->insample && steps > j->pert_steps))))
+        return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..64 (coarse-to-fine kernel, sampled candidates)");
     const int cpb = j->c2f ? j->cpb2 : j->cpb;
     const int nblk = (int)((B + cpb - 1) / cpb);
     hipStream_t st = (hipStream_t)stream;
     if (!d_ctrl && j->npert > 0 && !j->insample) {  // sampleWithNoise over the whole chip
-        const long long work = B * (long long)((j->npert + 1) / 2);
+        const long long work = (long long)steps * B * (long long)((j->npert + 1) / 2);
         hipLaunchKernelGGL(k_sample_sspp, dim3((unsigned)((work + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                           (unsigned long long)j->seed, (long long)first_id, (long long)B, j->D, j->p,
-                           j->npert, j->sigma, j->d_init, j->d_limits, j->d_pert);
+                           (unsigned long long)j->seed, (long long)first_id, (long long)step_stride,
+                           (long long)B, steps, j->D, j->p, j->npert, j->sigma, j->d_init, j->d_limits,
+                           j->d_pert);
         hipError_t es = hipGetLastError();
         if (es != hipSuccess) return hip_fail(es, "k_sample_sspp launch");
     }
@@ -2258,14 +2286,20 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     }
     const int nblk = (int)((B + j->cpb - 1) / j->cpb);
     hipStream_t st = (hipStream_t)stream;
-    if (k.sc.onegeom && k.sc.npairs > 0)
-        hipLaunchKernelGGL((k_tsp<1, true>), dim3(nblk), dim3(kBlock), j->lds, st, k, scene_t(j->scene),
-                           j->d_tab, j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out,
-                           d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part, j->d_sync, d_best);
-    else
-        hipLaunchKernelGGL((k_tsp<1, false>), dim3(nblk), dim3(kBlock), j->lds, st, k, scene_t(j->scene),
-                           j->d_tab, j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out,
-                           d_L, d_Cnf, d_Cwf, d_cost, d_status, j->d_part, j->d_sync, d_best);
+    const SceneT tt = scene_t(j->scene);
+#define SSPP_LAUNCH_TSP(OG, CBV)                                                                   \
+    hipLaunchKernelGGL((k_tsp<1, OG, CBV>), dim3(nblk), dim3(kBlock), j->lds, st, k, tt, j->d_tab, \
+                       j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
+                       d_status, j->d_part, j->d_sync, d_best)
+    const bool og = k.sc.onegeom && k.sc.npairs > 0;
+#ifdef XP_NOCB
+    k.sc.cylbox = 0;
+#endif
+    if (og && k.sc.cylbox) SSPP_LAUNCH_TSP(true, true);
+    else if (og) SSPP_LAUNCH_TSP(true, false);
+    else if (k.sc.cylbox) SSPP_LAUNCH_TSP(false, true);
+    else SSPP_LAUNCH_TSP(false, false);
+#undef SSPP_LAUNCH_TSP
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_tsp launch");
     return SSPP_OK;

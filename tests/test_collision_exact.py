@@ -172,3 +172,64 @@ def test_box_box_manifold_random_pairs():
             assert (nd > 0) == (dist < DEEP)
         multi += nd > 1
     assert checked > 390 and multi > 20
+
+
+def _mat_to_quat(M):
+    """rotation matrix (columns = body axes) -> quaternion (w, x, y, z)"""
+    tr = np.trace(M)
+    if tr > 0:
+        s = 2 * math.sqrt(1 + tr)
+        return np.array([s / 4, (M[2, 1] - M[1, 2]) / s, (M[0, 2] - M[2, 0]) / s, (M[1, 0] - M[0, 1]) / s])
+    i = int(np.argmax(np.diag(M)))
+    j, k = (i + 1) % 3, (i + 2) % 3
+    s = 2 * math.sqrt(1 + M[i, i] - M[j, j] - M[k, k])
+    q = np.zeros(4)
+    q[0] = (M[k, j] - M[j, k]) / s
+    q[1 + i] = s / 4
+    q[1 + j] = (M[j, i] + M[i, j]) / s
+    q[1 + k] = (M[k, i] + M[i, k]) / s
+    return q
+
+
+def test_cylinder_box_rim_edge_family():
+    """A box edge placed at a prescribed gap from the rim along their common normal (built
+    directly: a rim point p, a normal n in the rim's normal cone, an edge direction e perpendicular
+    to n, the box's two faces at that edge opening away from the cylinder).  The signed distance
+    is the gap, so contact (margin 1 mm) and deep contact flip exactly at the thresholds — this
+    exercises the rim-edge (ellipse) candidates, which the finite SAT axes do not contain."""
+    rng = np.random.default_rng(5)
+    R, H = 0.05, 0.04
+    margin = 0.001
+    checked = flips = 0
+    for _ in range(120):
+        th = rng.uniform(0, 2 * math.pi)
+        s = rng.choice([-1.0, 1.0])
+        rho = np.array([math.cos(th), math.sin(th), 0.0])
+        p = rho * R + np.array([0, 0, s * H])
+        al = rng.uniform(0.15, 1.4)  # normal between the radial direction and the cap normal
+        n = math.cos(al) * rho + math.sin(al) * np.array([0, 0, s])
+        e = np.cross(n, rng.normal(size=3))
+        e /= np.linalg.norm(e)
+        w = np.cross(e, n)
+        f1, f2 = (-n + w) / math.sqrt(2), (-n - w) / math.sqrt(2)  # outward normals at the edge
+        M = np.stack([e, f1, f2], 1)
+        ext = np.array([0.08, 0.05, 0.05])
+        for gap in (margin + 2e-6, margin - 2e-6, -1e-3 * rng.uniform(0.5, 3.0)):
+            q = p + gap * n
+            cb = q - ext[1] * f1 - ext[2] * f2
+            n_c, _, nd = contacts([(CYL, (R, H, 0), (0, 0, 0), (1, 0, 0, 0), margin)],
+                                  [(BOX, tuple(ext), (0, 0, 0), (1, 0, 0, 0))], cb, tuple(_mat_to_quat(M)))
+            T, a = cb, np.array([0, 0, 1.0])
+            if gap > 0:
+                # separated: the closest points are p and q, the distance is the gap
+                assert (n_c > 0) == (gap < margin), (th, s, al, gap)
+                # the 7 SAT axes alone would not have separated (a false contact)
+                flips += sat7_lower_bound(T, a, H, R, M, ext) < margin
+            else:
+                # penetrating: the depth can be below |gap| (another direction may be shorter)
+                dist = ref_signed_distance(T, a, H, R, M, ext, rng)
+                assert n_c > 0
+                if abs(dist - DEEP) > 1e-6:
+                    assert (nd > 0) == (dist < DEEP), (th, s, al, gap, dist)
+            checked += 1
+    assert checked == 360 and flips > 30
