@@ -1102,9 +1102,10 @@ static int cyl_box_overlap(const double* pa, const double* ma, const double* sz,
                            const double* mb, const double* eb, double thr) {
     or_cylbox c = make_cylbox(pa, ma, sz, pb, mb, eb);
     if (cb_base_sep(&c, thr)) return 0;
-    int deep = thr < 0.0;
-    if (deep ? cb_deep_witness(&c, -thr) : cb_touch_witness(&c, thr)) return 1;
+    /* past the SAT axes everything runs in the box's frame, as on the device */
     or_cylbox b = cb_box_frame(&c);
+    int deep = thr < 0.0;
+    if (deep ? cb_deep_witness(&b, -thr) : cb_touch_witness(&b, thr)) return 1;
     return !cb_ext_sep(&b, thr, deep);
 }
 

@@ -13,6 +13,12 @@
 #include <stdint.h>
 
 #define SSPP_HD __host__ __device__ __forceinline__
+// profiling counters of the narrowphase paths (SSPP_C2F_STATS builds; slots 10-13)
+#if defined(SSPP_CB_STAT) && defined(__HIP_DEVICE_COMPILE__)
+#define SSPP_NP_STAT(i) SSPP_CB_STAT(i)
+#else
+#define SSPP_NP_STAT(i) do { } while (0)
+#endif
 
 namespace sspd {
 
@@ -801,9 +807,10 @@ SSPP_HD CylBox cb_box_frame(const CylBox& c) {
     b.R = c.R; b.H = c.H;
     return b;
 }
-SSPP_HD bool cb_ext_sep_boxframe(double T0, double T1, double T2, double a0, double a1, double a2,
-                                 double e0, double e1, double e2, double R, double H, double thr,
-                                 bool all_roots) {
+// The candidate directions past the SAT axes and the witnesses, in the box's frame (box axes =
+// identity), from 12 doubles (so it fits the argument registers of a call).
+SSPP_HD bool cb_ext_overlap(double T0, double T1, double T2, double a0, double a1, double a2,
+                            double e0, double e1, double e2, double R, double H, double thr) {
     CylBox b;
     b.T[0] = T0; b.T[1] = T1; b.T[2] = T2;
     b.a[0] = a0; b.a[1] = a1; b.a[2] = a2;
@@ -813,33 +820,34 @@ SSPP_HD bool cb_ext_sep_boxframe(double T0, double T1, double T2, double a0, dou
 #pragma unroll
         for (int i = 0; i < 3; ++i) b.B[k][i] = k == i ? 1.0 : 0.0;
     b.R = R; b.H = H;
-    return cb_ext_sep(b, thr, all_roots);
+    SSPP_NP_STAT(12);
+    return !cb_ext_sep(b, thr, thr < 0.0);
 }
-// Out of line, for kernels at their register budget (k_tsp): the call happens only for pairs the
-// SAT axes and the witnesses leave undecided.
-__host__ __device__ inline __attribute__((noinline)) bool cb_ext_sep_call(
+// Out of line, for kernels at their register budget (k_tsp): reached only by the pairs neither
+// the SAT axes nor a witness decide (well under 0.1 % of the multi-goal bench's tests).
+__host__ __device__ inline __attribute__((noinline)) bool cb_ext_overlap_call(
     double T0, double T1, double T2, double a0, double a1, double a2, double e0, double e1,
-    double e2, double R, double H, double thr, bool all_roots) {
-    return cb_ext_sep_boxframe(T0, T1, T2, a0, a1, a2, e0, e1, e2, R, H, thr, all_roots);
+    double e2, double R, double H, double thr) {
+    return cb_ext_overlap(T0, T1, T2, a0, a1, a2, e0, e1, e2, R, H, thr);
 }
 
 // cylinder (A) vs box (B): signed distance < thr (thr = margin >= 0, or kDeep for a deep
-// contact).  The 7 SAT axes separate most pairs; overlaps are usually proven by a witness;
-// only what neither settles runs the remaining candidate directions (in the box's frame;
-// OUTLINE: as a call).
+// contact).  The 7 SAT axes (world frame) separate most pairs; the rest runs in the box frame:
+// witnesses prove most overlaps, the candidate directions (OUTLINE: as a call) decide the rest.
 template <bool OUTLINE>
 SSPP_HD bool cyl_box_overlap(const double* pa, const double* ma, const double* sz, const double* pb,
                              const double* mb, const double* eb, double thr) {
     const CylBox c = make_cylbox(pa, ma, sz, pb, mb, eb);
+    SSPP_NP_STAT(10);
     if (cb_base_sep(c, thr)) return false;
-    const bool deep = thr < 0.0;
-    if (deep ? cb_deep_witness(c, -thr) : cb_touch_witness(c, thr)) return true;
+    SSPP_NP_STAT(11);
     const CylBox b = cb_box_frame(c);
+    if (thr < 0.0 ? cb_deep_witness(b, -thr) : cb_touch_witness(b, thr)) return true;
     if (OUTLINE)
-        return !cb_ext_sep_call(b.T[0], b.T[1], b.T[2], b.a[0], b.a[1], b.a[2], b.e[0], b.e[1], b.e[2],
-                                b.R, b.H, thr, deep);
-    return !cb_ext_sep_boxframe(b.T[0], b.T[1], b.T[2], b.a[0], b.a[1], b.a[2], b.e[0], b.e[1], b.e[2],
-                                b.R, b.H, thr, deep);
+        return cb_ext_overlap_call(b.T[0], b.T[1], b.T[2], b.a[0], b.a[1], b.a[2], b.e[0], b.e[1], b.e[2],
+                                   b.R, b.H, thr);
+    return cb_ext_overlap(b.T[0], b.T[1], b.T[2], b.a[0], b.a[1], b.a[2], b.e[0], b.e[1], b.e[2],
+                          b.R, b.H, thr);
 }
 
 // Supported narrowphase pair? (types ordered t1 <= t2)
@@ -884,8 +892,10 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
     }
     // box-box: SAT (exact for boxes) decides contact; deep contacts: one pass, SAT + manifold
     if (NEED_DEEP) {
+        SSPP_NP_STAT(13);
         *nd = (margin >= kDeep || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
                   ? box_box_deep_count(p1, m1, s1, p2, m2, s2) : 0;
+        if (*nd > 0) SSPP_NP_STAT(14);
         return *nd;
     }
     return sat_box_box(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;

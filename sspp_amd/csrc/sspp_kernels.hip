@@ -24,6 +24,10 @@
 #include <vector>
 
 #include "model.h"
+#ifdef SSPP_C2F_STATS  // profiling builds only (tools/build_variant.sh stats -DSSPP_C2F_STATS)
+__device__ unsigned long long g_c2f_stats[16];
+#define SSPP_CB_STAT(i) atomicAdd(&g_c2f_stats[i], 1ull)
+#endif
 #include "sspp_device.h"
 
 using namespace sspd;
@@ -831,8 +835,7 @@ struct SsppC2F {
     int hull;      // candidate hull broadphase: 0 off, 1 all candidates, 2 phase-1 survivors
 };
 
-#ifdef SSPP_C2F_STATS  // profiling builds only (tools/build_variant.sh stats -DSSPP_C2F_STATS)
-__device__ unsigned long long g_c2f_stats[16];
+#ifdef SSPP_C2F_STATS
 #define C2F_STAT(i, v) do { const unsigned long long v_ = (v); if ((threadIdx.x & 63) == 0 && v_) atomicAdd(&g_c2f_stats[i], v_); } while (0)
 #else
 #define C2F_STAT(i, v) do { } while (0)
@@ -1237,12 +1240,15 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
 // tab: (cp+1) rows of 3 basis values at u = i * (1/cp); Minv: collocation inverse (n x n).
 #ifndef SSPP_TSP_WAVES_PER_EU
-#define SSPP_TSP_WAVES_PER_EU 4
+#define SSPP_TSP_WAVES_PER_EU 3
+#endif
+#ifndef SSPP_TSP_WAVES_PER_EU_CB  // with the exact cylinder-box test (its live state doubles)
+#define SSPP_TSP_WAVES_PER_EU_CB 2
 #endif
 // CB: the scene has cylinder-box pairs (without them the exact cylinder-box code is compiled
 // out: it costs registers even when it never runs)
 template <int NM, bool ONEGEOM, bool CB>
-__global__ __launch_bounds__(kBlock, SSPP_TSP_WAVES_PER_EU) void k_tsp(
+__global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WAVES_PER_EU) void k_tsp(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
     const double* __restrict__ sigma, const double* __restrict__ vias_in,
@@ -2292,9 +2298,6 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
                        j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
                        d_status, j->d_part, j->d_sync, d_best)
     const bool og = k.sc.onegeom && k.sc.npairs > 0;
-#ifdef XP_NOCB
-    k.sc.cylbox = 0;
-#endif
     if (og && k.sc.cylbox) SSPP_LAUNCH_TSP(true, true);
     else if (og) SSPP_LAUNCH_TSP(true, false);
     else if (k.sc.cylbox) SSPP_LAUNCH_TSP(false, true);
