@@ -552,7 +552,7 @@ def main():
     if os.path.exists(tf):
         rec = json.load(open(tf)).get(args.config)
         if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and \
-                rec.get("candidates_per_launch") == per_launch:
+                rec.get("candidates_per_launch") == per_launch and args.waypoints == 128:
             traffic, traffic_src = rec["hbm_bytes_per_launch"], rec["source"]
 
     if rank == 0:
@@ -566,7 +566,8 @@ def main():
         ff = os.path.join(ROOT, "profiles", "fp64_latest.json")
         if os.path.exists(ff):
             rec = json.load(open(ff)).get(args.config)
-            if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp"):
+            if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and \
+                    rec.get("candidates_per_launch", per_launch) == per_launch and args.waypoints == 128:
                 exec_per, exec_src = rec["fp64_flops_per_candidate"], rec["source"]
                 ach_exec = exec_per * per_launch / kernel_s / 1e12
         ach_gbs = bytes_per * per_launch / kernel_s / 1e9

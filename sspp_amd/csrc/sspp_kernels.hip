@@ -28,6 +28,9 @@
 __device__ unsigned long long g_c2f_stats[16];
 #define SSPP_CB_STAT(i) atomicAdd(&g_c2f_stats[i], 1ull)
 #endif
+#ifdef SSPP_WG_TIMING  // profiling builds only: per-workgroup (start, end, CU, survivors) of k_sspp_c2f
+__device__ unsigned long long g_wg_t[1 << 18];
+#endif
 #include "sspp_device.h"
 
 using namespace sspd;
@@ -919,7 +922,7 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
 }
 
 #ifndef SSPP_C2F_WAVES_PER_EU
-#define SSPP_C2F_WAVES_PER_EU 3  // also bounds the out-of-line narrowphase callees (their budget is the callers' minimum)
+#define SSPP_C2F_WAVES_PER_EU 4  // measured: 3 -> 1280, 4 -> 1396, 5 -> 1237, 6 -> 697 M cand/s (robocrane)
 #endif
 template <int D, int NM, int P, bool ONEGEOM, int NT>
 __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
@@ -940,6 +943,10 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     const int nvalid = (int)min((long long)cpb, a.B - cand0);
     const long long first_id = a.first_id + step * a.step_stride;
     if (a.ablate & 64) return;  // profiling: launch + dispatch cost only
+#ifdef SSPP_WG_TIMING
+    const unsigned long long wg_t0 = wall_clock64();
+    int wg_ns = -1;
+#endif
     if (step) {
         arc += step * a.B;
         feasible += step * a.B;
@@ -950,8 +957,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         if (best) best += step;
     }
     double* s_ctrl = smem;                                    // [cpb][n][D]
-    double* s_chord = s_ctrl + cpb * ndof;                    // [cpb][W-1]
-    double* s_vsum = s_chord + cpb * nch;                     // [cpb][lpc/64]
+    double* s_vsum = s_ctrl + cpb * ndof;                     // [cpb][lpc/64]
     double* s_arc = s_vsum + cpb * (a.lpc >> 6);              // [cpb]
     double* s_box = s_arc + cpb;                              // [cpb][2][NB]
     unsigned long long* s_mask = (unsigned long long*)(s_box + cpb * 2 * NB);  // [cpb]
@@ -1088,6 +1094,9 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         __syncthreads();
         const int ns = s_surv[cpb];
         if (tid == 0) C2F_STAT(6, ns);
+#ifdef SSPP_WG_TIMING
+        wg_ns = ns;
+#endif
         if (hull == 2 && ns > 0 && np <= 64) {  // the survivors' hull masks (see above)
             for (int e = tid; e < ns * NB; e += NT) {
                 const int si = e / NB, md = e - si * NB, m = md / 3, d = md - m * 3;
@@ -1161,46 +1170,25 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
         __syncthreads();
         const int nl = s_list[cpb];
-        if (a.arc_all) {
-            // every candidate: G1 threads per candidate over consecutive runs of chords, each
-            // point evaluated once
-            const int g = tid >> lg1, l = tid & (g1 - 1);
-            const int per = (nch + g1 - 1) >> lg1;
-            const int j0 = l * per, j1 = min(j0 + per, nch);
-            if (g < nvalid && j0 < j1) {
-                const double* myc = s_ctrl + g * ndof;
-                double* ch = s_chord + g * nch;
-                double qa[D], qb[D];
-                eval_pt<D, P>(myc, atab + j0 * P1, aspan[j0], qa);
-                for (int j = j0; j < j1; ++j) {
-                    eval_pt<D, P>(myc, atab + (j + 1) * P1, aspan[j + 1], qb);
-                    ch[j] = dist_nd<D>(qa, qb);
-#pragma unroll
-                    for (int d = 0; d < D; ++d) qa[d] = qb[d];
-                }
-            }
-        } else {
-            // the few collision-free candidates: one chord per thread over the workgroup; a
-            // chord's first point is the previous lane's second point (same candidate when
-            // j > 0), taken by shuffle: bit-identical to evaluating it again
-            for (int it = tid; it < nl * nch; it += NT) {
-                const int si = it / nch, j = it - si * nch, sl = s_list[si];
-                const double* myc = s_ctrl + sl * ndof;
-                double qa[D], qb[D];
-                eval_pt<D, P>(myc, atab + (j + 1) * P1, aspan[j + 1], qb);
-#pragma unroll
-                for (int d = 0; d < D; ++d) qa[d] = __shfl_up(qb[d], 1, 64);
-                if (j == 0 || (tid & 63) == 0) eval_pt<D, P>(myc, atab + j * P1, aspan[j], qa);
-                s_chord[sl * nch + j] = dist_nd<D>(qa, qb);
-            }
-        }
-        __syncthreads();
+        // one wave per (listed candidate, 64-lane group v of the lpc canonical lanes): lane l
+        // accumulates chords j = 64 v + l, + lpc, ... (the lane partials of or_canon_sum), then
+        // the xor butterfly gives the group's sum.  A chord's first point is the previous lane's
+        // second point (same candidate, same pass), taken by shuffle: bit-identical to
+        // evaluating it again.  No chord array: the workgroup's LDS holds only control points.
         const int lpc = a.lpc, nvw = lpc >> 6, lane = tid & 63;
         for (int vw = tid >> 6; vw < nl * nvw; vw += NT / 64) {  // wave-uniform
-            const int si = vw / nvw, vl = (vw - si * nvw) * 64 + lane;
-            const double* ch = s_chord + s_list[si] * nch;
+            const int si = vw / nvw, v = vw - si * nvw;
+            const double* myc = s_ctrl + s_list[si] * ndof;
             double acc = 0.0;
-            for (int j = vl; j < nch; j += lpc) acc = acc + ch[j];
+            for (int base = v * 64; base < nch; base += lpc) {  // wave-uniform trip count
+                const int j = base + lane, jj = j < nch ? j : nch - 1;
+                double qa[D], qb[D];
+                eval_pt<D, P>(myc, atab + (jj + 1) * P1, aspan[jj + 1], qb);
+#pragma unroll
+                for (int d = 0; d < D; ++d) qa[d] = __shfl_up(qb[d], 1, 64);
+                if (lane == 0) eval_pt<D, P>(myc, atab + jj * P1, aspan[jj], qa);
+                if (j < nch) acc = acc + dist_nd<D>(qa, qb);
+            }
             acc = wave_sum(acc);
             if (lane == 0) s_vsum[vw] = acc;
         }
@@ -1235,6 +1223,14 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         bb.cost = bi < 0 ? INFINITY : bc; bb.idx = bi; bb.count = __popcll(__ballot(f)); bb.pad = 0;
     }
     finish_batch<NT>(bb, part, sync, best, a.nblk_step, blk);
+#ifdef SSPP_WG_TIMING
+    if (tid == 0 && blockIdx.x < (1 << 16)) {
+        g_wg_t[4 * blockIdx.x] = wg_t0;
+        g_wg_t[4 * blockIdx.x + 1] = wall_clock64();
+        g_wg_t[4 * blockIdx.x + 2] = __smid();
+        g_wg_t[4 * blockIdx.x + 3] = (unsigned long long)(long long)wg_ns;
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
@@ -1991,7 +1987,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
             }
         }
         const int nm = j->nm < 1 ? 1 : j->nm;
-        j->lds2 = sizeof(double) * ((size_t)j->cpb2 * (n * D + (W - 1) + lanes_for(W - 1) / 64 + 1 + 6 * nm)) +
+        j->lds2 = sizeof(double) * ((size_t)j->cpb2 * (n * D + lanes_for(W - 1) / 64 + 1 + 6 * nm)) +
                   sizeof(unsigned long long) * j->cpb2 + sizeof(int) * (2 * j->cpb2 + 1);
         if (j->lds2 > 64 * 1024) j->c2f = 0;
     }
@@ -2445,6 +2441,14 @@ extern "C" int sspp_debug_c2f_stats(unsigned long long* out, int reset) {
         unsigned long long z[16] = {0};
         hipMemcpyToSymbol(HIP_SYMBOL(g_c2f_stats), z, sizeof z);
     }
+    return 0;
+}
+#endif
+
+#ifdef SSPP_WG_TIMING
+extern "C" int sspp_debug_wg_times(unsigned long long* out, int n) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_t), sizeof(unsigned long long) * (size_t)n);
     return 0;
 }
 #endif

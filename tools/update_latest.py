@@ -1,0 +1,85 @@
+"""Fold a PMC evidence run (tools/gpu_round2_pmc.sh) into profiles/traffic_latest.json and
+profiles/fp64_latest.json, which bench.py reads for roofline.traffic / roofline_fp64.
+    python tools/update_latest.py gpurun_out/TAG profiles/PREFIX
+Per config: the dominant kernel's launches of the roofline shape (the most frequent grid),
+mean FETCH_SIZE / WRITE_SIZE per launch (KiB; HBM bytes = 1024 * (2 * FETCH + WRITE), the
+gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md) and the executed FP64 flops (64 lanes x
+(ADD + MUL + TRANS + 2 FMA) F64 wave instructions).  Also writes PREFIX_<config>_pmc.json."""
+import collections
+import csv
+import json
+import os
+import sys
+
+KERNEL = {"robocrane": "k_sspp_c2f", "stacking": "k_tsp", "multigoal": "k_tsp"}
+PER_LAUNCH = {"robocrane": 32 * 4096, "stacking": 16384, "multigoal": 4098}
+STEPS = {"robocrane": "--steps 64 --warmup 4 (32 steps x 4096 candidates per launch)",
+         "stacking": "--config stacking --steps 4 --warmup 1",
+         "multigoal": "--config multigoal --steps 4 --warmup 1"}
+
+
+def rows(path, kern):
+    f = os.path.join(path, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        return []
+    return [r for r in csv.DictReader(open(f)) if kern in r["Kernel_Name"]]
+
+
+def per_launch(rs, counters):
+    """{counter: mean per launch} over the launches of the most frequent grid size."""
+    grid = collections.Counter(r["Grid_Size"] for r in rs).most_common(1)[0][0]
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in rs:
+        if r["Grid_Size"] == grid and r["Counter_Name"] in counters:
+            acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    out = {c: sum(v.values()) / len(v) for c, v in acc.items()}
+    out["launches"] = max(len(v) for v in acc.values())
+    out["grid"] = int(grid)
+    for k in ("VGPR_Count", "SGPR_Count", "Scratch_Size", "LDS_Block_Size"):
+        out[k] = int(next(r[k] for r in rs if r["Grid_Size"] == grid))
+    return out
+
+
+def main(src, prefix):
+    tf, ff = "profiles/traffic_latest.json", "profiles/fp64_latest.json"
+    traffic = json.load(open(tf)) if os.path.exists(tf) else {}
+    fp64 = json.load(open(ff)) if os.path.exists(ff) else {}
+    for cfg, kern in KERNEL.items():
+        d = os.path.join(src, cfg)
+        if not os.path.isdir(d):
+            continue
+        res = {"kernel": kern, "candidates_per_launch": PER_LAUNCH[cfg], "command": STEPS[cfg]}
+        fr, wr = rows(os.path.join(d, "pmc_fetch"), kern), rows(os.path.join(d, "pmc_write"), kern)
+        if fr and wr:
+            f, w = per_launch(fr, {"FETCH_SIZE"}), per_launch(wr, {"WRITE_SIZE"})
+            res.update(FETCH_SIZE_KiB=f["FETCH_SIZE"], WRITE_SIZE_KiB=w["WRITE_SIZE"], launches=f["launches"],
+                       grid=f["grid"], vgpr=f["VGPR_Count"], sgpr=f["SGPR_Count"],
+                       scratch_per_lane=f["Scratch_Size"], lds=f["LDS_Block_Size"])
+            res["hbm_bytes_per_launch"] = 1024.0 * (2.0 * f["FETCH_SIZE"] + w["WRITE_SIZE"])
+            traffic[cfg] = {"kernel": kern, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
+                            "candidates_per_launch": PER_LAUNCH[cfg],
+                            "source": "%s_%s_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
+                                      "FETCH x2 gfx950 correction; %s)" % (prefix, cfg, STEPS[cfg])}
+        pr = rows(os.path.join(d, "p1"), kern)
+        if pr:
+            m = per_launch(pr, {r["Counter_Name"] for r in pr})
+            res["mix"] = m
+            fl = 64.0 * (m["SQ_INSTS_VALU_ADD_F64"] + m["SQ_INSTS_VALU_MUL_F64"] +
+                         m["SQ_INSTS_VALU_TRANS_F64"] + 2 * m["SQ_INSTS_VALU_FMA_F64"])
+            res["fp64_flops_per_launch"] = fl
+            res["fp64_flops_per_candidate"] = fl / PER_LAUNCH[cfg]
+            fp64[cfg] = {"kernel": kern, "fp64_flops_per_candidate": res["fp64_flops_per_candidate"],
+                         "candidates_per_launch": PER_LAUNCH[cfg],
+                         "source": "%s_%s_pmc.json: 64 x (ADD+MUL+TRANS+2 FMA)_F64 wave instructions per "
+                                   "launch / %d candidates" % (prefix, cfg, PER_LAUNCH[cfg])}
+        occ = rows(os.path.join(d, "occ", "p1"), kern)
+        if occ:
+            res["occupancy"] = per_launch(occ, {r["Counter_Name"] for r in occ})
+        json.dump(res, open("%s_%s_pmc.json" % (prefix, cfg), "w"), indent=1, sort_keys=True)
+        print(cfg, json.dumps(res, sort_keys=True)[:600])
+    json.dump(traffic, open(tf, "w"), indent=1)
+    json.dump(fp64, open(ff, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:3])

@@ -1,0 +1,47 @@
+"""Per-workgroup timeline of one driver-shaped k_sspp_c2f launch (--steps 20 --warmup 5, 20
+steps in one launch).  Needs a -DSSPP_WG_TIMING variant via SSPP_LIB_PATH.
+    python tools/wg_timing.py [steps] [out.json]"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from sspp_amd import _lib  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+out_path = sys.argv[2] if len(sys.argv) > 2 else None
+sys.argv = ["bench.py", "--steps", str(steps), "--warmup", "5", "--no-cpu-baseline"]
+args = bench.parse()
+device = torch.device("cuda", 0)
+B, step, kernel_only, bytes_per, flops_per, meta, ctx = bench.setup_robocrane(args, device)
+run = bench.native_runner(args, ctx, B, 1, 0, device)
+run(5)
+torch.cuda.synchronize()
+run(steps)
+torch.cuda.synchronize()
+nwg = steps * 512
+buf = (C.c_ulonglong * (4 * nwg))()
+_lib.lib().__getattr__("sspp_debug_wg_times")(buf, 4 * nwg)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 4).astype(np.int64)
+t0 = a[:, 0].min()
+st = (a[:, 0] - t0) / 100.0  # wall clock: 100 MHz -> us
+en = (a[:, 1] - t0) / 100.0
+dur = en - st
+ns = a[:, 3]
+res = {"workgroups": int(nwg), "span_us": float(en.max()),
+       "dur_us_pcts": {p: float(np.percentile(dur, p)) for p in (10, 50, 90, 99, 100)},
+       "dur_us_by_survivors": {int(k): [int((ns == k).sum()), float(dur[ns == k].mean())]
+                               for k in np.unique(ns)},
+       "start_us_pcts": {p: float(np.percentile(st, p)) for p in (0, 10, 50, 90, 100)},
+       "end_us_pcts": {p: float(np.percentile(en, p)) for p in (10, 50, 90, 99, 100)},
+       "last_20_end": [[float(st[i]), float(en[i]), int(ns[i])] for i in np.argsort(en)[-20:]],
+       "concurrency_at": {t: int(((st <= t) & (en > t)).sum()) for t in (5, 10, 20, 40, 60, 80)}}
+print(json.dumps(res, indent=1))
+if out_path:
+    json.dump(res, open(out_path, "w"), indent=1)
