@@ -863,7 +863,10 @@ SSPP_HD bool pair_supported(int t1, int t2) {
 // NEED_DEEP=true:  only *nd (contacts with dist < -1e-3, Collision.h cost) is meaningful.
 // CB = false compiles out the cylinder-box code (only for scenes without such pairs); OUTLINE
 // calls the rare cylinder-box candidate search out of line.
-template <bool NEED_DEEP, bool CB = true, bool OUTLINE = false>
+// DEFER (feasibility only): a cylinder-box pair (already past the bounding-sphere test) returns
+// -1, undecided, without any narrowphase; the caller settles it later with the exact test
+// (k_sspp_c2f -> k_sspp_cbfix), so its pair loop carries none of that code.
+template <bool NEED_DEEP, bool CB = true, bool OUTLINE = false, bool DEFER = false>
 SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1, int t2,
                     const double* p2, const double* m2, const double* s2, double margin, int* nd) {
     *nd = 0;
@@ -881,6 +884,7 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
     }
     if (t1 == 5) {  // cylinder-box: exact signed distance test, one contact (MuJoCo's convex collider)
         if (!CB) return 0;
+        if (DEFER && !NEED_DEEP) return -1;
         if (NEED_DEEP) {
             int d = (margin >= kDeep) ? (int)cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, kDeep)
                                       : (int)(cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, margin) &&

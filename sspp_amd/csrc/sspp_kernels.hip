@@ -836,6 +836,7 @@ struct SsppC2F {
     long long step_stride;
     int arc_all;   // 0: arc length only for collision-free candidates (+inf otherwise)
     int hull;      // candidate hull broadphase: 0 off, 1 all candidates, 2 phase-1 survivors
+    unsigned* dfr; // [0]: candidates of this launch left undecided (cylinder-box), [1]: k_sspp_cbfix arrivals
 };
 
 #ifdef SSPP_C2F_STATS
@@ -848,10 +849,12 @@ struct SsppC2F {
 // test the pairs of their own mask.  gbits = the lanes of this lane's candidate within the
 // wave: when any of them touches, all of them stop (returns true for the group).  flag: the
 // candidate's LDS feasibility flag (phase 2), polled so lanes in other waves stop too.
+// A cylinder-box pair that passes the bounding-sphere test sets dfr (undecided) and counts as
+// no contact here (collide<..., DEFER>); k_sspp_cbfix settles it with the exact test.
 template <int D, int NM, bool ONEGEOM>
 __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned long long mymask,
                                            unsigned long long umask, unsigned long long gbits,
-                                           int* flag, const KScene& sc, const SceneT& T) {
+                                           int* flag, const KScene& sc, const SceneT& T, bool& dfr) {
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
     double mp[NM][3], mR[NM][9];
@@ -907,8 +910,9 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
                 }
                 int nd = 0;
                 const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
-                if (gfirst) nc = collide<false>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
-                else nc = collide<false>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+                if (gfirst) nc = collide<false, true, false, true>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+                else nc = collide<false, true, false, true>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+                if (nc < 0) { dfr = true; nc = 0; }
             }
         }
         C2F_STAT(flag ? 4 : 0, 1);                          // wave pair iterations (phase 2 / 1)
@@ -919,6 +923,47 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
         if (__ballot(live) == 0ull) break;
     }
     return ghit;
+}
+
+// The exact cylinder-box test (witnesses + candidate search, sspd::cyl_box_overlap) of one
+// waypoint over the pairs of `mask` (k_sspp_cbfix).
+template <int D, int NM, int P, bool ONEGEOM>
+__device__ __forceinline__ bool cb_point_exact(const double* ctrl, const double* row, int span,
+                                               unsigned long long mask, int np, SceneT T) {
+    double q[D];
+    eval_pt<D, P>(ctrl, row, span, q);
+    const cgeom_t geoms = (cgeom_t)T.geoms;
+    const cpair_t pairs = (cpair_t)T.pairs;
+    double mp[NM][3], mR[NM][9];
+    mover_poses<D, NM, 0>(q, (cmover_t)T.movers, mp, mR);
+    for (int k = 0; k < np; ++k) {
+        if (k < 64 && !((mask >> k) & 1ull)) continue;
+        const DPair pr = load_pair(pairs + k);
+        const DGeom G = load_geom(geoms + pr.gm);
+        if (!((G.type == 5 && pr.otype == 6) || (G.type == 6 && pr.otype == 5))) continue;
+        const bool second = NM > 1 && G.mover == 1;
+        double gp[3], gmat[9], op_[3], om_[9];
+        geom_pose(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp, gmat);
+        const double* op = pr.opos;
+        const double* om = pr.omat;
+        if (NM > 1 && pr.omover >= 0) {
+            const bool osecond = pr.omover == 1;
+            const double* R = osecond ? mR[NM - 1] : mR[0];
+            const double* Pp = osecond ? mp[NM - 1] : mp[0];
+            double t[3];
+            matvec3(R, pr.opos, t);
+            op_[0] = Pp[0] + t[0]; op_[1] = Pp[1] + t[1]; op_[2] = Pp[2] + t[2];
+            matmul3(R, pr.omat, om_);
+            op = op_; om = om_;
+        }
+        if (!pair_near(pr, G.rbound, gp, op, om)) continue;
+        int nd = 0;
+        const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
+        const int nc = gfirst ? collide<false>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd)
+                              : collide<false>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+        if (nc > 0) return true;
+    }
+    return false;
 }
 
 #ifndef SSPP_C2F_WAVES_PER_EU
@@ -963,6 +1008,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     unsigned long long* s_mask = (unsigned long long*)(s_box + cpb * 2 * NB);  // [cpb]
     int* s_feas = (int*)(s_mask + cpb);                       // [cpb]
     int* s_surv = s_feas + cpb;                               // [cpb + 1] (last = count)
+    int* s_defer = s_surv + cpb + 1;                          // [cpb] undecided cylinder-box pair
 
     // ---- prologue: control points (+ sampleWithNoise) in LDS.  Element e = sl * ndof + r is
     // walked with one division up front and add-with-carry afterwards.
@@ -1067,7 +1113,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         const unsigned long long low = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
         const unsigned long long gbits = low << (wg * g1);
         const bool valid = g < nvalid;
-        bool ghit = false;
+        bool ghit = false, dfr = false;
         if (collide_on) {
             const unsigned long long mymask = s_mask[g];
             unsigned long long umask = 0ull;  // union over the wave's groups (wave-uniform)
@@ -1077,9 +1123,13 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             double q[D];
             const int row = l < a.npts ? l : 0;
             eval_pt<D, P>(s_ctrl + (valid ? g : 0) * ndof, otab + row * P1, ospan[row], q);
-            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mymask, umask, gbits, nullptr, a.sc, TT);
+            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mymask, umask, gbits, nullptr, a.sc, TT, dfr);
         }
-        if (l == 0) s_feas[g] = valid && !ghit && !(collide_on && a.sc.static_block);
+        const bool gdef = (__ballot(dfr) & gbits) != 0ull;
+        if (l == 0) {
+            s_feas[g] = valid && !ghit && !(collide_on && a.sc.static_block);
+            s_defer[g] = gdef;
+        }
     }
     __syncthreads();
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
@@ -1148,8 +1198,10 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             if (it < items && hi > lo) gb = (hi - lo >= 64) ? ~0ull : (((1ull << (hi - lo)) - 1ull) << lo);
             double q[D];
             eval_pt<D, P>(s_ctrl + s * ndof, otab + j * P1, ospan[j], q);
-            const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s], umask, gb, s_feas + s, a.sc, TT);
+            bool dfr = false;
+            const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s], umask, gb, s_feas + s, a.sc, TT, dfr);
             if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     // ---- phase 3: arc length (computeArcLength, include/sspp.h:152-169) of the listed
@@ -1205,13 +1257,19 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         const long long c = cand0 + tid;
         if (s_feas[tid]) C2F_STAT(8, 0);
         arc[c] = s_arc[tid];
-        feasible[c] = (unsigned char)(s_feas[tid] != 0);
+        // 2: no contact except cylinder-box pairs left undecided; k_sspp_cbfix writes 0 or 1
+        feasible[c] = (unsigned char)(s_feas[tid] == 0 ? 0 : (s_defer[tid] ? 2 : 1));
     }
     // block argmin over the workgroup's feasible candidates: one wave, lexicographic (cost, id)
-    // xor butterfly (exact, order independent: the lowest id wins ties like the serial scan)
+    // xor butterfly (exact, order independent: the lowest id wins ties like the serial scan).
+    // Undecided candidates stay out; k_sspp_cbfix merges the ones it clears.
     BlockBest bb;
     if (tid < 64) {
-        const bool f = tid < nvalid && s_feas[tid] != 0;
+        const bool und = tid < nvalid && s_feas[tid] != 0 && s_defer[tid] != 0;
+        const unsigned long long um = __ballot(und);
+        if (tid == 0 && um != 0ull)
+            __hip_atomic_fetch_add(a.dfr, (unsigned)__popcll(um), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool f = tid < nvalid && s_feas[tid] != 0 && !und;
         double bc = f ? s_arc[tid] : INFINITY;
         long long bi = f ? first_id + cand0 + tid : -1;
 #pragma unroll
@@ -1231,6 +1289,113 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         g_wg_t[4 * blockIdx.x + 3] = (unsigned long long)(long long)wg_ns;
     }
 #endif
+}
+
+// ---------------------------------------------------------------- undecided cylinder-box pairs
+// k_sspp_c2f leaves a cylinder-box pair that passes the bounding-sphere test undecided (the
+// exact test's registers would spill its whole pair loop).  A candidate with no other contact is
+// written as feasible = 2, kept out of the argmin and counted in dfr[0].  This kernel, queued
+// right after it on the same stream, gives each such candidate the exact test at every
+// collision waypoint: a contact makes it infeasible (arc +inf unless arc_all), otherwise it is
+// feasible and is merged into its step's records (block record and fused result, lexicographic
+// (cost, id) under the step's lock, count + 1), so the outputs equal a kernel that ran the exact
+// test inline.  With dfr[0] == 0 (every scene without such pairs near a path) each workgroup
+// returns after one scalar load.  The last workgroup to finish re-arms dfr.
+constexpr int kFixThreads = 256;
+constexpr int kFixBlocks = 64;
+template <int D, int NM, int P, bool ONEGEOM>
+__global__ __launch_bounds__(kFixThreads) void k_sspp_cbfix(
+    SsppC2F a, SceneT T, int steps, const double* __restrict__ otab, const int* __restrict__ ospan,
+    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
+    const double* __restrict__ ctrl_in, const double* __restrict__ pert, double* __restrict__ arc,
+    unsigned char* __restrict__ feasible, BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    if (__hip_atomic_load(a.dfr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int P1 = P + 1;
+    __shared__ int s_list[kFixThreads + 1];
+    __shared__ int s_hit;
+    const int tid = threadIdx.x, n = a.n, ndof = n * D;
+    double* s_ctrl = smem;  // [n][D]
+    const long long total = (long long)steps * a.B;
+    for (long long base = (long long)blockIdx.x * kFixThreads; base < total; base += (long long)gridDim.x * kFixThreads) {
+        const long long c0 = base + tid;
+        if (tid == 0) s_list[kFixThreads] = 0;
+        __syncthreads();
+        if (c0 < total && feasible[c0] == 2) s_list[atomicAdd(&s_list[kFixThreads], 1)] = tid;
+        __syncthreads();
+        const int nl = s_list[kFixThreads];
+        for (int i = 0; i < nl; ++i) {  // workgroup-uniform
+            const long long c = base + s_list[i];
+            const int step = (int)(c / a.B);
+            const long long cand = c - (long long)step * a.B;
+            const long long first_id = a.first_id + step * a.step_stride;
+            // the candidate's control points, exactly as k_sspp_c2f's prologue made them
+            const int npert = (n - 2 * P) * D;
+            for (int r = tid; r < ndof; r += kFixThreads) {
+                const int k = r - P * D;
+                double v = init_ctrl[r];
+                if (ctrl_in) v = ctrl_in[cand * ndof + r];
+                else if (pert && !a.insample && !(a.ablate & 1) && k >= 0 && k < npert)
+                    v = pert[((long long)step * a.B + cand) * npert + k];
+                s_ctrl[r] = v;
+            }
+            if (tid == 0) s_hit = 0;
+            __syncthreads();
+            if (!ctrl_in && a.insample && !(a.ablate & 1)) {
+                const int npairs = (npert + 1) >> 1;
+                for (int m = tid; m < npairs; m += kFixThreads) {
+                    double z0, z1;
+                    normal_pair(a.seed, (unsigned long long)(first_id + cand), (unsigned)m, 0u, &z0, &z1);
+                    double* cc = s_ctrl + P * D;
+                    const int k0 = 2 * m, k1 = 2 * m + 1;
+                    cc[k0] = cc[k0] + (a.sigma * z0) * limits[k0 % D];
+                    if (k1 < npert) cc[k1] = cc[k1] + (a.sigma * z1) * limits[k1 % D];
+                }
+                __syncthreads();
+            }
+            for (int j = tid; j < a.npts; j += kFixThreads) {
+                if (__hip_atomic_load(&s_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                if (cb_point_exact<D, NM, P, ONEGEOM>(s_ctrl, otab + j * P1, ospan[j], ~0ull, a.sc.npairs, T))
+                    __hip_atomic_store(&s_hit, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                if (s_hit) {
+                    feasible[c] = 0;
+                    if (!a.arc_all) arc[c] = INFINITY;
+                } else {
+                    feasible[c] = 1;
+                    const double cost = arc[c];
+                    const long long id = first_id + cand;
+                    unsigned* lock = &sync[step].top[1];
+                    while (atomicCAS(lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(2);
+                    __threadfence();
+                    BlockBest* pb = part + (long long)step * a.nblk_step + cand / a.cpb;
+                    BlockBest r = ld_rec(pb);
+                    if (better(cost, id, r.cost, r.idx)) { r.cost = cost; r.idx = id; }
+                    r.count += 1;
+                    st_rec(pb, r);
+                    if (best) {
+                        volatile sspp_best* o = best + step;
+                        if (better(cost, id, o->cost, o->index)) { o->cost = cost; o->index = id; }
+                        o->count = o->count + 1;
+                    }
+                    __threadfence();
+                    atomicExch(lock, 0u);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // the last workgroup re-arms the counters for the next launch on this job
+    if (tid == 0) {
+        __threadfence();
+        const unsigned prev = __hip_atomic_fetch_add(a.dfr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            __hip_atomic_store(a.dfr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.dfr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
@@ -1509,6 +1674,8 @@ struct sspp_job {
     int* d_ospan = nullptr;
     DPair* d_pairs = nullptr;  // this job's pair table (closest-to-the-mean-path first)
     ArgminSync* d_sync = nullptr;  // sharded arrival counters of the fused argmin [kMaxSteps]
+    unsigned* d_dfr = nullptr;     // k_sspp_c2f -> k_sspp_cbfix counters (SsppC2F::dfr)
+    int has_cb = 0;                // the pair table has cylinder-box pairs (k_sspp_cbfix runs)
     std::vector<double> h_knots;   // host copies: the knot vector, and the staging of
     std::vector<double> h_stage;   // sspp_job_update_sspp's asynchronous uploads (init | limits)
     std::vector<DPair> h_pairs;
@@ -1988,7 +2155,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
         }
         const int nm = j->nm < 1 ? 1 : j->nm;
         j->lds2 = sizeof(double) * ((size_t)j->cpb2 * (n * D + lanes_for(W - 1) / 64 + 1 + 6 * nm)) +
-                  sizeof(unsigned long long) * j->cpb2 + sizeof(int) * (2 * j->cpb2 + 1);
+                  sizeof(unsigned long long) * j->cpb2 + sizeof(int) * (3 * j->cpb2 + 1);
         if (j->lds2 > 64 * 1024) j->c2f = 0;
     }
     if (j->npert > 0 && !j->insample && j->c2f) {  // room for kMaxSteps steps, capped at 256 MiB
@@ -2003,9 +2170,16 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     // one record per workgroup and step: k_sspp has nblk workgroups per batch (one step per
     // launch), k_sspp_c2f ceil(max_batch / cpb2) per step and up to kMaxSteps steps per launch
     const int64_t nrec = std::max<int64_t>(nblk, ((max_batch + j->cpb2 - 1) / j->cpb2) * kMaxSteps);
+    if (scene)
+        for (const DPair& pr : scene->pairs) {
+            const int t1 = scene->geoms[pr.gm].type, t2 = pr.otype;
+            if ((t1 == 5 && t2 == 6) || (t1 == 6 && t2 == 5)) j->has_cb = 1;
+        }
     if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nrec) != hipSuccess ||
         hipMalloc((void**)&j->d_sync, sizeof(ArgminSync) * kMaxSteps) != hipSuccess ||
-        hipMemset(j->d_sync, 0, sizeof(ArgminSync) * kMaxSteps) != hipSuccess) {
+        hipMemset(j->d_sync, 0, sizeof(ArgminSync) * kMaxSteps) != hipSuccess ||
+        hipMalloc((void**)&j->d_dfr, sizeof(unsigned) * 2) != hipSuccess ||
+        hipMemset(j->d_dfr, 0, sizeof(unsigned) * 2) != hipSuccess) {
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
     }
@@ -2042,6 +2216,18 @@ static SceneT scene_t_job(const sspp_job* j) {
     return t;
 }
 
+// k_sspp_cbfix after the scoring launch, only when the job's pairs include cylinder-box ones
+template <int D, int NM, int P, bool OG>
+static hipError_t launch_cbfix(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                               hipStream_t st) {
+    if (!j->has_cb || !k.has_scene) return hipSuccess;
+    hipLaunchKernelGGL((k_sspp_cbfix<D, NM, P, OG>), dim3(kFixBlocks), dim3(kFixThreads),
+                       sizeof(double) * j->n * D, st, k, scene_t_job(j), nblk / k.nblk_step, j->d_otab,
+                       j->d_ospan, j->d_init, j->d_limits, o.ctrl_in, j->d_pert, o.arc, o.feasible,
+                       j->d_part, j->d_sync, o.best);
+    return hipGetLastError();
+}
+
 template <int D, int NM, int P, int NT>
 static hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
                                 hipStream_t st) {
@@ -2051,12 +2237,14 @@ static hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppP
         hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true, NT>), dim3(nblk), dim3(NT), j->lds2, st, k,
                            scene_t_job(j), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
                            o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
-        return hipGetLastError();
+        const hipError_t e = hipGetLastError();
+        return e != hipSuccess ? e : launch_cbfix<D, 1, P, true>(k, j, o, nblk, st);
     }
     hipLaunchKernelGGL((k_sspp_c2f<D, NM, P, false, NT>), dim3(nblk), dim3(NT), j->lds2, st, k,
                        scene_t_job(j), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
                        o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    return e != hipSuccess ? e : launch_cbfix<D, NM, P, false>(k, j, o, nblk, st);
 }
 
 template <int D, int NM, int P>
@@ -2163,6 +2351,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         c.step_stride = step_stride;
         c.arc_all = j->arc_all;
         c.hull = j->hull;
+        c.dfr = j->d_dfr;
         e = j->p == 3 ? dispatch_c2f_p<3>(c, j, o, nblk * steps, st) : dispatch_c2f_p<2>(c, j, o, nblk * steps, st);
     } else {
         e = j->p == 3 ? dispatch_sspp_p<3>(k, j, o, nblk, st) : dispatch_sspp_p<2>(k, j, o, nblk, st);
@@ -2348,6 +2537,7 @@ extern "C" void sspp_job_free(sspp_job* j) {
     if (j->d_part) (void)hipFree(j->d_part);
     if (j->d_pert) (void)hipFree(j->d_pert);
     if (j->d_sync) (void)hipFree(j->d_sync);
+    if (j->d_dfr) (void)hipFree(j->d_dfr);
     delete j;
 }
 

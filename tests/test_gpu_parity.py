@@ -203,6 +203,29 @@ def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1, nt):
     assert r["best"][1] == O.argmin(arc_o, feas_o)[0]
 
 
+@pytest.mark.parametrize("kernel,g1,nt", KERNELS)
+def test_cylinder_box_sspp(robocrane, monkeypatch, kernel, g1, nt):
+    """The block grazing the gripper's col_mount cylinder cap (and col_base box): k_sspp_c2f
+    decides cylinder-box pairs the 7 SAT axes leave open in phase 2b (exact, out of the pair
+    loop); feasibility, arcs and the argmin must equal the oracle's exact test."""
+    import sspp_amd as S
+    monkeypatch.setenv("SSPP_KERNEL", kernel)
+    monkeypatch.setenv("SSPP_G1", g1)
+    monkeypatch.setenv("SSPP_NT", nt)
+    _, scene, oscene = robocrane
+    start = np.array([1.8, 2.2, 0.656, 1, 0, 0, 0])
+    end = np.array([2.2, 2.2, 0.656, 1, 0, 0, 0])
+    knots, ctrl0 = linear_init(start, end, 10)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.01, np.array([1, 1, 1, .2, .2, .2, .2]), 128,
+                    seed=11, max_batch=2048)
+    r = run_sspp(job, 2048)
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 128)
+    np.testing.assert_array_equal(r["feasible"], feas_o)
+    assert 0 < feas_o.sum() < 2048
+    assert arc_err(r["arc"], arc_o) <= COST_TOL
+    assert r["best"][1] == O.argmin(arc_o, feas_o)[0]
+
+
 @pytest.mark.parametrize("kernel", ["0", "1"])
 @pytest.mark.parametrize("insample", [0, 1])
 def test_fused_argmin_back_to_back(robocrane, monkeypatch, insample, kernel):
