@@ -30,6 +30,10 @@ __device__ unsigned long long g_c2f_stats[16];
 #endif
 #ifdef SSPP_WG_TIMING  // profiling builds only: per-workgroup (start, end, CU, survivors) of k_sspp_c2f
 __device__ unsigned long long g_wg_t[1 << 18];
+__device__ unsigned long long g_wg_ph[6 << 16];  // per workgroup: shader clock after each phase
+#define WG_PH(k) do { if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_wg_ph[6 * blockIdx.x + (k)] = clock64(); } while (0)
+#else
+#define WG_PH(k) do { } while (0)
 #endif
 #include "sspp_device.h"
 
@@ -992,6 +996,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     const unsigned long long wg_t0 = wall_clock64();
     int wg_ns = -1;
 #endif
+    WG_PH(0);
     if (step) {
         arc += step * a.B;
         feasible += step * a.B;
@@ -1058,6 +1063,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         double* dst = ctrl_out + cand0 * ndof;
         for (int e = tid; e < nvalid * ndof; e += NT) dst[e] = s_ctrl[e];
     }
+    WG_PH(1);
 
     const SceneT TT = T;
     const bool collide_on = a.has_scene && !(a.ablate & 2);
@@ -1132,6 +1138,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
     }
     __syncthreads();
+    WG_PH(2);
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
     const int R = a.npts - a.n1;
     if (collide_on && R > 0 && !(a.ablate & 8)) {
@@ -1204,6 +1211,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
+    WG_PH(3);
     // ---- phase 3: arc length (computeArcLength, include/sspp.h:152-169) of the listed
     // candidates: the collision-free ones (findBestPath scores only successful paths), or all
     // of them with arc_all.  Chords v_j -> v_{j+1} (v_i = s(i/(W-1))) go to LDS, then each
@@ -1252,6 +1260,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
     }
     __syncthreads();
+    WG_PH(4);
     if (tid == 0) C2F_STAT(7, nvalid);
     if (tid < nvalid) {
         const long long c = cand0 + tid;
@@ -1281,6 +1290,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         bb.cost = bi < 0 ? INFINITY : bc; bb.idx = bi; bb.count = __popcll(__ballot(f)); bb.pad = 0;
     }
     finish_batch<NT>(bb, part, sync, best, a.nblk_step, blk);
+    WG_PH(5);
 #ifdef SSPP_WG_TIMING
     if (tid == 0 && blockIdx.x < (1 << 16)) {
         g_wg_t[4 * blockIdx.x] = wg_t0;
@@ -2124,10 +2134,12 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : (j->c2f ? 1 : 0); }
     { const char* e = getenv("SSPP_HULL"); j->hull = e ? atoi(e) : 2; }
     {
-        // defaults measured on MI355X (robocrane, 8 steps/launch, 4 streams): one-wave
-        // workgroups of 8 candidates x 8 phase-1 lanes — 1.12 G cand/s vs 0.69 G for 256 x 16
+        // defaults measured on MI355X (robocrane, 32 steps/launch, 4 streams):
+        // one-wave workgroups of 16 candidates x 4 phase-1 lanes — 1.84 G cand/s against 1.56 G
+        // for 8 x 8 and 1.40 G for 256 x 8 (the kernel is VALU-issue bound: fewer lanes per
+        // candidate waste fewer pair-loop iterations on lanes that have already hit)
         const char* e = getenv("SSPP_G1");
-        int g1 = e ? atoi(e) : 8;
+        int g1 = e ? atoi(e) : 4;
         if (g1 != 4 && g1 != 8 && g1 != 16 && g1 != 32 && g1 != 64) g1 = 8;
         const char* t = getenv("SSPP_NT");
         int nt = t ? atoi(t) : 64;
@@ -2639,6 +2651,11 @@ extern "C" int sspp_debug_c2f_stats(unsigned long long* out, int reset) {
 extern "C" int sspp_debug_wg_times(unsigned long long* out, int n) {
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_t), sizeof(unsigned long long) * (size_t)n);
+    return 0;
+}
+extern "C" int sspp_debug_wg_phases(unsigned long long* out, int n) {
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_ph), sizeof(unsigned long long) * (size_t)n);
     return 0;
 }
 #endif

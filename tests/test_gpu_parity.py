@@ -57,7 +57,7 @@ def run_sspp(job, B, first=0, with_ctrl=True):
 
 # scoring kernels: (SSPP_KERNEL, SSPP_G1) — coarse-to-fine k_sspp_c2f with several phase-1
 # lane-group sizes, and the one-waypoint-per-lane k_sspp
-KERNELS = [("1", "8", "64"), ("1", "16", "256"), ("1", "4", "256"), ("1", "64", "64"),
+KERNELS = [("1", "4", "64"), ("1", "8", "64"), ("1", "16", "256"), ("1", "4", "256"), ("1", "64", "64"),
            ("1", "16", "128"), ("1", "16", "64"), ("0", "16", "256")]
 
 

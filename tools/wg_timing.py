@@ -25,7 +25,7 @@ run(5)
 torch.cuda.synchronize()
 run(steps)
 torch.cuda.synchronize()
-nwg = steps * 512
+nwg = steps * (B // (64 // int(os.environ.get("SSPP_G1", "4"))))  # NT = 64: cpb = 64 / G1
 buf = (C.c_ulonglong * (4 * nwg))()
 _lib.lib().__getattr__("sspp_debug_wg_times")(buf, 4 * nwg)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 4).astype(np.int64)
@@ -42,6 +42,14 @@ res = {"workgroups": int(nwg), "span_us": float(en.max()),
        "end_us_pcts": {p: float(np.percentile(en, p)) for p in (10, 50, 90, 99, 100)},
        "last_20_end": [[float(st[i]), float(en[i]), int(ns[i])] for i in np.argsort(en)[-20:]],
        "concurrency_at": {t: int(((st <= t) & (en > t)).sum()) for t in (5, 10, 20, 40, 60, 80)}}
+ph = (C.c_ulonglong * (6 * nwg))()
+_lib.lib().__getattr__("sspp_debug_wg_phases")(ph, 6 * nwg)
+ph = np.frombuffer(ph, dtype=np.uint64).reshape(nwg, 6).astype(np.int64)
+d = np.diff(ph, axis=1)  # shader clocks: sampling+ctrl, hull(1)+phase 1, phase 2 (+hull 2), arc, epilogue
+names = ["prologue_sampling", "phase1", "phase2", "phase3_arc", "epilogue_argmin"]
+res["phase_clocks_mean"] = {n: float(d[:, i].mean()) for i, n in enumerate(names)}
+res["phase_clocks_by_survivors"] = {int(k): {n: float(d[ns == k, i].mean()) for i, n in enumerate(names)}
+                                    for k in np.unique(ns)}
 print(json.dumps(res, indent=1))
 if out_path:
     json.dump(res, open(out_path, "w"), indent=1)
