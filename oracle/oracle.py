@@ -66,6 +66,7 @@ def lib():
         L.or_py_bspline.argtypes = [C.c_double, _d, C.c_int, _d, C.c_int, C.c_int, _d]
         L.or_normal_pair.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
                                      C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.or_normal_quad.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, _d]
         L.or_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                        C.POINTER(C.c_uint32)]
         L.or_sample_sspp.argtypes = [_d, C.c_int, C.c_int, C.c_int, C.c_double, _d, C.c_uint64,
@@ -160,6 +161,13 @@ def philox(ctr, key):
     o = (C.c_uint32 * 4)()
     lib().or_philox4x32_10(c, k, o)
     return list(o)
+
+
+def normal_quad(seed, cand, idx, stream):
+    """The SamplingPathPlanner sampler's four FP32 Box-Muller normals of one Philox call."""
+    z = np.zeros(4)
+    lib().or_normal_quad(seed, cand, idx, stream, z)
+    return z
 
 
 def normal_pair(seed, cand, idx, stream):

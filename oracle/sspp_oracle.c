@@ -294,6 +294,58 @@ void or_normal_pair(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream,
     *z1 = r * sn;
 }
 
+/* SamplingPathPlanner normals: the kernels' normal_quad (sspp_amd/csrc/sspp_kernels.hip), the
+   same FP32 operations in the same order (explicit fmaf, correctly rounded division and sqrtf,
+   round-half-even rintf), so the result is bit-identical: one Philox4x32-10 call -> four
+   24-bit uniforms -> two Box-Muller pairs; ln u by the atanh series on the mantissa, sin / cos
+   of 2 pi u after an exact quarter-turn reduction. */
+static float bm_log(float u) {
+    uint32_t bits;
+    memcpy(&bits, &u, 4);
+    int e = (int)(bits >> 23) - 127;
+    uint32_t mb = (bits & 0x7fffffu) | 0x3f800000u;
+    float m;
+    memcpy(&m, &mb, 4);
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    const float s = (m - 1.0f) / (m + 1.0f);
+    const float s2 = s * s;
+    float p = fmaf(s2, 0.111111111f, 0.142857143f);
+    p = fmaf(s2, p, 0.2f);
+    p = fmaf(s2, p, 0.333333333f);
+    p = fmaf(s2, p, 1.0f);
+    return fmaf((float)e, 0.693147181f, (s + s) * p);
+}
+static void bm_sincos2pi(float u, float* sn, float* cs) {
+    const float q = rintf(4.0f * u);
+    const float r = fmaf(-0.25f, q, u);
+    const float a = r * 6.28318531f;
+    const float a2 = a * a;
+    float sp = fmaf(a2, 2.75573192e-6f, -1.98412698e-4f);
+    sp = fmaf(a2, sp, 8.33333333e-3f);
+    sp = fmaf(a2, sp, -0.166666667f);
+    const float sa = fmaf(a * a2, sp, a);
+    float cp = fmaf(a2, 2.48015873e-5f, -1.38888889e-3f);
+    cp = fmaf(a2, cp, 4.16666667e-2f);
+    cp = fmaf(a2, cp, -0.5f);
+    const float ca = fmaf(a2, cp, 1.0f);
+    const int qi = (int)q & 3;
+    *sn = qi == 0 ? sa : (qi == 1 ? ca : (qi == 2 ? -sa : -ca));
+    *cs = qi == 0 ? ca : (qi == 1 ? -sa : (qi == 2 ? -ca : sa));
+}
+void or_normal_quad(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream, double z[4]) {
+    uint32_t o[4];
+    philox_words(seed, cand, idx, stream, o);
+    for (int h = 0; h < 2; ++h) {
+        const float u1 = (float)((o[2 * h] >> 8) + 1u) * 5.96046448e-8f;
+        const float u2 = (float)(o[2 * h + 1] >> 8) * 5.96046448e-8f;
+        const float r = sqrtf(-2.0f * bm_log(u1));
+        float sn, cs;
+        bm_sincos2pi(u2, &sn, &cs);
+        z[2 * h] = (double)(r * cs);
+        z[2 * h + 1] = (double)(r * sn);
+    }
+}
+
 static double uniform01(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream) {
     uint32_t o[4];
     philox_words(seed, cand, idx, stream, o);
@@ -312,9 +364,9 @@ void or_sample_sspp(const double* init_ctrl, int n, int D, int p, double sigma,
         for (int j = p; j < n - p; ++j) {
             for (int d = 0; d < D; ++d) {
                 int k = (j - p) * D + d;
-                double z0, z1;
-                or_normal_pair(seed, g, (uint32_t)(k >> 1), 0u, &z0, &z1);
-                double z = (k & 1) ? z1 : z0;
+                double zq[4];
+                or_normal_quad(seed, g, (uint32_t)(k >> 2), 0u, zq);
+                double z = zq[k & 3];
                 double noise = (sigma * z) * limits[d];
                 c[(size_t)j * D + d] = c[(size_t)j * D + d] + noise;
             }

@@ -87,6 +87,7 @@ void   or_py_bspline(double theta, const double* t, int nt, const double* c /* [
 
 /* ---- counter-based RNG (replaces std::default_random_engine) ---- */
 void   or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+void   or_normal_quad(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream, double z[4]);
 void   or_normal_pair(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream,
                       double* z0, double* z1);
 /* sampleWithNoise for candidates [first, first+B): ctrl_out [B][n][D] */

@@ -252,6 +252,57 @@ __device__ __forceinline__ void normal_pair(unsigned long long seed, unsigned lo
     *z0 = r * cs;
     *z1 = r * sn;
 }
+// SamplingPathPlanner normals (sampleWithNoise): one Philox4x32-10 call gives four 24-bit
+// uniforms -> two Box-Muller pairs in FP32, with fmaf polynomials written out (ln u by the atanh
+// series on the mantissa, sin / cos of 2 pi u after an exact quarter-turn reduction) and a
+// correctly rounded sqrtf, so oracle/sspp_oracle.c::or_normal_quad reproduces it bit for bit.
+// Four normals per Philox call and FP32 instead of FP64 log / sincospi: the FP64 sampler was
+// the largest phase of k_sspp_c2f (24 of 62 kclk per workgroup, tools/wg_timing.py).
+__device__ __forceinline__ float bm_log(float u) {  // ln u, u in [2^-24, 1]
+    const unsigned bits = __float_as_uint(u);
+    int e = (int)(bits >> 23) - 127;
+    float m = __uint_as_float((bits & 0x7fffffu) | 0x3f800000u);  // [1, 2)
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    const float s = (m - 1.0f) / (m + 1.0f);                      // |s| <= 0.1716
+    const float s2 = s * s;
+    float p = fmaf(s2, 0.111111111f, 0.142857143f);
+    p = fmaf(s2, p, 0.2f);
+    p = fmaf(s2, p, 0.333333333f);
+    p = fmaf(s2, p, 1.0f);
+    return fmaf((float)e, 0.693147181f, (s + s) * p);
+}
+__device__ __forceinline__ void bm_sincos2pi(float u, float* sn, float* cs) {  // u in [0, 1)
+    const float q = rintf(4.0f * u);
+    const float r = fmaf(-0.25f, q, u);  // exact
+    const float a = r * 6.28318531f;     // |a| <= pi / 4
+    const float a2 = a * a;
+    float sp = fmaf(a2, 2.75573192e-6f, -1.98412698e-4f);
+    sp = fmaf(a2, sp, 8.33333333e-3f);
+    sp = fmaf(a2, sp, -0.166666667f);
+    const float sa = fmaf(a * a2, sp, a);
+    float cp = fmaf(a2, 2.48015873e-5f, -1.38888889e-3f);
+    cp = fmaf(a2, cp, 4.16666667e-2f);
+    cp = fmaf(a2, cp, -0.5f);
+    const float ca = fmaf(a2, cp, 1.0f);
+    const int qi = (int)q & 3;
+    *sn = qi == 0 ? sa : (qi == 1 ? ca : (qi == 2 ? -sa : -ca));
+    *cs = qi == 0 ? ca : (qi == 1 ? -sa : (qi == 2 ? -ca : sa));
+}
+__device__ __forceinline__ void normal_quad(unsigned long long seed, unsigned long long g,
+                                            unsigned idx, unsigned stream, double z[4]) {
+    unsigned o[4];
+    philox_words(seed, g, idx, stream, o);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const float u1 = (float)((o[2 * h] >> 8) + 1u) * 5.96046448e-8f;  // (0, 1], exact
+        const float u2 = (float)(o[2 * h + 1] >> 8) * 5.96046448e-8f;     // [0, 1), exact
+        const float r = sqrtf(-2.0f * bm_log(u1));
+        float sn, cs;
+        bm_sincos2pi(u2, &sn, &cs);
+        z[2 * h] = (double)(r * cs);
+        z[2 * h + 1] = (double)(r * sn);
+    }
+}
 __device__ __forceinline__ double uniform01(unsigned long long seed, unsigned long long g,
                                             unsigned idx, unsigned stream) {
     unsigned o[4];
@@ -621,24 +672,20 @@ __global__ __launch_bounds__(kBlock) void k_sample_sspp(
     unsigned long long seed, long long first_id, long long step_stride, long long B, int steps,
     int D, int p, int npert, double sigma, const double* __restrict__ init_ctrl,
     const double* __restrict__ limits, double* __restrict__ pert) {
-    const int npairs = (npert + 1) >> 1;
+    const int nq = (npert + 3) >> 2;
     const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= (long long)steps * B * npairs) return;
-    const long long sb = t / npairs;
-    const int m = (int)(t - sb * npairs);
+    if (t >= (long long)steps * B * nq) return;
+    const long long sb = t / nq;
+    const int m = (int)(t - sb * nq);
     const long long s = sb / B, b = sb - s * B;
-    double z0, z1;
-    normal_pair(seed, (unsigned long long)(first_id + s * step_stride + b), (unsigned)m, 0u, &z0, &z1);
+    double z[4];
+    normal_quad(seed, (unsigned long long)(first_id + s * step_stride + b), (unsigned)m, 0u, z);
     const double* base = init_ctrl + p * D;
     double* out = pert + sb * npert;
-    const int k0 = 2 * m, k1 = 2 * m + 1;
-    {
-        const double noise = (sigma * z0) * limits[k0 % D];
-        out[k0] = base[k0] + noise;
-    }
-    if (k1 < npert) {
-        const double noise = (sigma * z1) * limits[k1 % D];
-        out[k1] = base[k1] + noise;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int k = 4 * m + h;
+        if (k < npert) out[k] = base[k] + (sigma * z[h]) * limits[k % D];
     }
 }
 
@@ -695,21 +742,17 @@ __global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
         }
         if (a.insample) {
             __syncthreads();
-            const int npairs = (npert + 1) >> 1;
-            for (int e = tid; e < cpb * npairs; e += kBlock) {
-                const int sl = e / npairs, m = e - sl * npairs;
+            const int nq = (npert + 3) >> 2;
+            for (int e = tid; e < cpb * nq; e += kBlock) {
+                const int sl = e / nq, m = e - sl * nq;
                 if (sl >= nvalid) continue;
-                double z0, z1;
-                normal_pair(a.seed, (unsigned long long)(a.first_id + cand0 + sl), (unsigned)m, 0u, &z0, &z1);
+                double z[4];
+                normal_quad(a.seed, (unsigned long long)(a.first_id + cand0 + sl), (unsigned)m, 0u, z);
                 double* c = s_ctrl + sl * ndof + P * D;
-                const int k0 = 2 * m, k1 = 2 * m + 1;
-                {
-                    const double noise = (a.sigma * z0) * limits[k0 % D];
-                    c[k0] = c[k0] + noise;
-                }
-                if (k1 < npert) {
-                    const double noise = (a.sigma * z1) * limits[k1 % D];
-                    c[k1] = c[k1] + noise;
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const int k = 4 * m + h;
+                    if (k < npert) c[k] = c[k] + (a.sigma * z[h]) * limits[k % D];
                 }
             }
         }
@@ -1015,12 +1058,11 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     int* s_surv = s_feas + cpb;                               // [cpb + 1] (last = count)
     int* s_defer = s_surv + cpb + 1;                          // [cpb] undecided cylinder-box pair
 
-    // ---- prologue: control points (+ sampleWithNoise) in LDS.  Element e = sl * ndof + r is
-    // walked with one division up front and add-with-carry afterwards.
+    // ---- prologue: control points (+ sampleWithNoise) in LDS.
     {
-        const int dsl = NT / ndof, dr = NT - dsl * ndof;
-        int sl = tid / ndof, r = tid - sl * ndof;
-        if (ctrl_in) {
+        if (ctrl_in) {  // element e = sl * ndof + r walked with add-with-carry
+            const int dsl = NT / ndof, dr = NT - dsl * ndof;
+            int sl = tid / ndof, r = tid - sl * ndof;
             const double* src = ctrl_in + cand0 * ndof;
             for (; sl < nvalid; sl += dsl) {
                 s_ctrl[sl * ndof + r] = src[sl * ndof + r];
@@ -1028,34 +1070,52 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
                 if (r >= ndof) { r -= ndof; ++sl; }
             }
         } else {
+            // lane-owned columns: the initial spline's value is loaded once per column and
+            // stored for every candidate (LDS stores only, no load latency per element)
             const int npert = (n - 2 * P) * D;
             const bool from_pert = !a.insample && !(a.ablate & 1);
-            for (; sl < cpb; sl += dsl) {
-                const int k = r - P * D;
-                s_ctrl[sl * ndof + r] = (from_pert && k >= 0 && k < npert && sl < nvalid)
-                                            ? pert[(cand0 + sl) * npert + k]
-                                            : init_ctrl[r];
-                r += dr;
-                if (r >= ndof) { r -= ndof; ++sl; }
+            for (int rr = tid; rr < ndof; rr += NT) {
+                const double v0 = init_ctrl[rr];
+                const int k = rr - P * D;
+                const bool pr = from_pert && k >= 0 && k < npert;
+                for (int s2 = 0; s2 < cpb; ++s2)
+                    s_ctrl[s2 * ndof + rr] = (pr && s2 < nvalid) ? pert[(cand0 + s2) * npert + k] : v0;
             }
         }
     }
     if (tid < cpb) s_mask[tid] = 0ull;
     __syncthreads();
     if (!ctrl_in && a.insample && !(a.ablate & 1)) {
+        // sampleWithNoise: item t = (candidate sl, Philox quad m: normals 4m .. 4m+3).  kUnr
+        // items per lane are drawn in straight-line code (ids past the end clamped, results
+        // dropped), so the scheduler interleaves their independent chains
+        constexpr int kUnr = 2;
         const int npert = (n - 2 * P) * D;
-        const int npairs = (npert + 1) >> 1;
-        const int dsl = NT / npairs, dm = NT - dsl * npairs;
-        int sl = tid / npairs, m = tid - sl * npairs;
-        for (; sl < nvalid; sl += dsl) {
-            double z0, z1;
-            normal_pair(a.seed, (unsigned long long)(first_id + cand0 + sl), (unsigned)m, 0u, &z0, &z1);
-            double* c = s_ctrl + sl * ndof + P * D;
-            const int k0 = 2 * m, k1 = 2 * m + 1;
-            c[k0] = c[k0] + (a.sigma * z0) * limits[k0 % D];
-            if (k1 < npert) c[k1] = c[k1] + (a.sigma * z1) * limits[k1 % D];
-            m += dm;
-            if (m >= npairs) { m -= npairs; ++sl; }
+        const int nq = (npert + 3) >> 2;
+        const int total = nvalid * nq;
+        const int dsl = NT / nq, dm = NT - dsl * nq;
+        int sl = tid / nq, m = tid - sl * nq;
+        for (int base = 0; base < total; base += kUnr * NT) {  // workgroup-uniform
+            double z[kUnr][4];
+            int usl[kUnr], um[kUnr];
+#pragma unroll
+            for (int u = 0; u < kUnr; ++u) {
+                usl[u] = sl; um[u] = m;
+                const int csl = sl < nvalid ? sl : 0;
+                normal_quad(a.seed, (unsigned long long)(first_id + cand0 + csl), (unsigned)m, 0u, z[u]);
+                m += dm; sl += dsl;
+                if (m >= nq) { m -= nq; ++sl; }
+            }
+#pragma unroll
+            for (int u = 0; u < kUnr; ++u) {
+                if (base + u * NT + tid >= total) continue;
+                double* c = s_ctrl + usl[u] * ndof + P * D;
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const int k = 4 * um[u] + h;
+                    if (k < npert) c[k] = c[k] + (a.sigma * z[u][h]) * limits[k % D];
+                }
+            }
         }
         __syncthreads();
     }
@@ -1352,14 +1412,15 @@ __global__ __launch_bounds__(kFixThreads) void k_sspp_cbfix(
             if (tid == 0) s_hit = 0;
             __syncthreads();
             if (!ctrl_in && a.insample && !(a.ablate & 1)) {
-                const int npairs = (npert + 1) >> 1;
-                for (int m = tid; m < npairs; m += kFixThreads) {
-                    double z0, z1;
-                    normal_pair(a.seed, (unsigned long long)(first_id + cand), (unsigned)m, 0u, &z0, &z1);
+                const int nq = (npert + 3) >> 2;
+                for (int m = tid; m < nq; m += kFixThreads) {
+                    double z[4];
+                    normal_quad(a.seed, (unsigned long long)(first_id + cand), (unsigned)m, 0u, z);
                     double* cc = s_ctrl + P * D;
-                    const int k0 = 2 * m, k1 = 2 * m + 1;
-                    cc[k0] = cc[k0] + (a.sigma * z0) * limits[k0 % D];
-                    if (k1 < npert) cc[k1] = cc[k1] + (a.sigma * z1) * limits[k1 % D];
+                    for (int h = 0; h < 4; ++h) {
+                        const int k = 4 * m + h;
+                        if (k < npert) cc[k] = cc[k] + (a.sigma * z[h]) * limits[k % D];
+                    }
                 }
                 __syncthreads();
             }
@@ -2343,7 +2404,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     const int nblk = (int)((B + cpb - 1) / cpb);
     hipStream_t st = (hipStream_t)stream;
     if (!d_ctrl && j->npert > 0 && !j->insample) {  // sampleWithNoise over the whole chip
-        const long long work = (long long)steps * B * (long long)((j->npert + 1) / 2);
+        const long long work = (long long)steps * B * (long long)((j->npert + 3) / 4);
         hipLaunchKernelGGL(k_sample_sspp, dim3((unsigned)((work + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                            (unsigned long long)j->seed, (long long)first_id, (long long)step_stride,
                            (long long)B, steps, j->D, j->p, j->npert, j->sigma, j->d_init, j->d_limits,

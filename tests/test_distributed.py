@@ -38,7 +38,7 @@ def _worker(rank, world, port, q):
     scene, knots, ctrl0 = _problem()
     per = B_ // world
     first = rank * per
-    ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 11, first, per)
+    ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 12, first, per)
     arc, feas = O.sspp_score(scene, knots, 3, ctrl, W_, nthreads=1)
     idx, cost = O.argmin(arc, feas)
     rec = torch.tensor([np.float64(cost).view(np.int64), idx + first if idx >= 0 else -1,
@@ -64,7 +64,7 @@ def test_sharded_argmin_equals_global(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     scene, knots, ctrl0 = _problem()
-    ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 11, 0, B_)
+    ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 12, 0, B_)
     arc, feas = O.sspp_score(scene, knots, 3, ctrl, W_, nthreads=1)
     idx, cost = O.argmin(arc, feas)
     assert feas.any() and not feas.all()

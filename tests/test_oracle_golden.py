@@ -120,6 +120,19 @@ def test_normal_sampler_statistics():
     assert abs(z.std() - 1.0) < 0.03
 
 
+def test_normal_quad_statistics():
+    """FP32 Box-Muller quads (SamplingPathPlanner sampler): moments, tails and the pairing."""
+    z = np.array([O.normal_quad(11, g, m, 0) for g in range(20000) for m in range(2)]).ravel()
+    assert abs(z.mean()) < 0.01
+    assert abs(z.std() - 1.0) < 0.01
+    assert abs(np.mean(z ** 4) - 3.0) < 0.1  # Gaussian kurtosis
+    assert 5.0 < np.abs(z).max() < 5.8       # u1 >= 2^-24: |z| <= sqrt(-2 ln 2^-24) = 5.77
+    for q in (0.5, 0.8413, 0.9772):          # CDF at 0, 1, 2 sigma
+        x = {0.5: 0.0, 0.8413: 1.0, 0.9772: 2.0}[q]
+        assert abs((z < x).mean() - q) < 0.01
+    assert abs(np.corrcoef(z[0::4], z[1::4])[0, 1]) < 0.02
+
+
 def test_sample_sspp_rule():
     """sampleWithNoise perturbs only columns j in [p, n-p) (include/sspp.h:121-127)."""
     init = np.arange(70.0).reshape(10, 7)
