@@ -301,12 +301,14 @@ class SsppSteps:
         self._A = (C.c_void_p * nb)(*[_ptr(a).value for a in arc_bufs])
         self._F = (C.c_void_p * nb)(*[_ptr(f).value for f in feas_bufs])
         self.nb, self.B, self.spl = nb, int(B), int(steps_per_launch)
+        self._fn = lib().sspp_steps_enqueue_sspp
 
     def enqueue(self, nsteps, first_id, step_stride, best=None):
-        """best: None or an (nsteps, 4) int64 device tensor for the per-step argmin records."""
-        check(lib().sspp_steps_enqueue_sspp(self._J, self.nb, self._S, self.B, int(nsteps),
-                                            self.spl, int(first_id), int(step_stride), self._A,
-                                            self._F, _ptr(best)), "steps enqueue")
+        """best: None, an (nsteps, 4) int64 device tensor for the per-step argmin records, or
+        that tensor's device address as an int (callers in a timed loop cache it)."""
+        bp = best if (best is None or isinstance(best, int)) else best.data_ptr()
+        check(self._fn(self._J, self.nb, self._S, self.B, nsteps, self.spl, first_id, step_stride,
+                       self._A, self._F, bp), "steps enqueue")
 
 
 class CesPlanner:

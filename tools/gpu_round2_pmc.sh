@@ -20,5 +20,9 @@ for c in stacking multigoal; do
   run $c/pmc_write WRITE_SIZE --config $c $TS
   run $c/p1 "$F64" --config $c $TS
 done
+C4="--batch 32768 --waypoints 256 --steps 64 --warmup 4 --roofline-launches 10"
+run robocrane_b32768_w256/pmc_fetch FETCH_SIZE $C4
+run robocrane_b32768_w256/pmc_write WRITE_SIZE $C4
+run robocrane_b32768_w256/p1 "$F64" $C4
 run robocrane/occ/p1 "$OCC" $RC
 echo DONE
