@@ -1050,10 +1050,14 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         if (best) best += step;
     }
     double* s_ctrl = smem;                                    // [cpb][n][D]
-    double* s_vsum = s_ctrl + cpb * ndof;                     // [cpb][lpc/64]
-    double* s_arc = s_vsum + cpb * (a.lpc >> 6);              // [cpb]
-    double* s_box = s_arc + cpb;                              // [cpb][2][NB]
-    unsigned long long* s_mask = (unsigned long long*)(s_box + cpb * 2 * NB);  // [cpb]
+    // s_box is dead once phase 2's hull masks are built (a barrier follows), so phase 3's
+    // s_vsum / s_arc reuse its space: 384 B less per 16-candidate workgroup, which lets LDS
+    // hold 16 workgroups per CU instead of 14
+    const int nvw3 = a.lpc >> 6, rbox = 2 * NB > nvw3 + 1 ? 2 * NB : nvw3 + 1;
+    double* s_box = s_ctrl + cpb * ndof;                      // [cpb][2][NB] (hull)
+    double* s_vsum = s_box;                                   // [cpb][lpc/64] (phase 3)
+    double* s_arc = s_box + cpb * nvw3;                       // [cpb] (phase 3, outputs)
+    unsigned long long* s_mask = (unsigned long long*)(s_box + cpb * rbox);  // [cpb]
     int* s_feas = (int*)(s_mask + cpb);                       // [cpb]
     int* s_surv = s_feas + cpb;                               // [cpb + 1] (last = count)
     int* s_defer = s_surv + cpb + 1;                          // [cpb] undecided cylinder-box pair
@@ -2227,7 +2231,8 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
             }
         }
         const int nm = j->nm < 1 ? 1 : j->nm;
-        j->lds2 = sizeof(double) * ((size_t)j->cpb2 * (n * D + lanes_for(W - 1) / 64 + 1 + 6 * nm)) +
+        const int rbox = std::max(6 * nm, lanes_for(W - 1) / 64 + 1);  // k_sspp_c2f: s_box / s_vsum + s_arc
+        j->lds2 = sizeof(double) * ((size_t)j->cpb2 * (n * D + rbox)) +
                   sizeof(unsigned long long) * j->cpb2 + sizeof(int) * (3 * j->cpb2 + 1);
         if (j->lds2 > 64 * 1024) j->c2f = 0;
     }
