@@ -20,7 +20,9 @@ PYMOD2   = sspp/_tsp$(PYEXT)
 PYINC    = $(shell $(PY) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
 PBINC    = $(shell $(PY) -c "import pybind11;print(pybind11.get_include())")
 
-HDRS = include/sspp_hip.h $(SRC)/model.h $(SRC)/sspp_device.h $(SRC)/xml_lite.h
+HDRS = include/sspp_hip.h $(SRC)/model.h $(SRC)/sspp_device.h $(SRC)/xml_lite.h $(SRC)/sspp_kern.h
+# kernel instantiations, one translation unit per dof (+ 0: TaskSpacePlanner), compiled in parallel
+INST = $(foreach d,0 1 2 3 4 6 7 9,$(OBJDIR)/sspp_inst_d$(d).o)
 
 all: $(LIB) $(PYMOD) $(PYMOD2) oracle
 
@@ -32,7 +34,11 @@ $(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(OBJDIR)/sspp_kernels.o $(OBJDIR)/ces.o $(OBJDIR)/planner.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o
+$(OBJDIR)/sspp_inst_d%.o: $(SRC)/sspp_inst.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -DSSPK_D=$* -c $< -o $@
+
+$(LIB): $(OBJDIR)/sspp_kernels.o $(INST) $(OBJDIR)/ces.o $(OBJDIR)/planner.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 

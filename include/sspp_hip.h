@@ -133,6 +133,9 @@ typedef struct sspp_sspp_args {
     int arc_all;            /* 0 (reference): arc length only for collision-free candidates
                                (findBestPath, include/sspp.h:171-192), +inf for the others;
                                1: arc length for every candidate                         */
+    int sampler;            /* 0 (default): FP64 Box-Muller normals, as the reference's
+                               std::normal_distribution<double> (include/sspp.h:116,125);
+                               1: opt-in FP32 Box-Muller quads (faster, |z| <= 5.77)     */
 } sspp_sspp_args;
 
 typedef struct sspp_tsp_args {
@@ -332,6 +335,11 @@ int sspp_score_ctrl_host(const sspp_scene* scene, const double* knots, int degre
 int sspp_sample_ctrl_host(const double* knots, int degree, const double* init_ctrl, int n, int D,
                           double sigma, const double* limits, uint64_t seed, int64_t first_id,
                           int64_t B, double* ctrl_out /* [B][n][D] */);
+
+/* ---- diagnostics ---- */
+/* spin-timeout word of a job's work-queue kernel: 0 = every wait of its in-launch hand-off was
+ * satisfied (tests assert this); synchronous */
+int sspp_debug_job_error(const sspp_job* job);
 
 #ifdef __cplusplus
 }

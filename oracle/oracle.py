@@ -66,11 +66,12 @@ def lib():
         L.or_py_bspline.argtypes = [C.c_double, _d, C.c_int, _d, C.c_int, C.c_int, _d]
         L.or_normal_pair.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
                                      C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.or_normal_pair_libm.argtypes = L.or_normal_pair.argtypes
         L.or_normal_quad.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, _d]
         L.or_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                        C.POINTER(C.c_uint32)]
         L.or_sample_sspp.argtypes = [_d, C.c_int, C.c_int, C.c_int, C.c_double, _d, C.c_uint64,
-                                     C.c_int64, C.c_int64, _d]
+                                     C.c_int64, C.c_int64, _d, C.c_int]
         L.or_sample_tsp.argtypes = [_d, _d, C.c_int, _d, _d, C.c_double, C.c_uint64, C.c_int64,
                                     C.c_int64, _d]
         L.or_point_contacts.argtypes = [C.c_void_p, _d, C.c_int, C.POINTER(C.c_double),
@@ -170,18 +171,26 @@ def normal_quad(seed, cand, idx, stream):
     return z
 
 
-def normal_pair(seed, cand, idx, stream):
+def normal_pair(seed, cand, idx, stream, libm=False):
+    """Two FP64 Box-Muller normals of one Philox call (the kernels' normal_pair); libm=True:
+    the same transform through libm log / sin / cos (accuracy reference)."""
     z0, z1 = C.c_double(), C.c_double()
-    lib().or_normal_pair(seed, cand, idx, stream, C.byref(z0), C.byref(z1))
+    f = lib().or_normal_pair_libm if libm else lib().or_normal_pair
+    f(seed, cand, idx, stream, C.byref(z0), C.byref(z1))
     return z0.value, z1.value
 
 
-def sample_sspp(init_ctrl, p, sigma, limits, seed, first, B):
+SAMPLER_FP64, SAMPLER_FP32 = 0, 1
+
+
+def sample_sspp(init_ctrl, p, sigma, limits, seed, first, B, sampler=SAMPLER_FP64):
+    """sampleWithNoise (include/sspp.h:114-130) for candidate ids [first, first + B);
+    sampler 0: FP64 Box-Muller pairs (default), 1: the opt-in FP32 quads."""
     init_ctrl = _f64(init_ctrl)
     n, D = init_ctrl.shape
     out = np.zeros((B, n, D))
     lib().or_sample_sspp(init_ctrl, n, D, p, float(sigma), _f64(limits).reshape(D), seed,
-                         first, B, out)
+                         first, B, out, int(sampler))
     return out
 
 
@@ -198,9 +207,16 @@ def sample_tsp(mean, sigma, lo, hi, z_min, seed, first, B):
 class Scene:
     """Oracle scene: model + moving set. mode 0 = qpos window of `arg` dofs, mode 1 = body id."""
 
-    def __init__(self, model, mode, arg):
+    def __init__(self, model, mode, arg, skip_types=()):
+        """skip_types: geom types made non-collidable (contype = conaffinity = 0), for tests
+        that show which candidates a pair type decides."""
         self._keep = {}
         m = _Model()
+        if skip_types:
+            model = dict(model)
+            off = np.isin(np.asarray(model["geom_type"]), list(skip_types))
+            model["geom_contype"] = np.where(off, 0, model["geom_contype"])
+            model["geom_conaffinity"] = np.where(off, 0, model["geom_conaffinity"])
 
         def put(name, arr, dtype):
             a = np.ascontiguousarray(np.asarray(arr, dtype=dtype))

@@ -279,6 +279,64 @@ static void or_sincospi(double x, double* s, double* c) {
     }
 }
 
+/* FP64 Box-Muller, the default normals of both planners (reference: std::normal_distribution
+   <double>, include/sspp.h:116,125 and include/sspp/tsp_sampler.h:17): the kernels' normal_pair
+   (sspp_amd/csrc/sspp_kernels.hip) operation for operation — ln u1 by the atanh series of the
+   mantissa to s^20, sin / cos of 2 pi u2 by Taylor polynomials on |a| <= pi/4 after an exact
+   quarter-turn reduction, explicit fma, IEEE division and sqrt — so every normal is bit-identical.
+   Accuracy against libm: tests/test_oracle_golden.py::test_normal_pair64_accuracy. */
+static double bm_log64(double u) {
+    uint64_t bits;
+    memcpy(&bits, &u, 8);
+    int e = (int)(bits >> 52) - 1023;
+    uint64_t mb = (bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
+    double m;
+    memcpy(&m, &mb, 8);
+    if (m > 0x1.6a09e667f3bcdp+0) { m = m * 0.5; e += 1; }
+    const double s = (m - 1.0) / (m + 1.0);
+    const double s2 = s * s;
+    double p = 0x1.8618618618618p-5;
+    p = fma(s2, p, 0x1.af286bca1af28p-5);
+    p = fma(s2, p, 0x1.e1e1e1e1e1e1ep-5);
+    p = fma(s2, p, 0x1.1111111111111p-4);
+    p = fma(s2, p, 0x1.3b13b13b13b14p-4);
+    p = fma(s2, p, 0x1.745d1745d1746p-4);
+    p = fma(s2, p, 0x1.c71c71c71c71cp-4);
+    p = fma(s2, p, 0x1.2492492492492p-3);
+    p = fma(s2, p, 0x1.999999999999ap-3);
+    p = fma(s2, p, 0x1.5555555555555p-2);
+    p = fma(s2, p, 1.0);
+    const double de = (double)e;
+    return fma(de, 0x1.62e42fefa3800p-1, fma(de, 0x1.ef35793c76730p-45, (s + s) * p));
+}
+static void bm_sincos2pi64(double u, double* sn, double* cs) {
+    const double q = rint(4.0 * u);
+    const double r = fma(-0.25, q, u);
+    const double a = r * 0x1.921fb54442d18p+2;
+    const double a2 = a * a;
+    double sp = 0x1.952c77030ad4ap-49;
+    sp = fma(a2, sp, -0x1.ae7f3e733b81fp-41);
+    sp = fma(a2, sp, 0x1.6124613a86d09p-33);
+    sp = fma(a2, sp, -0x1.ae64567f544e4p-26);
+    sp = fma(a2, sp, 0x1.71de3a556c734p-19);
+    sp = fma(a2, sp, -0x1.a01a01a01a01ap-13);
+    sp = fma(a2, sp, 0x1.1111111111111p-7);
+    sp = fma(a2, sp, -0x1.5555555555555p-3);
+    const double sa = fma(a * a2, sp, a);
+    double cp = -0x1.6827863b97d97p-53;
+    cp = fma(a2, cp, 0x1.ae7f3e733b81fp-45);
+    cp = fma(a2, cp, -0x1.93974a8c07c9dp-37);
+    cp = fma(a2, cp, 0x1.1eed8eff8d898p-29);
+    cp = fma(a2, cp, -0x1.27e4fb7789f5cp-22);
+    cp = fma(a2, cp, 0x1.a01a01a01a01ap-16);
+    cp = fma(a2, cp, -0x1.6c16c16c16c17p-10);
+    cp = fma(a2, cp, 0x1.5555555555555p-5);
+    cp = fma(a2, cp, -0x1.0000000000000p-1);
+    const double ca = fma(a2, cp, 1.0);
+    const int qi = (int)q & 3;
+    *sn = qi == 0 ? sa : (qi == 1 ? ca : (qi == 2 ? -sa : -ca));
+    *cs = qi == 0 ? ca : (qi == 1 ? -sa : (qi == 2 ? -ca : sa));
+}
 void or_normal_pair(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream, double* z0,
                     double* z1) {
     uint32_t o[4];
@@ -287,9 +345,25 @@ void or_normal_pair(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream,
     uint64_t b = (((uint64_t)o[2] << 32) | o[3]) >> 11;
     double u1 = (double)(a + 1) * TWO_M53; /* (0,1] */
     double u2 = (double)b * TWO_M53;       /* [0,1) */
+    double r = sqrt(-2.0 * bm_log64(u1));
+    double sn, cs;
+    bm_sincos2pi64(u2, &sn, &cs);
+    *z0 = r * cs;
+    *z1 = r * sn;
+}
+double or_bm_log64_test(double u) { return bm_log64(u); } /* tests: ln u against libm */
+/* the libm form of the same transform (log, sin/cos): the accuracy reference of the tests */
+void or_normal_pair_libm(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream, double* z0,
+                         double* z1) {
+    uint32_t o[4];
+    philox_words(seed, cand, idx, stream, o);
+    uint64_t a = (((uint64_t)o[0] << 32) | o[1]) >> 11;
+    uint64_t b = (((uint64_t)o[2] << 32) | o[3]) >> 11;
+    double u1 = (double)(a + 1) * TWO_M53;
+    double u2 = (double)b * TWO_M53;
     double r = sqrt(-2.0 * log(u1));
     double sn, cs;
-    or_sincospi(2.0 * u2, &sn, &cs); /* the kernels' sincospi(2 u2): no Payne-Hanek reduction */
+    or_sincospi(2.0 * u2, &sn, &cs);
     *z0 = r * cs;
     *z1 = r * sn;
 }
@@ -355,8 +429,10 @@ static double uniform01(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t str
 
 void or_sample_sspp(const double* init_ctrl, int n, int D, int p, double sigma,
                     const double* limits, uint64_t seed, int64_t first, int64_t B,
-                    double* ctrl_out) {
-    /* include/sspp.h:114-130: ctrl(d, j) += N(0, sigma) * limits(d), j in [p, n-p) */
+                    double* ctrl_out, int sampler) {
+    /* include/sspp.h:114-130: ctrl(d, j) += N(0, sigma) * limits(d), j in [p, n-p).  Normal k of
+       a candidate: sampler 0 (FP64, default) component k & 1 of Philox pair k >> 1; sampler 1
+       (FP32 quads, opt-in) component k & 3 of quad k >> 2. */
     for (int64_t b = 0; b < B; ++b) {
         uint64_t g = (uint64_t)(first + b);
         double* c = ctrl_out + (size_t)b * n * D;
@@ -364,9 +440,16 @@ void or_sample_sspp(const double* init_ctrl, int n, int D, int p, double sigma,
         for (int j = p; j < n - p; ++j) {
             for (int d = 0; d < D; ++d) {
                 int k = (j - p) * D + d;
-                double zq[4];
-                or_normal_quad(seed, g, (uint32_t)(k >> 2), 0u, zq);
-                double z = zq[k & 3];
+                double z;
+                if (sampler == 0) {
+                    double z0, z1;
+                    or_normal_pair(seed, g, (uint32_t)(k >> 1), 0u, &z0, &z1);
+                    z = (k & 1) ? z1 : z0;
+                } else {
+                    double zq[4];
+                    or_normal_quad(seed, g, (uint32_t)(k >> 2), 0u, zq);
+                    z = zq[k & 3];
+                }
                 double noise = (sigma * z) * limits[d];
                 c[(size_t)j * D + d] = c[(size_t)j * D + d] + noise;
             }

@@ -90,10 +90,13 @@ void   or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t o
 void   or_normal_quad(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream, double z[4]);
 void   or_normal_pair(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream,
                       double* z0, double* z1);
-/* sampleWithNoise for candidates [first, first+B): ctrl_out [B][n][D] */
+void   or_normal_pair_libm(uint64_t seed, uint64_t cand, uint32_t idx, uint32_t stream,
+                           double* z0, double* z1);
+/* sampleWithNoise for candidates [first, first+B): ctrl_out [B][n][D]; sampler 0 = FP64 pairs
+   (default), 1 = FP32 quads (opt-in) */
 void   or_sample_sspp(const double* init_ctrl, int n, int D, int p, double sigma,
                       const double* limits, uint64_t seed, int64_t first, int64_t B,
-                      double* ctrl_out);
+                      double* ctrl_out, int sampler);
 /* Sampler::sample_set: vias_out [B][K][4] */
 void   or_sample_tsp(const double* mean /* [K][4] */, const double* sigma /* [K][4] */, int K,
                      const double* lo, const double* hi, double z_min, uint64_t seed,

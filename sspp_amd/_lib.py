@@ -51,7 +51,8 @@ class SsppArgs(C.Structure):
     _fields_ = [("knots", C.POINTER(C.c_double)), ("degree", C.c_int),
                 ("init_ctrl", C.POINTER(C.c_double)), ("n_ctrl", C.c_int), ("dof", C.c_int),
                 ("sigma", C.c_double), ("limits", C.POINTER(C.c_double)),
-                ("check_points", C.c_int), ("seed", C.c_uint64), ("arc_all", C.c_int)]
+                ("check_points", C.c_int), ("seed", C.c_uint64), ("arc_all", C.c_int),
+                ("sampler", C.c_int)]
 
 
 class TspArgs(C.Structure):
@@ -149,6 +150,7 @@ SIGNATURES = {
     "sspp_ces_pack": (C.c_int, [_vp, _i, _vp, _vp]),
     "sspp_ces_unpack": (C.c_int, [_vp, _vp, _vp]),
     "sspp_ces_free": (None, [_vp]),
+    "sspp_debug_job_error": (C.c_int, [_vp]),
 }
 
 

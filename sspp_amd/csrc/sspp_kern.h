@@ -1,0 +1,2500 @@
+// sspp_kern.h — the MI355X (gfx950) candidate-scoring kernels and their launch templates.
+//
+// Included by sspp_kernels.hip (host side: scenes, jobs, the C ABI) and by sspp_inst.hip,
+// which the Makefile compiles once per dof (-DSSPK_D=1,2,3,4,6,7,9) and once for the
+// TaskSpacePlanner kernel (-DSSPK_D=0), each explicitly instantiating its entry points, so the
+// ~200 kernel instantiations compile in parallel.  Variant builds (tools/build_variant.sh)
+// define SSPP_SINGLE_TU and instantiate everything in sspp_kernels.hip.
+//
+//
+// Hot path (reference include/sspp.h:194-225 and include/sspp/tsp_planner.h:95-138):
+//   candidate sampling -> B-spline evaluation -> free-joint FK -> collision -> cost -> argmin.
+//
+// Work decomposition:
+//   * a candidate owns LPC = 64*ceil(items/64) lanes (capped at 256), one waypoint per lane;
+//     a 256-thread workgroup holds CPB = 256/LPC candidates;
+//   * the workgroup prologue builds the shared basis tables (span + N_0..N_p for every
+//     waypoint parameter) and the candidates' control points in LDS (Philox + Box-Muller
+//     in-kernel, or a coalesced copy of caller-supplied control points);
+//   * each lane evaluates its waypoint(s): spline from LDS, FK of the moving body, pair
+//     loop over the scene table (wave-uniform -> scalar loads), broadphase + narrowphase;
+//   * per-candidate sums use the canonical order (lane partials, xor butterfly per wave,
+//     waves in order) that oracle/sspp_oracle.c::or_canon_sum restates;
+//   * one BlockBest per workgroup, then a one-block argmin kernel (lowest id on ties).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "model.h"
+#ifdef SSPP_C2F_STATS  // profiling builds only (tools/build_variant.sh stats -DSSPP_C2F_STATS)
+__device__ unsigned long long g_c2f_stats[16];
+#define SSPP_CB_STAT(i) atomicAdd(&g_c2f_stats[i], 1ull)
+#endif
+#ifdef SSPP_WG_TIMING  // profiling builds only: per-workgroup (start, end, CU, survivors) of k_sspp_c2f
+__device__ unsigned long long g_wq_t[8 << 16];  // k_sspp_wq1 tiles / k_sspp_wq2 items: 8 stamps each
+__device__ unsigned long long g_wq_i[8 << 16];
+#define WQ_T(arr, idx, k, v) do { if (threadIdx.x == 0 && (idx) < (1u << 16)) arr[8 * (idx) + (k)] = (v); } while (0)
+#else
+#define WQ_T(arr, idx, k, v) do { } while (0)
+#endif
+#ifdef SSPP_WG_TIMING
+__device__ unsigned long long g_wg_t[1 << 18];
+__device__ unsigned long long g_wg_ph[6 << 16];  // per workgroup: shader clock after each phase
+#define WG_PH(k) do { if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_wg_ph[6 * blockIdx.x + (k)] = clock64(); } while (0)
+#else
+#define WG_PH(k) do { } while (0)
+#endif
+#include "sspp_device.h"
+
+using namespace sspd;
+
+namespace sspk {
+
+constexpr int kBlock = 256;
+#ifndef SSPP_SCORE_WAVES_PER_EU
+#define SSPP_SCORE_WAVES_PER_EU 4  // min waves per SIMD (4 -> <=128 VGPRs; measured best on gfx950)
+#endif
+constexpr int kMaxMovers = 2;
+constexpr int kMaxSteps = 64;  // steps per launch (k_sspp_c2f)
+
+struct KScene {
+    int npairs;
+    int onegeom;        // every pair shares one moving geom: its pose is computed once
+    int static_block;   // sspp: env-env contacts counted and present -> nothing feasible
+    double static_cost; // tsp: Collision.h cost of env-env contacts, added per waypoint
+    int cylbox;         // some moving pair is cylinder-box (selects the kernels that carry that code)
+};
+
+// Scene tables are passed as separate __restrict__ kernel arguments: the pair loop is
+// wave-uniform and the tables are provably not written by the kernel, so the compiler
+// reads them with scalar (s_load) instructions into SGPRs, once per wave.
+struct SceneT {
+    const DGeom* __restrict__ geoms;
+    const DPair* __restrict__ pairs;
+    const DMover* __restrict__ movers;
+};
+
+// Constant address space (4): loads through these are scalar (SMEM) whenever the address
+// is wave-uniform, independent of the alias analysis of the surrounding kernel.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SSPP_CONST __attribute__((address_space(4)))
+#else
+#define SSPP_CONST
+#endif
+typedef const SSPP_CONST DGeom* cgeom_t;
+typedef const SSPP_CONST DPair* cpair_t;
+typedef const SSPP_CONST DMover* cmover_t;
+
+__device__ __forceinline__ DGeom load_geom(cgeom_t p) {
+    DGeom g;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g.pos[k] = p->pos[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) g.mat[k] = p->mat[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g.size[k] = p->size[k];
+    g.rbound = p->rbound;
+    g.reach = p->reach;
+    g.type = p->type;
+    g.mover = p->mover;
+    g.orig = p->orig;
+    g.relrot = p->relrot;
+    return g;
+}
+__device__ __forceinline__ DPair load_pair(cpair_t p) {
+    DPair r;
+    r.gm = p->gm;
+    r.go = p->go;
+    r.otype = p->otype;
+    r.oorig = p->oorig;
+    r.omover = p->omover;
+    r.pad = 0;
+    r.margin = p->margin;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r.opos[k] = p->opos[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.omat[k] = p->omat[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r.osize[k] = p->osize[k];
+    r.orbound = p->orbound;
+    return r;
+}
+
+// ---------------------------------------------------------------- candidate-level broadphase
+// A B-spline lies in the convex hull of its control points (non-negative basis, partition of
+// unity), so every waypoint's mover position lies in the AABB [lo, hi] of the control points'
+// position columns.  A pair whose partner cannot come within rbound + margin of that box
+// (expanded by the moving geom's reach) for ANY waypoint is culled for the whole candidate:
+// exactly the pairs the per-waypoint bounding-sphere test would reject at every waypoint.
+// kHullPad absorbs the rounding of the spline evaluation (|error| ~ 1e-15).
+constexpr double kHullPad = 1e-9;
+
+__host__ __device__ __forceinline__ bool pair_may_touch(const DPair& pr, const DGeom& G, const double* lo,
+                                               const double* hi) {
+    if (pr.omover >= 0 || G.rbound <= 0.0) return true;
+    const double slack = G.reach + G.rbound + pr.margin + kHullPad;
+    if (pr.orbound > 0.0) {
+        double d2 = 0.0;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const double c = pr.opos[d];
+            const double e = c < lo[d] ? lo[d] - c : (c > hi[d] ? c - hi[d] : 0.0);
+            d2 = fma(e, e, d2);
+        }
+        const double lim = pr.orbound + slack;
+        return d2 <= lim * lim;
+    }
+    if (pr.otype == 0) {  // plane: lowest point of the box over the plane's normal
+        const double n0 = pr.omat[2], n1 = pr.omat[5], n2 = pr.omat[8];
+        const double m = (n0 >= 0 ? n0 * lo[0] : n0 * hi[0]) + (n1 >= 0 ? n1 * lo[1] : n1 * hi[1]) +
+                         (n2 >= 0 ? n2 * lo[2] : n2 * hi[2]) -
+                         (n0 * pr.opos[0] + n1 * pr.opos[1] + n2 * pr.opos[2]);
+        return m - slack < 0.0;
+    }
+    return true;
+}
+
+// Bit k of the result: pair k can touch (pairs >= 64 are always evaluated).  One lane per
+// pair, then a wave ballot -> the mask is wave-uniform (SGPRs).
+template <int D, int NM, int MODE>
+__device__ __forceinline__ unsigned long long hull_mask(const double* ctrl, int n, int npairs,
+                                                        cpair_t pairs, cgeom_t geoms,
+                                                        cmover_t movers) {
+    const int lane = threadIdx.x & 63;
+    bool act = false;
+    if (lane < npairs) {
+        const DPair pr = load_pair(pairs + lane);
+        const DGeom G = load_geom(geoms + pr.gm);
+        const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
+        double lo[3], hi[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int col = MODE == 1 ? d : 7 * m + d;
+            if (col < D) {
+                double a = ctrl[col], b = ctrl[col];
+                for (int j = 1; j < n; ++j) {
+                    const double v = ctrl[j * D + col];
+                    a = v < a ? v : a;
+                    b = v > b ? v : b;
+                }
+                lo[d] = a; hi[d] = b;
+            } else {
+                lo[d] = hi[d] = (double)movers[m].qpos0[d];
+            }
+        }
+        act = pair_may_touch(pr, G, lo, hi);
+    }
+    unsigned long long mask = __ballot(act);
+    if (npairs > 64) mask = ~0ull;
+    return mask;
+}
+
+struct BlockBest {
+    double cost;
+    long long idx;
+    long long count;
+    long long pad;
+};
+
+struct SsppK {
+    KScene sc;
+    int has_scene;
+    int ablate;    // profiling only (SSPP_ABLATE env): 1 no sampling, 2 no collision, 4 no arc
+    int insample;  // draw the candidates inside the scoring kernel (else k_sample_sspp)
+    int sampler;   // 0 FP64 Box-Muller pairs (default), 1 FP32 quads (opt-in)
+    int p, n, W;
+    double sigma;
+    unsigned long long seed;
+    long long first_id, B;
+    int lpc, cpb, shared_endpoints;
+    int arc_all;
+};
+
+struct TspK {
+    KScene sc;
+    int n, K, cp;
+    double start[4], end[4], lo[4], hi[4];
+    double z_min;
+    unsigned long long seed;
+    long long first_id, B;
+    double w_col, floor_z_min, floor_margin, floor_scale;
+    int lpc, cpb;
+    // CES slot mode (tsp_planner.h:78-93 seeds): launch candidate c is slot slot0 + c of the
+    // iteration's list [mean set, forwarded best (if any), samples...].  Slots below *nfixed
+    // copy fixed[slot]; slot s >= *nfixed is random sample s - *nfixed (Philox id first_id +
+    // s - *nfixed); slots past *nfixed + samples are padding (status 0, cost +inf).
+    int ces;
+    const double* fixed;    // [2][K][4]
+    const int* nfixed;
+    long long slot0, samples;
+};
+
+// ---------------------------------------------------------------- Philox4x32-10 + Box-Muller
+__device__ __forceinline__ void philox(unsigned c0, unsigned c1, unsigned c2, unsigned c3,
+                                       unsigned k0, unsigned k1, unsigned o[4]) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        // one 32 x 32 -> 64-bit multiply per product (v_mad_u64_u32): hi and lo together
+        const unsigned long long p0 = (unsigned long long)c0 * 0xD2511F53u;
+        const unsigned long long p1 = (unsigned long long)c2 * 0xCD9E8D57u;
+        const unsigned n0 = (unsigned)(p1 >> 32) ^ c1 ^ k0, n2 = (unsigned)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (unsigned)p1; c2 = n2; c3 = (unsigned)p0;
+    }
+    o[0] = c0; o[1] = c1; o[2] = c2; o[3] = c3;
+}
+__device__ __forceinline__ void philox_words(unsigned long long seed, unsigned long long g,
+                                             unsigned idx, unsigned stream, unsigned o[4]) {
+    philox(idx, stream, (unsigned)g, (unsigned)(g >> 32), (unsigned)seed, (unsigned)(seed >> 32), o);
+}
+// FP64 Box-Muller (the default sampler of both planners; std::normal_distribution<double> in the
+// reference, include/sspp.h:116,125 and include/sspp/tsp_sampler.h:17): one Philox4x32-10 call
+// gives two 53-bit uniforms u1 in (0, 1], u2 in [0, 1) -> z0 = r cos(2 pi u2), z1 = r sin(2 pi u2),
+// r = sqrt(-2 ln u1), |z| <= 8.57.  ln and sincos are written out as FP64 polynomials with
+// explicit fma (full double accuracy: the atanh series of ln m on m in [sqrt(1/2), sqrt(2)] to
+// s^20, Taylor sin / cos on |a| <= pi/4 to a^17 / a^18) and IEEE division and sqrt, so
+// oracle/sspp_oracle.c::or_normal_pair reproduces every normal bit for bit (libm's log and
+// sincospi agreed only to ~1 ulp).
+__device__ __forceinline__ double bm_log64(double u) {  // ln u, u in [2^-53, 1]
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(u);
+    int e = (int)(bits >> 52) - 1023;
+    double m = __longlong_as_double((long long)((bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
+    if (m > 0x1.6a09e667f3bcdp+0) { m = m * 0.5; e += 1; }  // m in [sqrt(1/2), sqrt(2)]
+    const double s = (m - 1.0) / (m + 1.0);                  // |s| <= 0.1716; m - 1 exact
+    const double s2 = s * s;
+    double p = 0x1.8618618618618p-5;                         // 1/21
+    p = fma(s2, p, 0x1.af286bca1af28p-5);                    // 1/19
+    p = fma(s2, p, 0x1.e1e1e1e1e1e1ep-5);                    // 1/17
+    p = fma(s2, p, 0x1.1111111111111p-4);                    // 1/15
+    p = fma(s2, p, 0x1.3b13b13b13b14p-4);                    // 1/13
+    p = fma(s2, p, 0x1.745d1745d1746p-4);                    // 1/11
+    p = fma(s2, p, 0x1.c71c71c71c71cp-4);                    // 1/9
+    p = fma(s2, p, 0x1.2492492492492p-3);                    // 1/7
+    p = fma(s2, p, 0x1.999999999999ap-3);                    // 1/5
+    p = fma(s2, p, 0x1.5555555555555p-2);                    // 1/3
+    p = fma(s2, p, 1.0);
+    const double de = (double)e;                             // ln 2 = hi + lo (hi: 42 bits)
+    return fma(de, 0x1.62e42fefa3800p-1, fma(de, 0x1.ef35793c76730p-45, (s + s) * p));
+}
+__device__ __forceinline__ void bm_sincos2pi64(double u, double* sn, double* cs) {  // u in [0, 1)
+    const double q = rint(4.0 * u);
+    const double r = fma(-0.25, q, u);         // exact, |r| <= 1/8
+    const double a = r * 0x1.921fb54442d18p+2; // 2 pi r, |a| <= pi/4
+    const double a2 = a * a;
+    double sp = 0x1.952c77030ad4ap-49;         // 1/17!
+    sp = fma(a2, sp, -0x1.ae7f3e733b81fp-41);
+    sp = fma(a2, sp, 0x1.6124613a86d09p-33);
+    sp = fma(a2, sp, -0x1.ae64567f544e4p-26);
+    sp = fma(a2, sp, 0x1.71de3a556c734p-19);
+    sp = fma(a2, sp, -0x1.a01a01a01a01ap-13);
+    sp = fma(a2, sp, 0x1.1111111111111p-7);
+    sp = fma(a2, sp, -0x1.5555555555555p-3);   // -1/3!
+    const double sa = fma(a * a2, sp, a);
+    double cp = -0x1.6827863b97d97p-53;        // -1/18!
+    cp = fma(a2, cp, 0x1.ae7f3e733b81fp-45);
+    cp = fma(a2, cp, -0x1.93974a8c07c9dp-37);
+    cp = fma(a2, cp, 0x1.1eed8eff8d898p-29);
+    cp = fma(a2, cp, -0x1.27e4fb7789f5cp-22);
+    cp = fma(a2, cp, 0x1.a01a01a01a01ap-16);
+    cp = fma(a2, cp, -0x1.6c16c16c16c17p-10);
+    cp = fma(a2, cp, 0x1.5555555555555p-5);
+    cp = fma(a2, cp, -0x1.0000000000000p-1);   // -1/2!
+    const double ca = fma(a2, cp, 1.0);
+    const int qi = (int)q & 3;
+    *sn = qi == 0 ? sa : (qi == 1 ? ca : (qi == 2 ? -sa : -ca));
+    *cs = qi == 0 ? ca : (qi == 1 ? -sa : (qi == 2 ? -ca : sa));
+}
+__device__ __forceinline__ void normal_pair(unsigned long long seed, unsigned long long g,
+                                            unsigned idx, unsigned stream, double* z0, double* z1) {
+    unsigned o[4];
+    philox_words(seed, g, idx, stream, o);
+    const unsigned long long a = ((((unsigned long long)o[0]) << 32) | o[1]) >> 11;
+    const unsigned long long b = ((((unsigned long long)o[2]) << 32) | o[3]) >> 11;
+    const double u1 = (double)(a + 1) * 0x1p-53;  // (0, 1], exact
+    const double u2 = (double)b * 0x1p-53;        // [0, 1), exact
+    const double r = sqrt(-2.0 * bm_log64(u1));
+    double sn, cs;
+    bm_sincos2pi64(u2, &sn, &cs);
+    *z0 = r * cs;
+    *z1 = r * sn;
+}
+// Opt-in FP32 SamplingPathPlanner normals (sspp_sspp_args::sampler = 1, the round-2 default): one
+// Philox4x32-10 call gives four 24-bit uniforms -> two Box-Muller pairs in FP32, with fmaf
+// polynomials written out (ln u by the atanh series on the mantissa, sin / cos of 2 pi u after an
+// exact quarter-turn reduction) and a correctly rounded sqrtf, so
+// oracle/sspp_oracle.c::or_normal_quad reproduces it bit for bit.  |z| <= 5.77 (u1 >= 2^-24):
+// narrower than the reference's std::normal_distribution<double>, hence not the default.
+__device__ __forceinline__ float bm_log(float u) {  // ln u, u in [2^-24, 1]
+    const unsigned bits = __float_as_uint(u);
+    int e = (int)(bits >> 23) - 127;
+    float m = __uint_as_float((bits & 0x7fffffu) | 0x3f800000u);  // [1, 2)
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    const float s = (m - 1.0f) / (m + 1.0f);                      // |s| <= 0.1716
+    const float s2 = s * s;
+    float p = fmaf(s2, 0.111111111f, 0.142857143f);
+    p = fmaf(s2, p, 0.2f);
+    p = fmaf(s2, p, 0.333333333f);
+    p = fmaf(s2, p, 1.0f);
+    return fmaf((float)e, 0.693147181f, (s + s) * p);
+}
+__device__ __forceinline__ void bm_sincos2pi(float u, float* sn, float* cs) {  // u in [0, 1)
+    const float q = rintf(4.0f * u);
+    const float r = fmaf(-0.25f, q, u);  // exact
+    const float a = r * 6.28318531f;     // |a| <= pi / 4
+    const float a2 = a * a;
+    float sp = fmaf(a2, 2.75573192e-6f, -1.98412698e-4f);
+    sp = fmaf(a2, sp, 8.33333333e-3f);
+    sp = fmaf(a2, sp, -0.166666667f);
+    const float sa = fmaf(a * a2, sp, a);
+    float cp = fmaf(a2, 2.48015873e-5f, -1.38888889e-3f);
+    cp = fmaf(a2, cp, 4.16666667e-2f);
+    cp = fmaf(a2, cp, -0.5f);
+    const float ca = fmaf(a2, cp, 1.0f);
+    const int qi = (int)q & 3;
+    *sn = qi == 0 ? sa : (qi == 1 ? ca : (qi == 2 ? -sa : -ca));
+    *cs = qi == 0 ? ca : (qi == 1 ? -sa : (qi == 2 ? -ca : sa));
+}
+__device__ __forceinline__ void normal_quad(unsigned long long seed, unsigned long long g,
+                                            unsigned idx, unsigned stream, double z[4]) {
+    unsigned o[4];
+    philox_words(seed, g, idx, stream, o);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const float u1 = (float)((o[2 * h] >> 8) + 1u) * 5.96046448e-8f;  // (0, 1], exact
+        const float u2 = (float)(o[2 * h + 1] >> 8) * 5.96046448e-8f;     // [0, 1), exact
+        const float r = sqrtf(-2.0f * bm_log(u1));
+        float sn, cs;
+        bm_sincos2pi(u2, &sn, &cs);
+        z[2 * h] = (double)(r * cs);
+        z[2 * h + 1] = (double)(r * sn);
+    }
+}
+__device__ __forceinline__ double uniform01(unsigned long long seed, unsigned long long g,
+                                            unsigned idx, unsigned stream) {
+    unsigned o[4];
+    philox_words(seed, g, idx, stream, o);
+    unsigned long long b = ((((unsigned long long)o[2]) << 32) | o[3]) >> 11;
+    return (double)b * 1.1102230246251565e-16;
+}
+
+// sampleWithNoise (include/sspp.h:114-130) in work items: item m of a candidate draws normals
+// 2m, 2m+1 (sampler 0: FP64 pair, Philox idx m) or 4m .. 4m+3 (sampler 1: FP32 quad) and adds
+// (sigma z) limits(d) to the perturbed control-point block c (column-major (j - p) * D + d).
+__device__ __forceinline__ int sample_items(int sampler, int npert) {
+    return sampler ? (npert + 3) >> 2 : (npert + 1) >> 1;
+}
+__device__ __forceinline__ void sample_item(int sampler, unsigned long long seed, unsigned long long g,
+                                            int m, int npert, int D, double sigma,
+                                            const double* __restrict__ limits, double* c) {
+    if (sampler == 0) {
+        double z0, z1;
+        normal_pair(seed, g, (unsigned)m, 0u, &z0, &z1);
+        const int k = 2 * m;
+        c[k] = c[k] + (sigma * z0) * limits[k % D];
+        if (k + 1 < npert) c[k + 1] = c[k + 1] + (sigma * z1) * limits[(k + 1) % D];
+    } else {
+        double z[4];
+        normal_quad(seed, g, (unsigned)m, 0u, z);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int k = 4 * m + h;
+            if (k < npert) c[k] = c[k] + (sigma * z[h]) * limits[k % D];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- spline from basis rows
+// N: p+1 basis values of one waypoint (host-precomputed table in global memory, L2 resident)
+template <int D, int P>
+__device__ __forceinline__ void eval_pt(const double* ctrl, const double* __restrict__ N,
+                                        int span, double* q) {
+    double Nr[P + 1];
+#pragma unroll
+    for (int r = 0; r <= P; ++r) Nr[r] = N[r];
+    const double* c0 = ctrl + (span - P) * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        double acc = Nr[0] * c0[d];
+#pragma unroll
+        for (int r = 1; r <= P; ++r) acc = fma(Nr[r], c0[r * D + d], acc);
+        q[d] = acc;
+    }
+}
+
+// the same from a basis row already in registers (prefetched ahead of its use)
+template <int D, int P>
+__device__ __forceinline__ void eval_pt_r(const double* ctrl, const double (&Nr)[P + 1], int span, double* q) {
+    const double* c0 = ctrl + (span - P) * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        double acc = Nr[0] * c0[d];
+#pragma unroll
+        for (int r = 1; r <= P; ++r) acc = fma(Nr[r], c0[r * D + d], acc);
+        q[d] = acc;
+    }
+}
+
+template <int D>
+__device__ __forceinline__ double dist_nd(const double* a, const double* b) {
+    double d0 = b[0] - a[0];
+    double s = d0 * d0;
+#pragma unroll
+    for (int d = 1; d < D; ++d) { double dd = b[d] - a[d]; s = fma(dd, dd, s); }
+    return sqrt(s);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------- one waypoint vs the scene
+// Mover root poses (position + rotation) for MODE 0 (q -> qpos[0:D] window, free joints at
+// qpos[7m:7m+7]) or MODE 1 ((x, y, z, yaw) -> the bound free body, utility.h:149-206).
+template <int D, int NM, int MODE>
+__device__ __forceinline__ void mover_poses(const double* q, cmover_t movers,
+                                            double (&mp)[NM][3], double (&mR)[NM][9]) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        double qp[7];
+        if (MODE == 0) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k)
+                qp[k] = (7 * m + k < D) ? q[(7 * m + k < D) ? 7 * m + k : 0] : (double)movers[m].qpos0[k];
+        } else {
+#ifndef SSPP_YAW_GENERIC
+            // yaw_to_quat (utility.h:198-206): q = (cos h, 0, 0, sin h) — a rotation about z.
+            // normalize4 + quat2mat written out for x = y = +0: every entry equals the generic
+            // formula's (sums with exact zeros), except the sign of the four zero entries,
+            // which only ever enter products and sums with non-zero terms
+            const double half = q[3] * 0.5;
+            double w = cos(half), z = sin(half);
+            const double nn = sqrt(fma(z, z, w * w));
+            if (nn < kMinVal) { w = 1.0; z = 0.0; }
+            else if (fabs(nn - 1.0) > kMinVal) { const double inv = 1.0 / nn; w *= inv; z *= inv; }
+            const double q00 = w * w, q33 = z * z, q03 = w * z;
+            double* R = mR[m];
+            R[0] = q00 - q33; R[1] = 2.0 * (0.0 - q03); R[2] = 0.0;
+            R[3] = 2.0 * (0.0 + q03); R[4] = q00 - q33; R[5] = 0.0;
+            R[6] = 0.0; R[7] = 0.0; R[8] = q00 + q33;
+            mp[m][0] = q[0]; mp[m][1] = q[1]; mp[m][2] = q[2];
+            continue;
+#else
+            double half = q[3] * 0.5;
+            qp[0] = q[0]; qp[1] = q[1]; qp[2] = q[2];
+            qp[3] = cos(half); qp[4] = 0.0; qp[5] = 0.0; qp[6] = sin(half);
+#endif
+        }
+        normalize4(qp + 3);
+        quat2mat(qp + 3, mR[m]);
+        mp[m][0] = qp[0]; mp[m][1] = qp[1]; mp[m][2] = qp[2];
+    }
+}
+
+// Geom pose from its mover's pose.  With an identity relative rotation the geom frame IS the
+// mover frame: copying R reproduces the oracle's quat2mat(mulquat(root, 1)) exactly.
+__device__ __forceinline__ void geom_pose(const double* P, const double* R, const DGeom& G,
+                                          double* gp, double* gm) {
+    double t[3];
+    matvec3(R, G.pos, t);
+    gp[0] = P[0] + t[0]; gp[1] = P[1] + t[1]; gp[2] = P[2] + t[2];
+    if (G.relrot) {
+        matmul3(R, G.mat, gm);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) gm[k] = R[k];
+    }
+}
+
+__device__ __forceinline__ void geom_pos(const double* P, const double* R, const DGeom& G, double* gp) {
+    double t[3];
+    matvec3(R, G.pos, t);
+    gp[0] = P[0] + t[0]; gp[1] = P[1] + t[1]; gp[2] = P[2] + t[2];
+}
+__device__ __forceinline__ void geom_rot(const double* R, const DGeom& G, double* gm) {
+    if (G.relrot) {
+        matmul3(R, G.mat, gm);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) gm[k] = R[k];
+    }
+}
+
+// Geom pose from a mover rotation about z (R[2] = R[5] = R[6] = R[7] = 0, MODE 1): the
+// generic dot products with those zero terms dropped (each dropped term adds an exact zero).
+template <bool ZR>
+__device__ __forceinline__ void geom_pos_t(const double* P, const double* R, const DGeom& G, double* gp) {
+    if (!ZR) { geom_pos(P, R, G, gp); return; }
+    gp[0] = P[0] + fma(R[1], G.pos[1], R[0] * G.pos[0]);
+    gp[1] = P[1] + fma(R[4], G.pos[1], R[3] * G.pos[0]);
+    gp[2] = P[2] + R[8] * G.pos[2];
+}
+template <bool ZR>
+__device__ __forceinline__ void geom_rot_t(const double* R, const DGeom& G, double* gm) {
+    if (!ZR || !G.relrot) { geom_rot(R, G, gm); return; }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        gm[j] = fma(R[1], G.mat[3 + j], R[0] * G.mat[j]);
+        gm[3 + j] = fma(R[4], G.mat[3 + j], R[3] * G.mat[j]);
+        gm[6 + j] = R[8] * G.mat[6 + j];
+    }
+}
+
+// Per-waypoint broadphase of one pair (exact: it only rejects pairs whose narrowphase cannot
+// report dist < margin).  Two spheres: MuJoCo's bounding-sphere test.  Plane vs a bounded
+// geom: every point of the geom lies within rbound of its centre, so a centre height over the
+// plane above rbound + margin (+ kHullPad for rounding) rules out a contact — the plane-box
+// corners satisfy t >= h - sum_j |n.a_j| e_j >= h - |e| = h - rbound (Cauchy-Schwarz).
+__device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const double* gp,
+                                          const double* op, const double* om) {
+    const double ro = pr.orbound;
+    if (rg > 0.0 && ro > 0.0) {
+        const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
+        const double thr = rg + ro + pr.margin;
+        return !(dot3(dc, dc) > thr * thr);
+    }
+    if (pr.otype == 0 && rg > 0.0) {
+        const double h = (gp[0] - op[0]) * om[2] + (gp[1] - op[1]) * om[5] + (gp[2] - op[2]) * om[8];
+        return !(h - rg > pr.margin + kHullPad);
+    }
+    return true;
+}
+
+// DEEP=false: checkCollision's ncon > 0 for one candidate.  Every active lane of the wave
+//   must belong to that candidate: the scan stops for the whole wave at the first pair where
+//   any lane finds a contact (returns 1 on every lane — the candidate is infeasible whatever
+//   the other waypoints give), or when *stop (the candidate's LDS flag, cleared by another
+//   wave of the same candidate) reads 0.  Returns 0 when no lane has a contact.
+// DEEP=true : returns 0, *cost = sum over deep contacts of -1/(center_dist + 1e-4) + static.
+template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true>
+__device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
+                             unsigned long long mask, double* cost, int* stop = nullptr) {
+    static_assert(!ONEGEOM || NM == 1, "single moving geom implies a single mover");
+    const cgeom_t geoms = (cgeom_t)T.geoms;
+    const cpair_t pairs = (cpair_t)T.pairs;
+    double mp[NM][3], mR[NM][9];
+    mover_poses<D, NM, MODE>(q, (cmover_t)T.movers, mp, mR);
+    double acc = 0.0;
+    int cur = -1;
+    double gp[3], gmat[9];
+    bool have_rot = true;  // multi-geom movers: a geom's rotation is formed at its first near pair
+    DGeom G;
+    constexpr bool ZR = MODE == 1;  // yaw-only mover rotation
+    if (ONEGEOM) {  // every pair shares one moving geom: pose once, mover pose dies here
+        cur = pairs[0].gm;
+        G = load_geom(geoms + cur);
+        geom_pos_t<ZR>(mp[0], mR[0], G, gp);
+        geom_rot_t<ZR>(mR[0], G, gmat);
+    }
+    const int np = sc.npairs;
+    for (int k = 0; k < np; ++k) {
+        if (k < 64) {
+            // skip culled pairs with a scalar bit scan
+            const unsigned long long rest = mask >> k;
+            if (rest == 0ull) break;
+            k += __builtin_ctzll(rest);
+            if (k >= np) break;
+        }
+        const DPair pr = load_pair(pairs + k);
+        if (!ONEGEOM && pr.gm != cur) {
+            cur = pr.gm;
+            G = load_geom(geoms + cur);
+            const bool second = NM > 1 && G.mover == 1;
+            geom_pos_t<ZR>(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp);
+            have_rot = false;
+        }
+        double op_[3], om_[9];
+        const double* op = pr.opos;
+        const double* om = pr.omat;
+        if (NM > 1 && pr.omover >= 0) {
+            const bool second = pr.omover == 1;
+            const double* R = second ? mR[NM - 1] : mR[0];
+            const double* P = second ? mp[NM - 1] : mp[0];
+            double t[3];
+            matvec3(R, pr.opos, t);
+            op_[0] = P[0] + t[0]; op_[1] = P[1] + t[1]; op_[2] = P[2] + t[2];
+            matmul3(R, pr.omat, om_);
+            op = op_; om = om_;
+        }
+        const bool near = pair_near(pr, G.rbound, gp, op, om);
+        int nd = 0, nc = 0;
+        if (near) {
+            if (!ONEGEOM && !have_rot) {
+                const bool second = NM > 1 && G.mover == 1;
+                geom_rot_t<ZR>(second ? mR[NM - 1] : mR[0], G, gmat);
+                have_rot = true;
+            }
+            const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
+            if (gfirst) nc = collide<DEEP, CB, DEEP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+            else nc = collide<DEEP, CB, DEEP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+        }
+        if (!DEEP) {
+            // the loop trip is wave-uniform, so every active lane reaches this vote
+            if (__ballot(nc > 0) != 0ull) return 1;
+            if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                return 1;
+        } else if (nd > 0) {
+            const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
+            const double cd = sqrt(dot3(dc, dc));
+            const double term = -1.0 / (cd + 1e-4);
+            for (int i = 0; i < nd; ++i) acc = acc + term;
+        }
+    }
+    if (DEEP) *cost = acc + sc.static_cost;
+    return 0;
+}
+
+// ---------------------------------------------------------------- batch argmin helpers
+__device__ __forceinline__ bool better(double c1, long long i1, double c2, long long i2) {
+    // lexicographic (cost, index); index -1 means "none"
+    if (i2 < 0) return i1 >= 0;
+    if (i1 < 0) return false;
+    return (c1 < c2) || (c1 == c2 && i1 < i2);
+}
+
+// ---------------------------------------------------------------- fused batch argmin
+// Each workgroup publishes one BlockBest; arrivals are counted on 8 sharded counters (one
+// 64-byte line each, shard = block % 8) so no single word sees more than ~B/16 atomics.
+// The last arriver of a shard reduces that shard and publishes a shard record; the last of
+// the shards reduces the 8 shard records into *out and re-arms every counter.
+// Hand-off (cdna_hip_programming.md Guideline 16, R1 with sc1 on both sides): records are
+// written with 8-byte agent-scope relaxed atomic stores (global_store ... sc1, write-through),
+// every storing lane drains with s_waitcnt vmcnt(0) before its relaxed agent atomic add, and
+// consumers read records only with agent-scope relaxed atomic loads (sc1, bypass L1) after
+// their add returned "last" and a workgroup barrier.  No release/acquire fences needed.
+struct ArgminSync {
+    unsigned int shard[8][16];  // arrival counters, one cache line each
+    unsigned int top[16];
+    BlockBest rec[8];           // shard results
+};
+
+__device__ __forceinline__ void st_rec(BlockBest* p, const BlockBest& b) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q + 0, (unsigned long long)__double_as_longlong(b.cost), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (unsigned long long)b.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 2, (unsigned long long)b.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ BlockBest ld_rec(BlockBest* p) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    BlockBest b;
+    b.cost = __longlong_as_double((long long)__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    b.idx = (long long)__hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b.count = (long long)__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b.pad = 0;
+    return b;
+}
+
+// block-wide lexicographic reduction of records idx0 + stride*i, i < n (all NT threads call)
+template <int NT = kBlock>
+__device__ BlockBest reduce_recs(BlockBest* recs, int idx0, int stride, int n, double* scratch) {
+    double bc = INFINITY;
+    long long bi = -1, cnt = 0;
+    for (int i = threadIdx.x; i < n; i += NT) {
+        const BlockBest b = ld_rec(recs + idx0 + (long long)stride * i);
+        cnt += b.count;
+        if (better(b.cost, b.idx, bc, bi)) { bc = b.cost; bi = b.idx; }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double oc = __shfl_xor(bc, off, 64);
+        const long long oi = __shfl_xor(bi, off, 64);
+        cnt += __shfl_xor(cnt, off, 64);
+        if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        scratch[3 * w] = bc;
+        scratch[3 * w + 1] = __longlong_as_double(bi);
+        scratch[3 * w + 2] = __longlong_as_double(cnt);
+    }
+    __syncthreads();
+    BlockBest r;
+    r.cost = scratch[0];
+    r.idx = __double_as_longlong(scratch[1]);
+    r.count = __double_as_longlong(scratch[2]);
+    r.pad = 0;
+    for (int k = 1; k < NT / 64; ++k) {
+        const double oc = scratch[3 * k];
+        const long long oi = __double_as_longlong(scratch[3 * k + 1]);
+        r.count += __double_as_longlong(scratch[3 * k + 2]);
+        if (better(oc, oi, r.cost, r.idx)) { r.cost = oc; r.idx = oi; }
+    }
+    return r;
+}
+
+// All NT threads of the workgroup call this after thread 0 filled `bb`.
+template <int NT = kBlock>
+__device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, ArgminSync* sync,
+                             sspp_best* out, int nblk = -1, int b = -1) {
+    __shared__ double scratch[16];
+    if (nblk < 0) { nblk = gridDim.x; b = blockIdx.x; }
+    const int sh = b & 7;
+    const int nsh = nblk < 8 ? nblk : 8;
+    int* flag = reinterpret_cast<int*>(scratch + 14);
+    if (!out) {
+        if (threadIdx.x == 0) part[b] = bb;
+        return;
+    }
+    if (threadIdx.x == 0) {
+        st_rec(part + b, bb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned shard_n = (unsigned)((nblk - sh + 7) >> 3);
+        const unsigned prev = __hip_atomic_fetch_add(&sync->shard[sh][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = prev == shard_n - 1;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const BlockBest shard_best = reduce_recs<NT>(part, sh, 8, (nblk - sh + 7) >> 3, scratch);
+    if (threadIdx.x == 0) {
+        st_rec(sync->rec + sh, shard_best);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(&sync->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = prev == (unsigned)nsh - 1;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const BlockBest r = reduce_recs<NT>(sync->rec, 0, 1, nsh, scratch);
+    if (threadIdx.x == 0) {
+        out->cost = r.idx < 0 ? INFINITY : r.cost;
+        out->index = r.idx;
+        out->count = r.count;
+        out->reserved = 0;
+        for (int k = 0; k < 8; ++k) __hip_atomic_store(&sync->shard[k][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sync->top[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+
+// ---------------------------------------------------------------- SamplingPathPlanner kernel
+// tab: host-precomputed basis rows, (W+1) collision rows u = i/W then W arc rows v = i/(W-1),
+// P+1 doubles each; span: matching knot spans.
+template <int D, int NM, int P, bool ONEGEOM>
+__global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
+    SsppK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
+    const double* __restrict__ ctrl_in, const double* __restrict__ pert,
+    double* __restrict__ ctrl_out, double* __restrict__ arc, unsigned char* __restrict__ feasible,
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int P1 = P + 1;
+    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, W = a.W;
+    const int ndof = n * D;
+    const int slot = tid / lpc, lane = tid - slot * lpc;
+    const long long cand0 = (long long)blockIdx.x * cpb;
+    double* s_ctrl = smem;                        // [cpb][n][D]
+    double* s_wsum = s_ctrl + cpb * ndof;         // [4]
+    double* s_arc = s_wsum + kBlock / 64;         // [4]
+    int* s_flag = (int*)(s_arc + 4);              // [cpb] + shared endpoints
+    const double* tcol = tab;
+    const double* tarc = tab + (W + 1) * P1;
+    const int* scol = span;
+    const int* sarc = span + (W + 1);
+
+    if (tid <= cpb) s_flag[tid] = 1;
+    const long long nvalid = min((long long)cpb, a.B - cand0);
+    // prefetch this lane's basis rows (global, L2-resident) while the control points stage
+    double Ncol[P1];
+    int sc0 = P;
+    {
+        const int i = lane + 1 < W ? lane + 1 : W - 1;
+#pragma unroll
+        for (int r = 0; r < P1; ++r) Ncol[r] = tcol[i * P1 + r];
+        sc0 = scol[i];
+    }
+    if (ctrl_in) {
+        const double* src = ctrl_in + cand0 * ndof;
+        for (int e = tid; e < nvalid * ndof; e += kBlock) s_ctrl[e] = src[e];
+    } else {
+        // init control points + perturbed columns j in [p, n-p): from the sampler kernel, or
+        // (insample) drawn here by the workgroup itself
+        const int npert = (n - 2 * P) * D;
+        const bool from_pert = !a.insample && !(a.ablate & 1);
+        for (int e = tid; e < cpb * ndof; e += kBlock) {
+            const int sl = e / ndof, r = e - sl * ndof;
+            const int k = r - P * D;
+            s_ctrl[e] = (from_pert && k >= 0 && k < npert && sl < nvalid)
+                            ? pert[(cand0 + sl) * npert + k]
+                            : init_ctrl[r];
+        }
+        if (a.insample) {
+            __syncthreads();
+            const int nq = sample_items(a.sampler, npert);
+            for (int e = tid; e < cpb * nq; e += kBlock) {
+                const int sl = e / nq, m = e - sl * nq;
+                if (sl >= nvalid) continue;
+                sample_item(a.sampler, a.seed, (unsigned long long)(a.first_id + cand0 + sl), m, npert, D,
+                            a.sigma, limits, s_ctrl + sl * ndof + P * D);
+            }
+        }
+    }
+    __syncthreads();
+    if (ctrl_out) {
+        double* dst = ctrl_out + cand0 * ndof;
+        for (int e = tid; e < nvalid * ndof; e += kBlock) dst[e] = s_ctrl[e];
+    }
+
+    const bool valid = slot < nvalid;
+    const double* myc = s_ctrl + slot * ndof;
+    double q[D], q2[D];
+    const unsigned long long mask =
+        a.has_scene ? hull_mask<D, NM, 0>(myc, n, a.sc.npairs, (cpair_t)T.pairs, (cgeom_t)T.geoms,
+                                          (cmover_t)T.movers)
+                    : 0ull;
+
+    // checkCollision: interior points i = 1..W-1 one per lane; endpoints i = 0, W on a spare lane
+    // Flags are plain LDS stores (every writer stores 0; read after the barrier below):
+    // no volatile/atomic access, so the scene tables stay on the scalar-load path.
+    if (a.has_scene && valid && !(a.ablate & 2)) {
+        int* vflag = s_flag;
+        if (a.sc.static_block) vflag[slot] = 0;
+        for (int j = lane; j < W - 1; j += lpc) {
+            const int i = j + 1;
+            if (j == lane) eval_pt<D, P>(myc, Ncol, sc0, q);
+            else eval_pt<D, P>(myc, tcol + i * P1, scol[i], q);
+            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr, vflag + slot)) {
+                __hip_atomic_store(vflag + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
+            }
+        }
+        const int spare = (W - 1) % lpc == 0 ? 0 : lpc - 1;
+        bool duty0 = false, dutyW = false;
+        int fidx = slot;
+        if (a.shared_endpoints) {
+            fidx = cpb;
+            if (lane == spare) {
+                if (nvalid == 1) { duty0 = dutyW = slot == 0; }
+                else { duty0 = slot == 0; dutyW = slot == 1; }
+            }
+        } else if (lane == spare) {
+            duty0 = dutyW = true;
+        }
+        if (duty0) {
+            eval_pt<D, P>(myc, tcol, scol[0], q);
+            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr)) vflag[fidx] = 0;
+        }
+        if (dutyW) {
+            eval_pt<D, P>(myc, tcol + W * P1, scol[W], q);
+            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr)) vflag[fidx] = 0;
+        }
+    }
+
+    // computeArcLength: chords between v_{i-1} and v_i, i = 1..W-1
+    double acc = 0.0;
+    if (valid && !(a.ablate & 4)) {
+        for (int j = lane; j < W - 1; j += lpc) {
+            const int i = j + 1;
+            eval_pt<D, P>(myc, tarc + (i - 1) * P1, sarc[i - 1], q);
+            eval_pt<D, P>(myc, tarc + i * P1, sarc[i], q2);
+            acc = acc + dist_nd<D>(q, q2);
+        }
+    }
+    acc = wave_sum(acc);
+    if ((tid & 63) == 0) s_wsum[tid >> 6] = acc;
+    __syncthreads();
+    if (lane == 0 && valid) {
+        const int w0 = (slot * lpc) >> 6, nw = lpc >> 6;
+        double t = s_wsum[w0];
+        for (int w = 1; w < nw; ++w) t = t + s_wsum[w0 + w];
+        const long long c = cand0 + slot;
+        const int f = s_flag[slot] & s_flag[cpb];
+        arc[c] = (f || a.arc_all) ? t : INFINITY;
+        feasible[c] = (unsigned char)f;
+        s_arc[slot] = f ? t : INFINITY;
+    }
+    __syncthreads();
+    BlockBest bb;
+    if (tid == 0) {
+        bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
+        for (int s = 0; s < nvalid; ++s) {
+            if (!(s_flag[s] & s_flag[cpb])) continue;
+            bb.count++;
+            if (s_arc[s] < bb.cost) { bb.cost = s_arc[s]; bb.idx = a.first_id + cand0 + s; }
+        }
+    }
+    finish_batch(bb, part, sync, best);
+}
+
+// ================================================================ coarse-to-fine feasibility
+// k_sspp_c2f: SamplingPathPlanner scoring, workgroup = CPB candidates (CPB = 256 / G1).
+//
+// checkCollision (include/sspp.h:132-150) stops at the first waypoint in contact, so the result
+// is an OR over waypoints and pairs; the order in which they are examined cannot change it.
+// An infeasible candidate is typically in contact over a long stretch of its path (robocrane,
+// config 2: ~55 of 129 waypoints), so a handful of well-spread waypoints finds almost all of
+// them.  The host orders the W+1 collision waypoints breadth-first by interval bisection
+// (ord table); then per workgroup:
+//   phase 1  G1 lanes per candidate test the first G1 waypoints of that order; a candidate's
+//            lanes leave the pair loop together at the first pair any of them touches
+//            (ballot over the candidate's lane group);
+//   phase 2  the survivors (few: the feasible ones plus the rare misses) are compacted in LDS
+//            and their remaining waypoints spread over all 256 lanes; a lane group that finds
+//            a contact clears the candidate's LDS flag, which stops its other lanes;
+//   phase 3  arc length for every candidate, in passes of 256/LPC candidates that keep the
+//            canonical reduction order of oracle/sspp_oracle.c::or_canon_sum;
+//   phase 4  block argmin + the fused batch argmin (finish_batch).
+// Sampling (sampleWithNoise, include/sspp.h:114-130) runs in the prologue: one Box-Muller pair
+// per thread.
+struct SsppC2F {
+    KScene sc;
+    int has_scene;
+    int ablate;
+    int insample;
+    int sampler;
+    int p, n, W;
+    double sigma;
+    unsigned long long seed;
+    long long first_id, B;
+    int g1, cpb;   // phase-1 lanes per candidate (divides 64), candidates per workgroup
+    int npts, n1;  // collision waypoints per candidate (W+1), phase-1 waypoints (<= g1)
+    int lpc;       // canonical lanes of the arc-length sum (or_lanes_for(W-1))
+    // several independent steps (batches) per launch: workgroup b belongs to step b / nblk_step;
+    // step s scores ids first_id + s * step_stride + [0, B) into arc/feasible + s * B, its own
+    // argmin records / counters (part + s * nblk_step, sync + s) and best[s]
+    int nblk_step;
+    long long step_stride;
+    int arc_all;   // 0: arc length only for collision-free candidates (+inf otherwise)
+    int hull;      // candidate hull broadphase: 0 off, 1 all candidates, 2 phase-1 survivors
+    unsigned* dfr; // [0]: candidates of this launch left undecided (cylinder-box), [1]: k_sspp_cbfix arrivals
+    int nt;        // launch shape (host side): threads per workgroup, dynamic LDS bytes
+    int lds;
+};
+
+#ifdef SSPP_C2F_STATS
+#define C2F_STAT(i, v) do { const unsigned long long v_ = (v); if ((threadIdx.x & 63) == 0 && v_) atomicAdd(&g_c2f_stats[i], v_); } while (0)
+#else
+#define C2F_STAT(i, v) do { } while (0)
+#endif
+
+// Pair loop of one waypoint per lane.  All 64 lanes run the (wave-uniform) loop; `live` lanes
+// test the pairs of their own mask.  gbits = the lanes of this lane's candidate within the
+// wave: when any of them touches, all of them stop (returns true for the group).  flag: the
+// candidate's LDS feasibility flag (phase 2), polled so lanes in other waves stop too.
+// A cylinder-box pair that passes the bounding-sphere test sets dfr (undecided) and counts as
+// no contact here (collide<..., DEFER>); k_sspp_cbfix settles it with the exact test.
+template <int D, int NM, bool ONEGEOM>
+__device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned long long mymask,
+                                           unsigned long long umask, unsigned long long gbits,
+                                           int* flag, const KScene& sc, const SceneT& T, bool& dfr) {
+    const cgeom_t geoms = (cgeom_t)T.geoms;
+    const cpair_t pairs = (cpair_t)T.pairs;
+    double mp[NM][3], mR[NM][9];
+    mover_poses<D, NM, 0>(q, (cmover_t)T.movers, mp, mR);
+    int cur = -1;
+    double gp[3], gmat[9];
+    bool have_rot = true;
+    DGeom G;
+    if (ONEGEOM) {
+        cur = pairs[0].gm;
+        G = load_geom(geoms + cur);
+        geom_pose(mp[0], mR[0], G, gp, gmat);
+    }
+    bool ghit = false;
+    const int np = sc.npairs;
+    for (int k = 0; k < np; ++k) {
+        if (k < 64) {
+            const unsigned long long rest = umask >> k;
+            if (rest == 0ull) break;
+            k += __builtin_ctzll(rest);
+            if (k >= np) break;
+        }
+        const DPair pr = load_pair(pairs + k);
+        if (!ONEGEOM && pr.gm != cur) {
+            cur = pr.gm;
+            G = load_geom(geoms + cur);
+            const bool second = NM > 1 && G.mover == 1;
+            geom_pos(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp);
+            have_rot = false;
+        }
+        int nc = 0;
+        if (live && (k >= 64 || ((mymask >> k) & 1ull))) {
+            double op_[3], om_[9];
+            const double* op = pr.opos;
+            const double* om = pr.omat;
+            if (NM > 1 && pr.omover >= 0) {
+                const bool second = pr.omover == 1;
+                const double* R = second ? mR[NM - 1] : mR[0];
+                const double* P = second ? mp[NM - 1] : mp[0];
+                double t[3];
+                matvec3(R, pr.opos, t);
+                op_[0] = P[0] + t[0]; op_[1] = P[1] + t[1]; op_[2] = P[2] + t[2];
+                matmul3(R, pr.omat, om_);
+                op = op_; om = om_;
+            }
+            const bool nr = pair_near(pr, G.rbound, gp, op, om);
+            C2F_STAT(2, __popcll(__ballot(nr)));
+            if (nr) {
+                if (!ONEGEOM && !have_rot) {
+                    const bool second = NM > 1 && G.mover == 1;
+                    geom_rot(second ? mR[NM - 1] : mR[0], G, gmat);
+                    have_rot = true;
+                }
+                int nd = 0;
+                const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
+                if (gfirst) nc = collide<false, true, false, true>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+                else nc = collide<false, true, false, true>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+                if (nc < 0) { dfr = true; nc = 0; }
+            }
+        }
+        C2F_STAT(flag ? 4 : 0, 1);                          // wave pair iterations (phase 2 / 1)
+        C2F_STAT(flag ? 5 : 1, __popcll(__ballot(live && (k >= 64 || ((mymask >> k) & 1ull)))));
+        if (__ballot(nc > 0) & gbits) { ghit = true; live = false; }
+        if (flag && live && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+            live = false;
+        if (__ballot(live) == 0ull) break;
+    }
+    return ghit;
+}
+
+// The exact cylinder-box test (witnesses + candidate search, sspd::cyl_box_overlap) of one
+// waypoint over the pairs of `mask` (k_sspp_cbfix).
+template <int D, int NM, int P, bool ONEGEOM>
+__device__ __forceinline__ bool cb_point_exact(const double* ctrl, const double* row, int span,
+                                               unsigned long long mask, int np, SceneT T) {
+    double q[D];
+    eval_pt<D, P>(ctrl, row, span, q);
+    const cgeom_t geoms = (cgeom_t)T.geoms;
+    const cpair_t pairs = (cpair_t)T.pairs;
+    double mp[NM][3], mR[NM][9];
+    mover_poses<D, NM, 0>(q, (cmover_t)T.movers, mp, mR);
+    for (int k = 0; k < np; ++k) {
+        if (k < 64 && !((mask >> k) & 1ull)) continue;
+        const DPair pr = load_pair(pairs + k);
+        const DGeom G = load_geom(geoms + pr.gm);
+        if (!((G.type == 5 && pr.otype == 6) || (G.type == 6 && pr.otype == 5))) continue;
+        const bool second = NM > 1 && G.mover == 1;
+        double gp[3], gmat[9], op_[3], om_[9];
+        geom_pose(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp, gmat);
+        const double* op = pr.opos;
+        const double* om = pr.omat;
+        if (NM > 1 && pr.omover >= 0) {
+            const bool osecond = pr.omover == 1;
+            const double* R = osecond ? mR[NM - 1] : mR[0];
+            const double* Pp = osecond ? mp[NM - 1] : mp[0];
+            double t[3];
+            matvec3(R, pr.opos, t);
+            op_[0] = Pp[0] + t[0]; op_[1] = Pp[1] + t[1]; op_[2] = Pp[2] + t[2];
+            matmul3(R, pr.omat, om_);
+            op = op_; om = om_;
+        }
+        if (!pair_near(pr, G.rbound, gp, op, om)) continue;
+        int nd = 0;
+        const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
+        const int nc = gfirst ? collide<false>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd)
+                              : collide<false>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+        if (nc > 0) return true;
+    }
+    return false;
+}
+
+#ifndef SSPP_C2F_WAVES_PER_EU
+#define SSPP_C2F_WAVES_PER_EU 4  // measured: 3 -> 1280, 4 -> 1396, 5 -> 1237, 6 -> 697 M cand/s (robocrane)
+#endif
+template <int D, int NM, int P, bool ONEGEOM, int NT>
+__global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
+    SsppC2F a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
+    const double* __restrict__ atab, const int* __restrict__ aspan,
+    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
+    const double* __restrict__ ctrl_in, const double* __restrict__ pert,
+    double* __restrict__ ctrl_out, double* __restrict__ arc, unsigned char* __restrict__ feasible,
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int P1 = P + 1;
+    constexpr int NB = 3 * NM;  // AABB extents per candidate (x, y, z per mover)
+    const int tid = threadIdx.x, cpb = a.cpb, n = a.n, W = a.W, g1 = a.g1;
+    const int lg1 = __builtin_ctz(g1);
+    const int ndof = n * D, nch = W - 1;
+    const int step = blockIdx.x / a.nblk_step, blk = blockIdx.x - step * a.nblk_step;
+    const long long cand0 = (long long)blk * cpb;
+    const int nvalid = (int)min((long long)cpb, a.B - cand0);
+    const long long first_id = a.first_id + step * a.step_stride;
+    if (a.ablate & 64) return;  // profiling: launch + dispatch cost only
+#ifdef SSPP_WG_TIMING
+    const unsigned long long wg_t0 = wall_clock64();
+    int wg_ns = -1;
+#endif
+    WG_PH(0);
+    if (step) {
+        arc += step * a.B;
+        feasible += step * a.B;
+        if (pert) pert += step * a.B * ((n - 2 * P) * D);
+        if (ctrl_out) ctrl_out += step * a.B * ndof;
+        part += step * a.nblk_step;
+        sync += step;
+        if (best) best += step;
+    }
+    double* s_ctrl = smem;                                    // [cpb][n][D]
+    double* s_lim = s_ctrl + cpb * ndof;                      // [D] sampleWithNoise limits
+    // s_box is dead once phase 2's hull masks are built (a barrier follows), so phase 3's
+    // s_vsum / s_arc reuse its space: 384 B less per 16-candidate workgroup, which lets LDS
+    // hold 16 workgroups per CU instead of 14
+    const int nvw3 = a.lpc >> 6, rbox = 2 * NB > nvw3 + 1 ? 2 * NB : nvw3 + 1;
+    double* s_box = s_lim + D;                                // [cpb][2][NB] (hull)
+    double* s_vsum = s_box;                                   // [cpb][lpc/64] (phase 3)
+    double* s_arc = s_box + cpb * nvw3;                       // [cpb] (phase 3, outputs)
+    unsigned long long* s_mask = (unsigned long long*)(s_box + cpb * rbox);  // [cpb]
+    int* s_feas = (int*)(s_mask + cpb);                       // [cpb]
+    int* s_surv = s_feas + cpb;                               // [cpb + 1] (last = count)
+    int* s_defer = s_surv + cpb + 1;                          // [cpb] undecided cylinder-box pair
+
+    // ---- prologue: control points (+ sampleWithNoise) in LDS.  Every independent global read
+    // of the prologue and phase 1 (the initial spline, the limits, this lane's phase-1 basis row)
+    // is issued here, so their L2 round trips overlap instead of following one another.
+    const int g_p1 = tid >> lg1, l_p1 = tid & (g1 - 1);
+    const int row_p1 = l_p1 < a.npts ? l_p1 : 0;
+    double N_p1[P1];
+#pragma unroll
+    for (int r = 0; r < P1; ++r) N_p1[r] = otab[row_p1 * P1 + r];
+    const int span_p1 = ospan[row_p1];
+    if (tid < D) s_lim[tid] = limits[tid];
+    {
+        if (ctrl_in) {  // element e = sl * ndof + r walked with add-with-carry
+            const int dsl = NT / ndof, dr = NT - dsl * ndof;
+            int sl = tid / ndof, r = tid - sl * ndof;
+            const double* src = ctrl_in + cand0 * ndof;
+            for (; sl < nvalid; sl += dsl) {
+                s_ctrl[sl * ndof + r] = src[sl * ndof + r];
+                r += dr;
+                if (r >= ndof) { r -= ndof; ++sl; }
+            }
+        } else {
+            // lane-owned columns: the initial spline's value is loaded once per column and
+            // stored for every candidate (LDS stores only, no load latency per element)
+            const int npert = (n - 2 * P) * D;
+            const bool from_pert = !a.insample && !(a.ablate & 1);
+            for (int rr = tid; rr < ndof; rr += NT) {
+                const double v0 = init_ctrl[rr];
+                const int k = rr - P * D;
+                const bool pr = from_pert && k >= 0 && k < npert;
+                for (int s2 = 0; s2 < cpb; ++s2)
+                    s_ctrl[s2 * ndof + rr] = (pr && s2 < nvalid) ? pert[(cand0 + s2) * npert + k] : v0;
+            }
+        }
+    }
+    if (tid < cpb) s_mask[tid] = 0ull;
+    __syncthreads();
+    if (!ctrl_in && a.insample && !(a.ablate & 1)) {
+        // sampleWithNoise: item t = (candidate sl, sampler item m), spread over the workgroup
+        const int npert = (n - 2 * P) * D;
+        const int nq = sample_items(a.sampler, npert);
+        const int total = nvalid * nq;
+        for (int t = tid; t < total; t += NT) {
+            const int sl = t / nq, m = t - sl * nq;
+            sample_item(a.sampler, a.seed, (unsigned long long)(first_id + cand0 + sl), m, npert, D, a.sigma,
+                        s_lim, s_ctrl + sl * ndof + P * D);
+        }
+        __syncthreads();
+    }
+    if (ctrl_out) {
+        double* dst = ctrl_out + cand0 * ndof;
+        for (int e = tid; e < nvalid * ndof; e += NT) dst[e] = s_ctrl[e];
+    }
+    WG_PH(1);
+
+    const SceneT TT = T;
+    const bool collide_on = a.has_scene && !(a.ablate & 2);
+    const int np = a.sc.npairs;
+    // ---- candidate-level broadphase (convex hull of the control points, see pair_may_touch):
+    // AABB per (candidate, mover, axis), then one (candidate, pair) test per thread; the mask
+    // bits are OR-ed into LDS.
+    // hull = 1: every candidate before phase 1; hull = 2 (default): only phase 1's survivors,
+    // before phase 2 — phase 1 stops at the first touching pair anyway, and on robocrane the
+    // all-candidate hull cost more than it saved (measured: 1.11 vs 1.22 G cand/s without it)
+    const int hull = (a.ablate & 32) ? 0 : a.hull;
+    if (collide_on && hull == 1) {
+        for (int e = tid; e < cpb * NB; e += NT) {
+            const int sl = e / NB, md = e - sl * NB, m = md / 3, d = md - m * 3;
+            const int col = 7 * m + d;
+            double lo, hi;
+            if (col < D) {
+                const double* c = s_ctrl + sl * ndof + col;
+                lo = hi = c[0];
+                for (int j = 1; j < n; ++j) {
+                    const double v = c[j * D];
+                    lo = v < lo ? v : lo;
+                    hi = v > hi ? v : hi;
+                }
+            } else {
+                lo = hi = (double)((cmover_t)TT.movers)[m].qpos0[d];
+            }
+            s_box[sl * 2 * NB + md] = lo;
+            s_box[sl * 2 * NB + NB + md] = hi;
+        }
+        __syncthreads();
+        if (np > 64) {
+            if (tid < cpb) s_mask[tid] = ~0ull;
+        } else {
+            for (int e = tid; e < cpb * np; e += NT) {
+                const int sl = e / np, k = e - sl * np;
+                const DPair pr = load_pair((cpair_t)TT.pairs + k);
+                const DGeom G = load_geom((cgeom_t)TT.geoms + pr.gm);
+                const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
+                const double* bx = s_box + sl * 2 * NB;
+                if (pair_may_touch(pr, G, bx + 3 * m, bx + NB + 3 * m))
+                    atomicOr(s_mask + sl, 1ull << k);
+            }
+        }
+        __syncthreads();
+    } else if (collide_on) {
+        if (tid < cpb) s_mask[tid] = ~0ull;
+        __syncthreads();
+    }
+    // ---- phase 1: G1 lanes per candidate, first n1 waypoints of the coarse-to-fine order
+    {
+        const int g = tid >> lg1, l = tid & (g1 - 1), wg = (tid & 63) >> lg1;
+        const unsigned long long low = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
+        const unsigned long long gbits = low << (wg * g1);
+        const bool valid = g < nvalid;
+        bool ghit = false, dfr = false;
+        if (collide_on) {
+            const unsigned long long mymask = s_mask[g];
+            unsigned long long umask = 0ull;  // union over the wave's groups (wave-uniform)
+            const int g0 = (tid & ~63) >> lg1;
+            for (int w = 0; w < (64 >> lg1); ++w) umask |= s_mask[g0 + w];
+            const bool live = valid && l < a.n1 && !a.sc.static_block && !(a.ablate & 16);
+            double q[D];
+            eval_pt_r<D, P>(s_ctrl + (valid ? g : 0) * ndof, N_p1, span_p1, q);
+            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mymask, umask, gbits, nullptr, a.sc, TT, dfr);
+        }
+        const bool gdef = (__ballot(dfr) & gbits) != 0ull;
+        if (l == 0) {
+            s_feas[g] = valid && !ghit && !(collide_on && a.sc.static_block);
+            s_defer[g] = gdef;
+        }
+    }
+    __syncthreads();
+    WG_PH(2);
+    // ---- phase 2: survivors' remaining waypoints over the whole workgroup
+    const int R = a.npts - a.n1;
+    if (collide_on && R > 0 && !(a.ablate & 8)) {
+        if (tid < 64) {  // survivors compacted by one wave ballot (cpb <= 64), in candidate order
+            const bool f = tid < nvalid && s_feas[tid] != 0;
+            const unsigned long long m = __ballot(f);
+            if (f) s_surv[__popcll(m & ((1ull << tid) - 1ull))] = tid;
+            if (tid == 0) s_surv[cpb] = __popcll(m);
+        }
+        __syncthreads();
+        const int ns = s_surv[cpb];
+        if (tid == 0) C2F_STAT(6, ns);
+#ifdef SSPP_WG_TIMING
+        wg_ns = ns;
+#endif
+        if (hull == 2 && ns > 0 && np <= 64) {  // the survivors' hull masks (see above)
+            for (int e = tid; e < ns * NB; e += NT) {
+                const int si = e / NB, md = e - si * NB, m = md / 3, d = md - m * 3;
+                const int sl = s_surv[si], col = 7 * m + d;
+                double lo, hi;
+                if (col < D) {
+                    const double* c = s_ctrl + sl * ndof + col;
+                    lo = hi = c[0];
+                    for (int j = 1; j < n; ++j) {
+                        const double v = c[j * D];
+                        lo = v < lo ? v : lo;
+                        hi = v > hi ? v : hi;
+                    }
+                } else {
+                    lo = hi = (double)((cmover_t)TT.movers)[m].qpos0[d];
+                }
+                s_box[sl * 2 * NB + md] = lo;
+                s_box[sl * 2 * NB + NB + md] = hi;
+            }
+            if (tid < ns) s_mask[s_surv[tid]] = 0ull;
+            __syncthreads();
+            for (int e = tid; e < ns * np; e += NT) {
+                const int si = e / np, k = e - si * np, sl = s_surv[si];
+                const DPair pr = load_pair((cpair_t)TT.pairs + k);
+                const DGeom G = load_geom((cgeom_t)TT.geoms + pr.gm);
+                const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
+                const double* bx = s_box + sl * 2 * NB;
+                if (pair_may_touch(pr, G, bx + 3 * m, bx + NB + 3 * m))
+                    atomicOr(s_mask + sl, 1ull << k);
+            }
+            __syncthreads();
+        }
+        unsigned long long umask = 0ull;
+        for (int i = 0; i < ns; ++i) umask |= s_mask[s_surv[i]];
+        const int items = ns * R;
+        for (int base = 0; base < items; base += NT) {  // workgroup-uniform trip count
+            const int it = base + tid;
+            bool live = it < items;
+            const int si = live ? it / R : 0;
+            const int s = s_surv[si];
+            const int j = a.n1 + (live ? it - si * R : 0);
+            live = live && __hip_atomic_load(s_feas + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+            // lanes of this wave that work on the same survivor
+            const int wave_it0 = base + (tid & ~63);
+            int lo = si * R - wave_it0, hi = (si + 1) * R - wave_it0;
+            lo = lo < 0 ? 0 : lo;
+            hi = hi > 64 ? 64 : hi;
+            unsigned long long gb = 0ull;
+            if (it < items && hi > lo) gb = (hi - lo >= 64) ? ~0ull : (((1ull << (hi - lo)) - 1ull) << lo);
+            double q[D];
+            eval_pt<D, P>(s_ctrl + s * ndof, otab + j * P1, ospan[j], q);
+            bool dfr = false;
+            const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s], umask, gb, s_feas + s, a.sc, TT, dfr);
+            if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    WG_PH(3);
+    // ---- phase 3: arc length (computeArcLength, include/sspp.h:152-169) of the listed
+    // candidates: the collision-free ones (findBestPath scores only successful paths), or all
+    // of them with arc_all.  Chords v_j -> v_{j+1} (v_i = s(i/(W-1))) go to LDS, then each
+    // candidate's chords are summed in the canonical order of oracle/sspp_oracle.c::or_canon_sum:
+    // lpc lane partials (chords vl, vl+lpc, ...), an xor butterfly per 64 lanes, 64-lane groups
+    // in order.
+    if (tid < cpb) s_arc[tid] = INFINITY;
+    if (!(a.ablate & 4)) {
+        __syncthreads();
+        int* s_list = s_surv;  // phase 2 is done with it
+        if (tid < 64) {  // one wave ballot, candidate order
+            const bool f = tid < nvalid && (a.arc_all || s_feas[tid] != 0);
+            const unsigned long long m = __ballot(f);
+            if (f) s_list[__popcll(m & ((1ull << tid) - 1ull))] = tid;
+            if (tid == 0) s_list[cpb] = __popcll(m);
+        }
+        __syncthreads();
+        const int nl = s_list[cpb];
+        // one wave per (listed candidate, 64-lane group v of the lpc canonical lanes): lane l
+        // accumulates chords j = 64 v + l, + lpc, ... (the lane partials of or_canon_sum), then
+        // the xor butterfly gives the group's sum.  A chord's first point is the previous lane's
+        // second point (same candidate, same pass), taken by shuffle: bit-identical to
+        // evaluating it again.  No chord array: the workgroup's LDS holds only control points.
+        const int lpc = a.lpc, nvw = lpc >> 6, lane = tid & 63;
+        for (int vw = tid >> 6; vw < nl * nvw; vw += NT / 64) {  // wave-uniform
+            const int si = vw / nvw, v = vw - si * nvw;
+            const double* myc = s_ctrl + s_list[si] * ndof;
+            double acc = 0.0;
+            for (int base = v * 64; base < nch; base += lpc) {  // wave-uniform trip count
+                const int j = base + lane, jj = j < nch ? j : nch - 1;
+                double qa[D], qb[D];
+                eval_pt<D, P>(myc, atab + (jj + 1) * P1, aspan[jj + 1], qb);
+#pragma unroll
+                for (int d = 0; d < D; ++d) qa[d] = __shfl_up(qb[d], 1, 64);
+                if (lane == 0) eval_pt<D, P>(myc, atab + jj * P1, aspan[jj], qa);
+                if (j < nch) acc = acc + dist_nd<D>(qa, qb);
+            }
+            acc = wave_sum(acc);
+            if (lane == 0) s_vsum[vw] = acc;
+        }
+        __syncthreads();
+        if (tid < nl) {
+            double t = s_vsum[tid * nvw];
+            for (int w = 1; w < nvw; ++w) t = t + s_vsum[tid * nvw + w];
+            s_arc[s_list[tid]] = t;
+        }
+    }
+    __syncthreads();
+    WG_PH(4);
+    if (tid == 0) C2F_STAT(7, nvalid);
+    if (tid < nvalid) {
+        const long long c = cand0 + tid;
+        if (s_feas[tid]) C2F_STAT(8, 0);
+        arc[c] = s_arc[tid];
+        // 2: no contact except cylinder-box pairs left undecided; k_sspp_cbfix writes 0 or 1
+        feasible[c] = (unsigned char)(s_feas[tid] == 0 ? 0 : (s_defer[tid] ? 2 : 1));
+    }
+    // block argmin over the workgroup's feasible candidates: one wave, lexicographic (cost, id)
+    // xor butterfly (exact, order independent: the lowest id wins ties like the serial scan).
+    // Undecided candidates stay out; k_sspp_cbfix merges the ones it clears.
+    BlockBest bb;
+    if (tid < 64) {
+        const bool und = tid < nvalid && s_feas[tid] != 0 && s_defer[tid] != 0;
+        const unsigned long long um = __ballot(und);
+        if (tid == 0 && um != 0ull)
+            __hip_atomic_fetch_add(a.dfr, (unsigned)__popcll(um), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool f = tid < nvalid && s_feas[tid] != 0 && !und;
+        double bc = f ? s_arc[tid] : INFINITY;
+        long long bi = f ? first_id + cand0 + tid : -1;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double oc = __shfl_xor(bc, off, 64);
+            const long long oi = __shfl_xor(bi, off, 64);
+            if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
+        }
+        bb.cost = bi < 0 ? INFINITY : bc; bb.idx = bi; bb.count = __popcll(__ballot(f)); bb.pad = 0;
+    }
+    finish_batch<NT>(bb, part, sync, best, a.nblk_step, blk);
+    WG_PH(5);
+#ifdef SSPP_WG_TIMING
+    if (tid == 0 && blockIdx.x < (1 << 16)) {
+        g_wg_t[4 * blockIdx.x] = wg_t0;
+        g_wg_t[4 * blockIdx.x + 1] = wall_clock64();
+        g_wg_t[4 * blockIdx.x + 2] = __smid();
+        g_wg_t[4 * blockIdx.x + 3] = (unsigned long long)(long long)wg_ns;
+    }
+#endif
+}
+
+// ---------------------------------------------------------------- undecided cylinder-box pairs
+// k_sspp_c2f leaves a cylinder-box pair that passes the bounding-sphere test undecided (the
+// exact test's registers would spill its whole pair loop).  A candidate with no other contact is
+// written as feasible = 2, kept out of the argmin and counted in dfr[0].  This kernel, queued
+// right after it on the same stream, gives each such candidate the exact test at every
+// collision waypoint: a contact makes it infeasible (arc +inf unless arc_all), otherwise it is
+// feasible and is merged into its step's records (block record and fused result, lexicographic
+// (cost, id) under the step's lock, count + 1), so the outputs equal a kernel that ran the exact
+// test inline.  With dfr[0] == 0 (every scene without such pairs near a path) each workgroup
+// returns after one scalar load.  The last workgroup to finish re-arms dfr.
+constexpr int kFixThreads = 256;
+constexpr int kFixBlocks = 64;
+template <int D, int NM, int P, bool ONEGEOM>
+__global__ __launch_bounds__(kFixThreads) void k_sspp_cbfix(
+    SsppC2F a, SceneT T, int steps, const double* __restrict__ otab, const int* __restrict__ ospan,
+    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
+    const double* __restrict__ ctrl_in, const double* __restrict__ pert, double* __restrict__ arc,
+    unsigned char* __restrict__ feasible, BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    if (__hip_atomic_load(a.dfr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int P1 = P + 1;
+    __shared__ int s_list[kFixThreads + 1];
+    __shared__ int s_hit;
+    const int tid = threadIdx.x, n = a.n, ndof = n * D;
+    double* s_ctrl = smem;  // [n][D]
+    const long long total = (long long)steps * a.B;
+    for (long long base = (long long)blockIdx.x * kFixThreads; base < total; base += (long long)gridDim.x * kFixThreads) {
+        const long long c0 = base + tid;
+        if (tid == 0) s_list[kFixThreads] = 0;
+        __syncthreads();
+        if (c0 < total && feasible[c0] == 2) s_list[atomicAdd(&s_list[kFixThreads], 1)] = tid;
+        __syncthreads();
+        const int nl = s_list[kFixThreads];
+        for (int i = 0; i < nl; ++i) {  // workgroup-uniform
+            const long long c = base + s_list[i];
+            const int step = (int)(c / a.B);
+            const long long cand = c - (long long)step * a.B;
+            const long long first_id = a.first_id + step * a.step_stride;
+            // the candidate's control points, exactly as k_sspp_c2f's prologue made them
+            const int npert = (n - 2 * P) * D;
+            for (int r = tid; r < ndof; r += kFixThreads) {
+                const int k = r - P * D;
+                double v = init_ctrl[r];
+                if (ctrl_in) v = ctrl_in[cand * ndof + r];
+                else if (pert && !a.insample && !(a.ablate & 1) && k >= 0 && k < npert)
+                    v = pert[((long long)step * a.B + cand) * npert + k];
+                s_ctrl[r] = v;
+            }
+            if (tid == 0) s_hit = 0;
+            __syncthreads();
+            if (!ctrl_in && a.insample && !(a.ablate & 1)) {
+                const int nq = sample_items(a.sampler, npert);
+                for (int m = tid; m < nq; m += kFixThreads)
+                    sample_item(a.sampler, a.seed, (unsigned long long)(first_id + cand), m, npert, D, a.sigma,
+                                limits, s_ctrl + P * D);
+                __syncthreads();
+            }
+            for (int j = tid; j < a.npts; j += kFixThreads) {
+                if (__hip_atomic_load(&s_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                if (cb_point_exact<D, NM, P, ONEGEOM>(s_ctrl, otab + j * P1, ospan[j], ~0ull, a.sc.npairs, T))
+                    __hip_atomic_store(&s_hit, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                if (s_hit) {
+                    feasible[c] = 0;
+                    if (!a.arc_all) arc[c] = INFINITY;
+                } else {
+                    feasible[c] = 1;
+                    const double cost = arc[c];
+                    const long long id = first_id + cand;
+                    unsigned* lock = &sync[step].top[1];
+                    while (atomicCAS(lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(2);
+                    __threadfence();
+                    BlockBest* pb = part + (long long)step * a.nblk_step + cand / a.cpb;
+                    BlockBest r = ld_rec(pb);
+                    if (better(cost, id, r.cost, r.idx)) { r.cost = cost; r.idx = id; }
+                    r.count += 1;
+                    st_rec(pb, r);
+                    if (best) {
+                        volatile sspp_best* o = best + step;
+                        if (better(cost, id, o->cost, o->index)) { o->cost = cost; o->index = id; }
+                        o->count = o->count + 1;
+                    }
+                    __threadfence();
+                    atomicExch(lock, 0u);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // the last workgroup re-arms the counters for the next launch on this job
+    if (tid == 0) {
+        __threadfence();
+        const unsigned prev = __hip_atomic_fetch_add(a.dfr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            __hip_atomic_store(a.dfr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.dfr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// ================================================================ two-kernel scoring (k_sspp_wq1/2)
+// SamplingPathPlanner scoring (include/sspp.h:194-225) shaped so that one plan() batch of 4096
+// candidates fills the chip and its slowest candidate — a feasible one, whose check must visit
+// every waypoint and every pair — runs on several waves at once.
+//   k_sspp_wq1: one TILE of cpw candidates of one step per one-wave workgroup (grid = tiles):
+//     sampleWithNoise (Philox + FP64 Box-Muller into LDS), then phase 1 — g1 = 64 / cpw lanes per
+//     candidate test the first n1 waypoints of the coarse-to-fine order (k_sspp_c2f's phase 1).  A
+//     candidate with a contact is decided (infeasible).  Every other one is a SURVIVOR: its
+//     perturbed control points and hull mask go to its record (indexed by candidate) and it joins
+//     queue shard (tile % 8).  Candidates decided feasible here (no scene, or no waypoint left)
+//     go straight to their step's feasible list.  No wave waits for another.
+//   k_sspp_wq2 (queued behind it on the stream): a survivor is nchunk x npg ITEMS — its waypoints
+//     [n1 + 64 c, n1 + 64 (c + 1)) (one per lane) against pair group g of its hull-masked pairs
+//     (the live pairs dealt round robin over npg groups).  Workgroup b drains shard b % 8 with one
+//     returning atomic add per claim (8 shards: 8 words share the claims).  A contact sets the
+//     record's hit bit; the item that finishes last (the pending count in the same 64-bit word,
+//     so its decrement returns the hit bit too) decides the candidate: cylinder-box pairs left
+//     undecided by the scan (collide<..., DEFER>) get the exact test here, out of line
+//     (wq_cb_exact, CB variant only), and a feasible candidate gets its arc length
+//     (computeArcLength, canonical order) and one entry in its step's feasible list.  A step is
+//     decided when its survivors are; the wave deciding the last one reduces the list
+//     (findBestPath: lowest arc, lowest id) into best[step].  Steps without survivors are
+//     reduced by workgroup `step` on entry.
+// Hand-offs: k_sspp_wq1 -> k_sspp_wq2 through the kernel boundary (plain stores / loads); inside
+// k_sspp_wq2 list entries and hit bits travel as 8-byte sc1 stores drained before the counter
+// add that signals them, read with sc1 loads after that add's return (cdna_hip_programming.md
+// Guideline 16, R1).  The last k_sspp_wq2 workgroup out (sharded arrival counters) re-arms the
+// queue counters; a step's reducer re-arms the step's.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+#else
+typedef unsigned gu32_t;
+typedef unsigned long long gu64_t;
+#endif
+constexpr int kWqShards = 8;
+struct WqCtr {  // per job, zeroed at creation; every counter on its own 64-byte line
+    unsigned tail[kWqShards][16];   // survivors queued per shard (k_sspp_wq1)
+    unsigned head[kWqShards][16];   // items claimed per shard (k_sspp_wq2)
+    unsigned exitc[kWqShards][16];  // k_sspp_wq2 arrivals per shard (block % 8)
+    unsigned top[16];
+    unsigned error[16];             // diagnostics: a queue entry past the capacity
+};
+struct WqStep {  // per step of a launch
+    unsigned nsurv;    // survivors (k_sspp_wq1)
+    unsigned decided;  // survivors decided (k_sspp_wq2)
+    unsigned nent;     // entries in the step's feasible list
+    unsigned count;    // feasible candidates
+    unsigned pad[12];
+};
+struct WqSurv {  // survivor record, at the candidate's index (step * B + candidate)
+    unsigned long long mask;   // hull-masked pairs (bit k: pair k may touch)
+    unsigned long long pend;   // pending items (low 32 bits) | hit (bit 32)
+    unsigned long long p1def;  // undecided cylinder-box pairs at phase-1 waypoints
+    unsigned long long pad;
+};
+struct WqEnt {  // feasible-list entry
+    unsigned long long cost, idx;
+};
+struct SsppWQ {
+    KScene sc;
+    int has_scene, ablate, sampler;
+    int p, n, W, npert;
+    double sigma;
+    unsigned long long seed;
+    long long first_id, B, step_stride;
+    int steps;
+    int cpw, g1, n1, npts, lpc, nchunk, npg, arc_all, hull;
+    unsigned tps, ntiles, nps;  // tiles per step, tiles, items per survivor (nchunk * npg)
+    long long cap;              // candidates the record / queue buffers hold
+    WqCtr* ctr;
+    WqStep* stp;
+    WqSurv* surv;               // [cap]
+    double* spert;              // survivors' perturbed control points [cap][npert]
+    unsigned* queue;            // [kWqShards][cap] record indices
+    WqEnt* list;                // feasible lists [step][B]
+};
+#define WQ_RLX __ATOMIC_RELAXED
+#define WQ_AG __HIP_MEMORY_SCOPE_AGENT
+__device__ __forceinline__ unsigned wq_add(unsigned* p, unsigned v) {
+    return __hip_atomic_fetch_add((gu32_t*)p, v, WQ_RLX, WQ_AG);
+}
+__device__ __forceinline__ void wq_st(unsigned* p, unsigned v) { __hip_atomic_store((gu32_t*)p, v, WQ_RLX, WQ_AG); }
+__device__ __forceinline__ unsigned long long wq_ld64(const unsigned long long* p) {
+    return __hip_atomic_load((gu64_t*)const_cast<unsigned long long*>(p), WQ_RLX, WQ_AG);
+}
+__device__ __forceinline__ void wq_st64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store((gu64_t*)p, v, WQ_RLX, WQ_AG);
+}
+__device__ __forceinline__ unsigned long long wq_add64(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_fetch_add((gu64_t*)p, v, WQ_RLX, WQ_AG);
+}
+__device__ __forceinline__ unsigned long long wq_or64(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_fetch_or((gu64_t*)p, v, WQ_RLX, WQ_AG);
+}
+__device__ __forceinline__ void wq_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ unsigned long long wq_bcast64(unsigned long long v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// computeArcLength (include/sspp.h:152-169) of one candidate by one wave, in the canonical
+// order of oracle/sspp_oracle.c::or_canon_sum (lpc lane partials, xor butterfly per 64 lanes,
+// 64-lane groups in order); a chord's first point is the previous lane's second (shuffle).
+template <int D, int P>
+__device__ __forceinline__ double wave_arc(const double* myc, int nch, int lpc, const double* __restrict__ atab,
+                                           const int* __restrict__ aspan) {
+    constexpr int P1 = P + 1;
+    const int lane = threadIdx.x & 63, nvw = lpc >> 6;
+    double tot = 0.0;
+    for (int v = 0; v < nvw; ++v) {  // wave-uniform
+        double acc = 0.0;
+        for (int base = v * 64; base < nch; base += lpc) {
+            const int j = base + lane, jj = j < nch ? j : nch - 1;
+            double qa[D], qb[D];
+            eval_pt<D, P>(myc, atab + (jj + 1) * P1, aspan[jj + 1], qb);
+#pragma unroll
+            for (int d = 0; d < D; ++d) qa[d] = __shfl_up(qb[d], 1, 64);
+            if (lane == 0) eval_pt<D, P>(myc, atab + jj * P1, aspan[jj], qa);
+            if (j < nch) acc = acc + dist_nd<D>(qa, qb);
+        }
+        acc = wave_sum(acc);
+        tot = v == 0 ? acc : tot + acc;
+    }
+    return tot;
+}
+
+// the exact cylinder-box test (sspd::cyl_box_overlap) of one waypoint, out of line: reached only
+// for pairs the scan left undecided, and its registers stay out of the scan loop
+template <int D, int NM, int P>
+__device__ __attribute__((noinline)) bool wq_cb_exact(const double* ctrl, const double* row, int span,
+                                                      int np, SceneT T) {
+    return cb_point_exact<D, NM, P, false>(ctrl, row, span, ~0ull, np, T);
+}
+
+// the pairs of `mask` whose rank among its set bits is g mod npg (item pair groups)
+__device__ __forceinline__ unsigned long long wq_group_mask(unsigned long long mask, int g, int npg) {
+    if (npg <= 1) return mask;
+    unsigned long long out = 0ull;
+    int r = 0;
+    for (unsigned long long m = mask; m; m &= m - 1ull, ++r)
+        if (r % npg == g) out |= m & (0ull - m);
+    return out;
+}
+
+// lane 0: one feasible-list entry (cost, id) standing for nfeas feasible candidates
+__device__ __forceinline__ void wq_append(const SsppWQ& a, int step, double cost, long long idx, unsigned nfeas) {
+    WqStep* S = a.stp + step;
+    const unsigned slot = wq_add(&S->nent, 1u);
+    WqEnt* e = a.list + (long long)step * a.B + slot;
+    wq_st64(&e->cost, (unsigned long long)__double_as_longlong(cost));
+    wq_st64(&e->idx, (unsigned long long)idx);
+    wq_add(&S->count, nfeas);
+}
+
+// whole wave: reduce step `step`'s feasible list into best[step] (the step's counters are re-armed
+// by the last k_sspp_wq2 workgroup: a step's survivor count must stay readable all launch long)
+__device__ __forceinline__ void wq_step_finish(const SsppWQ& a, int step, sspp_best* best) {
+    const int lane = threadIdx.x & 63;
+    WqStep* S = a.stp + step;
+    const unsigned ne = __builtin_amdgcn_readfirstlane(wq_add(&S->nent, 0u));
+    const unsigned cnt = __builtin_amdgcn_readfirstlane(wq_add(&S->count, 0u));
+    const WqEnt* L = a.list + (long long)step * a.B;
+    double bc = INFINITY;
+    long long bi = -1;
+    for (unsigned i = lane; i < ne; i += 64) {
+        const double c = __longlong_as_double((long long)wq_ld64(&L[i].cost));
+        const long long id = (long long)wq_ld64(&L[i].idx);
+        if (better(c, id, bc, bi)) { bc = c; bi = id; }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double oc = __shfl_xor(bc, off, 64);
+        const long long oi = __shfl_xor(bi, off, 64);
+        if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
+    }
+    if (lane == 0) {
+        if (best) {
+            best[step].cost = bi < 0 ? INFINITY : bc;
+            best[step].index = bi;
+            best[step].count = cnt;
+            best[step].reserved = 0;
+        }
+    }
+}
+
+#ifndef SSPP_WQ1_WAVES_PER_EU
+#define SSPP_WQ1_WAVES_PER_EU 4
+#endif
+#ifndef SSPP_WQ2_WAVES_PER_EU
+#define SSPP_WQ2_WAVES_PER_EU 4
+#endif
+template <int D, int NM, int P, bool ONEGEOM>
+__global__ __launch_bounds__(64, SSPP_WQ1_WAVES_PER_EU) void k_sspp_wq1(
+    SsppWQ a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
+    const double* __restrict__ atab, const int* __restrict__ aspan,
+    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
+    const double* __restrict__ ctrl_in, double* __restrict__ ctrl_out, double* __restrict__ arc,
+    unsigned char* __restrict__ feasible) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int P1 = P + 1;
+    constexpr int NB = 3 * NM;
+    if (a.ablate & 64) return;  // profiling: launch + dispatch cost only
+    const int lane = threadIdx.x;
+    const int n = a.n, ndof = n * D, cpw = a.cpw, g1 = a.g1, lg1 = __builtin_ctz(g1);
+    const int np = a.sc.npairs, npert = a.npert;
+    double* s_ctrl = smem;                // [cpw][ndof]
+    double* s_box = s_ctrl + cpw * ndof;  // [2][NB] a survivor's control-point AABB
+    const bool collide_on = a.has_scene && !(a.ablate & 2);
+    const unsigned long long glow = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
+    const unsigned id = blockIdx.x;
+    const int step = (int)(id / a.tps);
+    const long long cand0 = (long long)(id - (unsigned)step * a.tps) * cpw;
+    const int nvalid = (int)min((long long)cpw, a.B - cand0);
+    const long long gid0 = a.first_id + step * a.step_stride + cand0;
+    const long long out0 = (long long)step * a.B + cand0;
+    WQ_T(g_wq_t, id, 0, wall_clock64());
+    WQ_T(g_wq_t, id, 1, clock64());
+    // ---- control points: the initial spline + sampleWithNoise (or the caller's splines)
+    if (ctrl_in) {
+        for (int e = lane; e < nvalid * ndof; e += 64) s_ctrl[e] = ctrl_in[cand0 * ndof + e];
+    } else {
+        for (int rr = lane; rr < ndof; rr += 64) {
+            const double v0 = init_ctrl[rr];
+            for (int s2 = 0; s2 < cpw; ++s2) s_ctrl[s2 * ndof + rr] = v0;
+        }
+        __syncthreads();
+        if (!(a.ablate & 1)) {
+            const int nq = sample_items(a.sampler, npert), total = nvalid * nq;
+            for (int t = lane; t < total; t += 64) {
+                const int sl = t / nq, m = t - sl * nq;
+                sample_item(a.sampler, a.seed, (unsigned long long)(gid0 + sl), m, npert, D, a.sigma, limits,
+                            s_ctrl + sl * ndof + P * D);
+            }
+        }
+    }
+    __syncthreads();
+    if (ctrl_out) {
+        double* dst = ctrl_out + out0 * ndof;
+        for (int e = lane; e < nvalid * ndof; e += 64) dst[e] = s_ctrl[e];
+    }
+    WQ_T(g_wq_t, id, 2, clock64());
+    // ---- phase 1: g1 lanes per candidate, the first n1 coarse-to-fine waypoints, every pair
+    bool ghit = false, dfr = false;
+    const bool scan = collide_on && !a.sc.static_block;
+    {
+        const int g = lane >> lg1, l = lane & (g1 - 1);
+        if (scan) {
+            const bool live = g < nvalid && l < a.n1 && !(a.ablate & 16);
+            const int row = l < a.npts ? l : 0;
+            double q[D];
+            eval_pt<D, P>(s_ctrl + (g < nvalid ? g : 0) * ndof, otab + row * P1, ospan[row], q);
+            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, ~0ull, ~0ull, glow << (lane & ~(g1 - 1)), nullptr, a.sc, T, dfr);
+        }
+    }
+    WQ_T(g_wq_t, id, 3, clock64());
+    // ---- decide what phase 1 decided; queue the survivors
+    const unsigned long long hb = __ballot(ghit), db = __ballot(dfr);
+    const bool isc = lane < nvalid;
+    const int sh = isc ? lane * g1 : 0;
+    const bool chit = isc && collide_on && (a.sc.static_block || ((hb >> sh) & 1ull));
+    const bool cdef = isc && collide_on && !chit && (((db >> sh) & glow) != 0ull);
+    const bool csurv = isc && collide_on && !chit && (a.npts > a.n1 || cdef);
+    const bool cfeas = isc && !chit && !csurv;
+    const unsigned long long need = __ballot(a.arc_all ? isc : cfeas);
+    double my_arc = INFINITY;
+    for (unsigned long long m = need; m; m &= m - 1ull) {  // wave-uniform
+        const int g = __builtin_ctzll(m);
+        const double t = wave_arc<D, P>(s_ctrl + g * ndof, a.W - 1, a.lpc, atab, aspan);
+        if (lane == g) my_arc = t;
+    }
+    if (isc) {
+        if (!csurv) feasible[out0 + lane] = cfeas ? 1 : 0;
+        if (!csurv || a.arc_all) arc[out0 + lane] = (a.arc_all || cfeas) ? my_arc : INFINITY;
+    }
+    const unsigned long long fb = __ballot(cfeas);
+    if (fb) {  // the tile's decided-feasible candidates: one list entry (lowest arc, lowest id)
+        double bc = cfeas ? my_arc : INFINITY;
+        long long bi = cfeas ? gid0 + lane : -1;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double oc = __shfl_xor(bc, off, 64);
+            const long long oi = __shfl_xor(bi, off, 64);
+            if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
+        }
+        if (lane == 0) wq_append(a, step, bc, bi, (unsigned)__popcll(fb));
+    }
+    const unsigned long long sb = __ballot(csurv);
+    const int nsv = __popcll(sb);
+    WQ_T(g_wq_t, id, 4, clock64());
+    WQ_T(g_wq_t, id, 5, wall_clock64());
+    WQ_T(g_wq_t, id, 6, (unsigned long long)nsv);
+    WQ_T(g_wq_t, id, 7, (unsigned long long)__smid());
+    if (!nsv) return;
+    const int shard = (int)(id & (kWqShards - 1));
+    unsigned base = 0;
+    if (lane == 0) {
+        base = wq_add(&a.ctr->tail[shard][0], (unsigned)nsv);
+        wq_add(&a.stp[step].nsurv, (unsigned)nsv);
+    }
+    base = __builtin_amdgcn_readfirstlane(base);
+    int i = 0;
+    for (unsigned long long m = sb; m; m &= m - 1ull, ++i) {  // wave-uniform
+        const int g = __builtin_ctzll(m);
+        const double* c = s_ctrl + g * ndof;
+        unsigned long long hm = ~0ull;
+        if (a.hull != 0 && np <= 64 && !(a.ablate & 32)) {
+            // candidate-level broadphase (pair_may_touch): the control points' AABB per mover axis
+            if (lane < NB) {
+                const int mm = lane / 3, d = lane - mm * 3, col = 7 * mm + d;
+                double lo, hi;
+                if (col < D) {
+                    lo = hi = c[col];
+                    for (int jj = 1; jj < n; ++jj) {
+                        const double v = c[jj * D + col];
+                        lo = v < lo ? v : lo;
+                        hi = v > hi ? v : hi;
+                    }
+                } else {
+                    lo = hi = (double)((cmover_t)T.movers)[mm].qpos0[d];
+                }
+                s_box[lane] = lo;
+                s_box[NB + lane] = hi;
+            }
+            __syncthreads();
+            bool t = false;
+            if (lane < np) {
+                const DPair pr = load_pair((cpair_t)T.pairs + lane);
+                const DGeom G = load_geom((cgeom_t)T.geoms + pr.gm);
+                const int mm = (NM > 1 && G.mover == 1) ? 1 : 0;
+                t = pair_may_touch(pr, G, s_box + 3 * mm, s_box + NB + 3 * mm);
+            }
+            hm = __ballot(t);
+            __syncthreads();
+        }
+        const long long rec = out0 + g;
+        if (!ctrl_in)
+            for (int k = lane; k < npert; k += 64) a.spert[rec * npert + k] = c[P * D + k];
+        const int def_g = __shfl((int)cdef, g, 64);
+        if (lane == 0) {
+            WqSurv* R = a.surv + rec;
+            R->mask = hm;
+            R->pend = (unsigned long long)a.nps;  // pending = nps, hit = 0
+            R->p1def = (unsigned long long)(unsigned)def_g;
+            const unsigned slot = base + (unsigned)i;
+            if (slot < (unsigned)a.cap) a.queue[(long long)shard * a.cap + slot] = (unsigned)rec;
+            else wq_st(&a.ctr->error[0], 1u);
+        }
+    }
+}
+
+template <int D, int NM, int P, bool ONEGEOM, bool CB>
+__global__ __launch_bounds__(64, SSPP_WQ2_WAVES_PER_EU) void k_sspp_wq2(
+    SsppWQ a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
+    const double* __restrict__ atab, const int* __restrict__ aspan,
+    const double* __restrict__ init_ctrl, const double* __restrict__ ctrl_in, double* __restrict__ arc,
+    unsigned char* __restrict__ feasible, sspp_best* best) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int P1 = P + 1;
+    if (a.ablate & 64) return;
+    const int lane = threadIdx.x;
+    const int ndof = a.n * D, np = a.sc.npairs, npert = a.npert;
+    double* s_ctrl = smem;  // [ndof] the item's candidate
+    WqCtr* C = a.ctr;
+    const int shard = (int)(blockIdx.x & (kWqShards - 1));
+    // steps with no survivor: their candidates were all decided by k_sspp_wq1
+    if ((int)blockIdx.x < a.steps && a.stp[blockIdx.x].nsurv == 0u) wq_step_finish(a, (int)blockIdx.x, best);
+    const unsigned nps = a.nps;
+    const unsigned long long lim = (unsigned long long)C->tail[shard][0] * nps;
+    for (;;) {
+        unsigned id = 0;
+        if (lane == 0) id = wq_add(&C->head[shard][0], 1u);
+        id = __builtin_amdgcn_readfirstlane(id);
+        if ((unsigned long long)id >= lim) break;
+#ifdef SSPP_WG_TIMING
+        const unsigned tix = (unsigned)shard * 8192u + (id < 8192u ? id : 8191u);
+#endif
+        WQ_T(g_wq_i, tix, 0, wall_clock64());
+        WQ_T(g_wq_i, tix, 1, clock64());
+        const unsigned e = id / nps, r = id - e * nps;
+        const unsigned chunk = r / (unsigned)a.npg;
+        const int grp = (int)(r - chunk * (unsigned)a.npg);
+        const long long rec = (long long)a.queue[(long long)shard * a.cap + e];
+        const int step = (int)(rec / a.B);
+        const long long cand = rec - (long long)step * a.B;
+        WqSurv* R = a.surv + rec;
+        const unsigned long long mask = wq_group_mask(wq_bcast64(R->mask), grp, a.npg);
+        const bool p1def = R->p1def != 0ull;
+        const bool hit0 = (wq_bcast64(wq_ld64(&R->pend)) >> 32) != 0ull;  // a hint: may lag
+        if (!hit0) {
+            for (int rr = lane; rr < ndof; rr += 64) {
+                double v;
+                if (ctrl_in) {
+                    v = ctrl_in[cand * ndof + rr];
+                } else {
+                    v = init_ctrl[rr];
+                    const int k = rr - P * D;
+                    if (k >= 0 && k < npert) v = a.spert[rec * npert + k];
+                }
+                s_ctrl[rr] = v;
+            }
+        }
+        __syncthreads();
+        WQ_T(g_wq_i, tix, 2, clock64());
+        const int j = a.n1 + (int)chunk * 64 + lane;
+        const bool scan = !hit0 && mask != 0ull && !(a.ablate & 8);
+        const bool live = scan && j < a.npts;
+        const int row = live ? j : 0;
+        bool ghit = false, dfr = false;
+        if (scan) {
+            double q[D];
+            eval_pt<D, P>(s_ctrl, otab + row * P1, ospan[row], q);
+            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mask, mask, ~0ull, nullptr, a.sc, T, dfr);
+        }
+        WQ_T(g_wq_i, tix, 3, clock64());
+        WQ_T(g_wq_i, tix, 6, (unsigned long long)__popcll(mask) | ((unsigned long long)hit0 << 32));
+        bool anyhit = __ballot(ghit) != 0ull;
+        if (CB && scan && !anyhit && __ballot(dfr) != 0ull) {
+            bool h = false;
+            if (dfr) h = wq_cb_exact<D, NM, P>(s_ctrl, otab + row * P1, ospan[row], np, T);
+            anyhit = __ballot(h) != 0ull;
+        }
+        unsigned long long prev = 0ull;
+        if (lane == 0) {
+            if (anyhit) wq_or64(&R->pend, 1ull << 32);
+            prev = wq_add64(&R->pend, ~0ull);  // pending - 1; returns the hit bit with the count
+        }
+        prev = wq_bcast64(prev);
+        if ((unsigned)prev == 1u) {  // the survivor's last item: decide it
+            bool bad = (prev >> 32) != 0ull;
+            if (CB && !bad && p1def) {  // phase 1's undecided cylinder-box pairs, exactly
+                bool h = false;
+                if (lane < a.n1) h = wq_cb_exact<D, NM, P>(s_ctrl, otab + lane * P1, ospan[lane], np, T);
+                bad = __ballot(h) != 0ull;
+            }
+            double t = INFINITY;
+            if (!bad) t = wave_arc<D, P>(s_ctrl, a.W - 1, a.lpc, atab, aspan);
+            unsigned prev_d = 0;
+            if (lane == 0) {
+                feasible[rec] = bad ? 0 : 1;
+                if (!a.arc_all) arc[rec] = t;
+                if (!bad) wq_append(a, step, t, a.first_id + step * a.step_stride + cand, 1u);
+                wq_drain();  // the list entry is out before the decision count that signals it
+                prev_d = wq_add(&a.stp[step].decided, 1u);
+            }
+            prev_d = __builtin_amdgcn_readfirstlane(prev_d);
+            if (prev_d + 1u == a.stp[step].nsurv) wq_step_finish(a, step, best);
+        }
+        WQ_T(g_wq_i, tix, 4, clock64());
+        WQ_T(g_wq_i, tix, 5, wall_clock64());
+        WQ_T(g_wq_i, tix, 7, (unsigned long long)__smid() | ((unsigned long long)((unsigned)prev == 1u) << 32) |
+                                 ((unsigned long long)anyhit << 33));
+        __syncthreads();  // LDS is free for the next item
+    }
+    // ---- leave: the last workgroup out re-arms the queue counters for the next launch
+    if (lane == 0) {
+        const unsigned nsh = (gridDim.x - (unsigned)shard + kWqShards - 1) / kWqShards;
+        if (wq_add(&C->exitc[shard][0], 1u) == nsh - 1u) {
+            const unsigned nshards = gridDim.x < (unsigned)kWqShards ? gridDim.x : (unsigned)kWqShards;
+            if (wq_add(&C->top[0], 1u) == nshards - 1u) {
+                for (int k = 0; k < kWqShards; ++k) {
+                    wq_st(&C->tail[k][0], 0u);
+                    wq_st(&C->head[k][0], 0u);
+                    wq_st(&C->exitc[k][0], 0u);
+                }
+                for (int st = 0; st < a.steps; ++st) {
+                    wq_st(&a.stp[st].nsurv, 0u);
+                    wq_st(&a.stp[st].decided, 0u);
+                    wq_st(&a.stp[st].nent, 0u);
+                    wq_st(&a.stp[st].count, 0u);
+                }
+                wq_st(&C->top[0], 0u);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- TaskSpacePlanner kernel
+// tab: (cp+1) rows of 3 basis values at u = i * (1/cp); Minv: collocation inverse (n x n).
+#ifndef SSPP_TSP_WAVES_PER_EU
+#define SSPP_TSP_WAVES_PER_EU 3
+#endif
+#ifndef SSPP_TSP_WAVES_PER_EU_CB  // with the exact cylinder-box test (its live state doubles)
+#define SSPP_TSP_WAVES_PER_EU_CB 2
+#endif
+// CB: the scene has cylinder-box pairs (without them the exact cylinder-box code is compiled
+// out: it costs registers even when it never runs)
+template <int NM, bool ONEGEOM, bool CB>
+__global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WAVES_PER_EU) void k_tsp(
+    TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ Minv, const double* __restrict__ mean,
+    const double* __restrict__ sigma, const double* __restrict__ vias_in,
+    double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
+    double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int D = 4, P = 2, P1 = 3;
+    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, K = a.K, cp = a.cp;
+    const int slot = tid / lpc, lane = tid - slot * lpc;
+    const long long cand0 = (long long)blockIdx.x * cpb;
+    const int ndof = n * D;
+    double* s_V = smem;                      // [cpb][n][4]
+    double* s_ctrl = s_V + cpb * ndof;       // [cpb][n][4]
+    double* s_wsum = s_ctrl + cpb * ndof;    // [3][4]
+    double* s_best = s_wsum + 3 * (kBlock / 64);
+    int* s_stat = (int*)(s_best + 4);        // [cpb]
+
+    const long long nvalid = min((long long)cpb, a.B - cand0);
+    const long long nfx = a.ces ? (long long)*a.nfixed : 0;  // uniform: scalar load
+    for (int e = tid; e < cpb * 2 * D; e += kBlock) {
+        const int s = e / (2 * D), r = e - s * 2 * D;
+        if (r < D) s_V[s * ndof + r] = a.start[r];
+        else s_V[s * ndof + (n - 1) * D + (r - D)] = a.end[r - D];
+    }
+    if (vias_in) {
+        for (int e = tid; e < nvalid * K * D; e += kBlock) {
+            const int s = e / (K * D), r = e - s * K * D;
+            s_V[s * ndof + D + r] = vias_in[(cand0 + s) * K * D + r];
+        }
+    } else {
+        // Sampler::sample_set (tsp_sampler.h:12-51) with Philox streams per (candidate, via, dim)
+        for (int e = tid; e < cpb * K * D; e += kBlock) {
+            const int s = e / (K * D), r = e - s * K * D;
+            if (s >= nvalid) continue;
+            const int v = r / D, i = r - v * D;
+            long long gi = cand0 + s;
+            if (a.ces) {
+                const long long slot = a.slot0 + cand0 + s;
+                if (slot < nfx) {  // mean set / forwarded best: no sampling
+                    s_V[s * ndof + D + r] = a.fixed[(slot * K + v) * D + i];
+                    continue;
+                }
+                gi = slot - nfx;
+                if (gi >= a.samples) {  // padding slot
+                    s_V[s * ndof + D + r] = mean[v * D + i];
+                    continue;
+                }
+            }
+            const unsigned long long g = (unsigned long long)(a.first_id + gi);
+            const double m = mean[v * D + i], sg = sigma[v * D + i];
+            double val;
+            if (i < 3) {
+                bool ok = false;
+                val = 0.0;
+                for (int t = 0; t < 99; ++t) {
+                    double z0, z1;
+                    normal_pair(a.seed, g, (unsigned)(((v * 4 + i) << 7) | t), 1u, &z0, &z1);
+                    val = z0 * sg;
+                    val = val + m;
+                    if (!(val < a.lo[i] || val > a.hi[i])) { ok = true; break; }
+                }
+                if (!ok) {
+                    double u = uniform01(a.seed, g, (unsigned)(((v * 4 + i) << 7) | 127), 1u);
+                    val = u * (a.hi[i] - a.lo[i]);
+                    val = val + a.lo[i];
+                }
+                if (i == 2 && val < a.z_min) val = a.z_min;
+            } else if (a.lo[3] != a.hi[3]) {
+                double z0, z1;
+                normal_pair(a.seed, g, (unsigned)((v * 4 + 3) << 7), 1u, &z0, &z1);
+                val = z0 * sg;
+                val = val + m;
+                const double range = a.hi[3] - a.lo[3];
+                while (val < a.lo[3]) val += range;
+                while (val > a.hi[3]) val -= range;
+            } else {
+                val = m;
+            }
+            s_V[s * ndof + D + r] = val;
+        }
+    }
+    __syncthreads();
+    if (vias_out) {
+        for (int e = tid; e < nvalid * K * D; e += kBlock) {
+            const int s = e / (K * D), r = e - s * K * D;
+            vias_out[(cand0 + s) * K * D + r] = s_V[s * ndof + D + r];
+        }
+    }
+    // PathModel::fromVias: ctrl = A^-1 V (collocation inverse precomputed on the host)
+    for (int e = tid; e < cpb * ndof; e += kBlock) {
+        const int s = e / ndof, r = e - s * ndof, j = r / D, d = r - j * D;
+        const double* Vs = s_V + s * ndof;
+        double acc = Minv[j * n] * Vs[d];
+        for (int i = 1; i < n; ++i) acc = fma(Minv[j * n + i], Vs[i * D + d], acc);
+        s_ctrl[e] = acc;
+    }
+    __syncthreads();
+
+    // Evaluator::eval_one_pass (tsp_evaluator.h:18-32), waypoint i = 1..cp per lane
+    const bool valid = slot < nvalid;
+    const double* myc = s_ctrl + slot * ndof;
+    const unsigned long long mask = hull_mask<D, NM, 1>(myc, n, a.sc.npairs, (cpair_t)T.pairs,
+                                                        (cgeom_t)T.geoms, (cmover_t)T.movers);
+    double aL = 0.0, aC = 0.0, aW = 0.0;
+    // cp <= lpc: one waypoint per lane, so s((i-1)du) is the previous lane's s(i du); take it
+    // by shuffle (bit-identical: same eval_pt inputs) except on a wave's first lane
+    const bool one_pass = cp <= lpc;
+    if (valid) {
+        for (int j = lane; j < cp; j += lpc) {
+            const int i = j + 1;
+            double pv[4], pc[4];
+            eval_pt<D, P>(myc, tab + i * P1, span[i], pc);
+            if (one_pass) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pc[d], 1, 64);
+                if ((tid & 63) == 0) eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
+            } else {
+                eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
+            }
+            aL = aL + dist_nd<D>(pv, pc);
+            double c = 0.0;
+#ifndef SSPP_PROF_NOCOLL  // profiling variant only
+            point_collide<D, NM, 1, true, ONEGEOM, CB>(pc, a.sc, T, mask, &c);
+#endif
+            const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
+            const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
+            aC = aC + c;
+            aW = aW + (c + fp);
+        }
+    }
+    aL = wave_sum(aL);
+    aC = wave_sum(aC);
+    aW = wave_sum(aW);
+    constexpr int NW = kBlock / 64;
+    if ((tid & 63) == 0) {
+        s_wsum[tid >> 6] = aL;
+        s_wsum[NW + (tid >> 6)] = aC;
+        s_wsum[2 * NW + (tid >> 6)] = aW;
+    }
+    __syncthreads();
+    if (lane == 0 && valid) {
+        const int w0 = (slot * lpc) >> 6, nw = lpc >> 6;
+        double L = s_wsum[w0], Cn = s_wsum[NW + w0], Cw = s_wsum[2 * NW + w0];
+        for (int w = 1; w < nw; ++w) {
+            L = L + s_wsum[w0 + w];
+            Cn = Cn + s_wsum[NW + w0 + w];
+            Cw = Cw + s_wsum[2 * NW + w0 + w];
+        }
+        const long long c = cand0 + slot;
+        int st = Cn == 0.0;
+        double cost = L + a.w_col * Cw;
+        if (a.ces && a.slot0 + c >= nfx + a.samples) {  // padding slot
+            st = 0; cost = INFINITY; L = 0.0; Cn = 0.0; Cw = 0.0;
+        }
+        oL[c] = L; oCnf[c] = Cn; oCwf[c] = Cw; ocost[c] = cost;
+        ostatus[c] = (unsigned char)st;
+        s_stat[slot] = st;
+        s_best[slot] = cost;
+    }
+    __syncthreads();
+    BlockBest bb;
+    if (tid == 0) {
+        bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
+        for (int s = 0; s < nvalid; ++s) {
+            if (!s_stat[s]) continue;
+            bb.count++;
+            if (s_best[s] < bb.cost) { bb.cost = s_best[s]; bb.idx = a.first_id + cand0 + s; }
+        }
+    }
+    finish_batch(bb, part, sync, best);
+}
+
+// ---------------------------------------------------------------- argmin over block results
+
+
+inline int lanes_for(int items) {
+    int l = ((items + 63) / 64) * 64;
+    return std::min(std::max(l, 64), kBlock);
+}
+
+}  // namespace sspk
+
+using namespace sspk;
+
+struct sspp_scene {
+    int mode, arg, dof;
+    int count_static;
+    std::vector<DGeom> geoms;
+    std::vector<DPair> pairs;
+    std::vector<DMover> movers;
+    int n_moving_geoms = 0, n_static_geoms = 0, n_static_pairs = 0, static_contacts = 0;
+    double static_cost = 0.0;
+    DGeom* d_geoms = nullptr;
+    DPair* d_pairs = nullptr;
+    DMover* d_movers = nullptr;
+    int device = 0;
+};
+
+struct sspp_job {
+    int kind = 0;  // 0 sspp, 1 tsp
+    const sspp_scene* scene = nullptr;
+    int D = 0, p = 0, n = 0, W = 0, nknots = 0, K = 0, cp = 0;
+    int lpc = 0, cpb = 0, nm = 1, shared_endpoints = 0;
+    size_t lds = 0;
+    int64_t max_batch = 0;
+    double sigma = 0.0;
+    uint64_t seed = 0;
+    double* d_knots = nullptr;
+    double* d_tab = nullptr;   // basis rows (host-precomputed, P+1 doubles per waypoint)
+    int* d_span = nullptr;     // knot span per waypoint
+    double* d_init = nullptr;
+    double* d_limits = nullptr;
+    double* d_Minv = nullptr;
+    double* d_mean = nullptr;
+    double* d_sigma = nullptr;
+    BlockBest* d_part = nullptr;
+    double* d_pert = nullptr;  // sampler output: perturbed columns [pert_steps][max_batch][(n-2p)*D]
+    int npert = 0;
+    int pert_steps = 1;        // steps per launch the sampler buffer holds
+    int insample = 0;          // sample inside the scoring kernel (SSPP_INSAMPLE=1)
+    // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
+    int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16, nt2 = 256;
+    int shape_forced = 0;      // SSPP_NT / SSPP_G1 fix the c2f shape, else it is chosen per launch
+    int64_t part_cap = 0;      // BlockBest records d_part holds
+    int arc_all = 0;           // arc length for every candidate (else collision-free only)
+    int hull = 2;              // c2f hull broadphase (SSPP_HULL: 0 off, 1 all, 2 survivors)
+    size_t lds2 = 0;
+    double* d_otab = nullptr;  // collision rows in coarse-to-fine order
+    int* d_ospan = nullptr;
+    DPair* d_pairs = nullptr;  // this job's pair table (closest-to-the-mean-path first)
+    DPair* d_pairs_s = nullptr;  // the same without the pairs no sampled candidate can reach
+    int np_full = 0, np_samp = 0, cb_full = 0, cb_samp = 0, og_full = 1, og_samp = 1;
+    ArgminSync* d_sync = nullptr;  // sharded arrival counters of the fused argmin [kMaxSteps]
+    unsigned* d_dfr = nullptr;     // k_sspp_c2f -> k_sspp_cbfix counters (SsppC2F::dfr)
+    int has_cb = 0;                // the pair table has cylinder-box pairs (k_sspp_cbfix runs)
+    int sampler = 0;               // 0 FP64 Box-Muller pairs (default), 1 FP32 quads (opt-in)
+    // work-queue kernel (k_sspp_wq, the default: SSPP_KERNEL=2)
+    int wq = 1;
+    WqCtr* d_wctr = nullptr;       // launch counters
+    WqStep* d_wstp = nullptr;      // per-step decision counters [kMaxSteps]
+    WqSurv* d_wsurv = nullptr;     // survivor records [wq_cap]
+    double* d_wspert = nullptr;    // survivors' perturbed control points [wq_cap][npert]
+    unsigned* d_wqueue = nullptr;  // survivor queue shards [kWqShards][wq_cap]
+    WqEnt* d_wlist = nullptr;      // feasible lists [wq_cap]
+    int64_t wq_cap = 0;            // candidates per launch the buffers hold
+    int wq_occ = 0, wq_occ_lds = -1;  // resident k_sspp_wq2 workgroups (all CUs) at that LDS size
+    std::vector<double> h_knots;   // host copies: the knot vector, and the staging of
+    std::vector<double> h_stage;   // sspp_job_update_sspp's asynchronous uploads (init | limits)
+    std::vector<DPair> h_pairs, h_pairs_s;
+    double start[4], end[4], lo[4], hi[4];
+    double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
+};
+
+
+namespace sspk {
+
+inline KScene kscene(const sspp_scene* s, bool tsp) {
+    KScene k{};
+    if (!s) return k;
+    k.npairs = (int)s->pairs.size();
+    k.onegeom = 1;
+    for (const DPair& p : s->pairs) k.onegeom &= (p.gm == s->pairs[0].gm);
+    k.static_block = (!tsp && s->count_static && s->static_contacts > 0) ? 1 : 0;
+    k.static_cost = tsp ? s->static_cost : 0.0;
+    for (const DPair& p : s->pairs) {
+        const int tg = s->geoms[p.gm].type;
+        k.cylbox |= (tg == 5 && p.otype == 6) || (tg == 6 && p.otype == 5);
+    }
+    return k;
+}
+
+inline SceneT scene_t(const sspp_scene* s) {
+    SceneT t{};
+    if (!s) return t;
+    t.geoms = s->d_geoms;
+    t.pairs = s->d_pairs;
+    t.movers = s->d_movers;
+    return t;
+}
+
+
+struct SsppPtrs {
+    const double* ctrl_in;
+    double* ctrl_out;
+    double* arc;
+    unsigned char* feasible;
+    sspp_best* best;
+};
+
+template <int D, int NM, int P>
+hipError_t launch_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                              hipStream_t st) {
+    if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
+        hipLaunchKernelGGL((k_sspp<D, 1, P, true>), dim3(nblk), dim3(kBlock), j->lds, st, k,
+                           scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
+                           j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((k_sspp<D, NM, P, false>), dim3(nblk), dim3(kBlock), j->lds, st, k,
+                       scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
+                       j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
+    return hipGetLastError();
+}
+
+// the job's pair table: sampled candidates use the reachable subset, caller splines the full one
+inline SceneT scene_t_job(const sspp_job* j, bool sampled) {
+    SceneT t = scene_t(j->scene);
+    if (j->d_pairs) t.pairs = sampled ? j->d_pairs_s : j->d_pairs;
+    return t;
+}
+inline KScene kscene_job(const sspp_job* j, bool sampled) {
+    KScene k = kscene(j->scene, false);
+    if (j->d_pairs) {
+        k.npairs = sampled ? j->np_samp : j->np_full;
+        k.onegeom = sampled ? j->og_samp : j->og_full;
+        k.cylbox = sampled ? j->cb_samp : j->cb_full;
+    }
+    return k;
+}
+
+// k_sspp_cbfix after the scoring launch, only when the job's pairs include cylinder-box ones
+template <int D, int NM, int P, bool OG>
+hipError_t launch_cbfix(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                               hipStream_t st) {
+    if (!k.sc.cylbox || !k.has_scene) return hipSuccess;
+    hipLaunchKernelGGL((k_sspp_cbfix<D, NM, P, OG>), dim3(kFixBlocks), dim3(kFixThreads),
+                       sizeof(double) * j->n * D, st, k, scene_t_job(j, !o.ctrl_in), nblk / k.nblk_step, j->d_otab,
+                       j->d_ospan, j->d_init, j->d_limits, o.ctrl_in, j->d_pert, o.arc, o.feasible,
+                       j->d_part, j->d_sync, o.best);
+    return hipGetLastError();
+}
+
+template <int D, int NM, int P, int NT>
+hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                                hipStream_t st) {
+    const double* atab = j->d_tab + (size_t)(j->W + 1) * (P + 1);
+    const int* aspan = j->d_span + (j->W + 1);
+    if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
+        hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true, NT>), dim3(nblk), dim3(NT), k.lds, st, k,
+                           scene_t_job(j, !o.ctrl_in), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
+                           o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
+        const hipError_t e = hipGetLastError();
+        return e != hipSuccess ? e : launch_cbfix<D, 1, P, true>(k, j, o, nblk, st);
+    }
+    hipLaunchKernelGGL((k_sspp_c2f<D, NM, P, false, NT>), dim3(nblk), dim3(NT), k.lds, st, k,
+                       scene_t_job(j, !o.ctrl_in), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
+                       o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
+    const hipError_t e = hipGetLastError();
+    return e != hipSuccess ? e : launch_cbfix<D, NM, P, false>(k, j, o, nblk, st);
+}
+
+template <int D, int NM, int P>
+hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
+                             hipStream_t st) {
+    if (k.nt == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
+#ifdef SSPP_DEV_ONLY  // variant builds for experiments: robocrane shape only (fast compile)
+    return hipErrorInvalidValue;
+#else
+    if (k.nt == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st);
+    return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
+#endif
+}
+
+template <int D, int NM, int P, bool OG, bool CB>
+hipError_t launch_wq_t(const SsppWQ& k, sspp_job* j, const SsppPtrs& o, size_t lds, hipStream_t st) {
+    const double* atab = j->d_tab + (size_t)(j->W + 1) * (P + 1);
+    const int* aspan = j->d_span + (j->W + 1);
+    const SceneT T = scene_t_job(j, !o.ctrl_in);
+    hipLaunchKernelGGL((k_sspp_wq1<D, NM, P, OG>), dim3(k.ntiles), dim3(64), lds, st, k, T, j->d_otab, j->d_ospan,
+                       atab, aspan, j->d_init, j->d_limits, o.ctrl_in, o.ctrl_out, o.arc, o.feasible);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t lds2 = sizeof(double) * (size_t)j->n * D;
+    if (j->wq_occ_lds != (int)lds2) {  // resident k_sspp_wq2 waves: blocks per CU (occupancy API) x CUs
+        int nb = 0, dev = 0, cus = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sspp_wq2<D, NM, P, OG, CB>, 64, lds2);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        j->wq_occ = std::max(1, nb) * std::max(1, cus);
+        j->wq_occ_lds = (int)lds2;
+    }
+    // k_sspp_wq2 workgroups: one per 16 candidates of the launch (survivors are a few %), at least
+    // one per step (steps without survivors are reduced by workgroup `step`) and per shard, at most
+    // the resident waves (SSPP_WQ_G2 overrides)
+    static const int env_g2 = [] { const char* v = getenv("SSPP_WQ_G2"); return v ? atoi(v) : 0; }();
+    long long g2 = env_g2 > 0 ? env_g2 : std::min<long long>((long long)k.steps * k.B / 16, j->wq_occ);
+    g2 = std::max<long long>(g2, std::max(k.steps, kWqShards));
+    hipLaunchKernelGGL((k_sspp_wq2<D, NM, P, OG, CB>), dim3((unsigned)g2), dim3(64), lds2, st, k, T, j->d_otab,
+                       j->d_ospan, atab, aspan, j->d_init, o.ctrl_in, o.arc, o.feasible, o.best);
+    return hipGetLastError();
+}
+
+template <int D, int NM, int P>
+hipError_t launch_wq(const SsppWQ& k, sspp_job* j, const SsppPtrs& o, size_t lds, hipStream_t st) {
+    const bool og = NM == 1 && k.sc.onegeom && k.sc.npairs > 0;
+    if (k.sc.cylbox) return og ? launch_wq_t<D, 1, P, true, true>(k, j, o, lds, st)
+                               : launch_wq_t<D, NM, P, false, true>(k, j, o, lds, st);
+    return og ? launch_wq_t<D, 1, P, true, false>(k, j, o, lds, st) : launch_wq_t<D, NM, P, false, false>(k, j, o, lds, st);
+}
+
+
+// ---- per-dof entry points, instantiated one dof per translation unit (sspp_inst.hip, built
+// with -DSSPK_D=1..9) so the kernels compile in parallel; the host code (sspp_kernels.hip)
+// switches on the job's dof
+template <int D>
+hipError_t entry_wq(const SsppWQ& k, sspp_job* j, const SsppPtrs& o, size_t lds, hipStream_t st) {
+    if (j->nm == 2) {
+        if constexpr (D == 9) return j->p == 3 ? launch_wq<9, 2, 3>(k, j, o, lds, st) : launch_wq<9, 2, 2>(k, j, o, lds, st);
+        return hipErrorInvalidValue;
+    }
+#ifdef SSPP_DEV_ONLY
+    if (j->p != 3) return hipErrorInvalidValue;
+    return launch_wq<D, 1, 3>(k, j, o, lds, st);
+#else
+    return j->p == 3 ? launch_wq<D, 1, 3>(k, j, o, lds, st) : launch_wq<D, 1, 2>(k, j, o, lds, st);
+#endif
+}
+template <int D>
+hipError_t entry_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
+    if (j->nm == 2) {
+        if constexpr (D == 9) return j->p == 3 ? launch_c2f<9, 2, 3>(k, j, o, nblk, st) : launch_c2f<9, 2, 2>(k, j, o, nblk, st);
+        return hipErrorInvalidValue;
+    }
+#ifdef SSPP_DEV_ONLY
+    if (j->p != 3) return hipErrorInvalidValue;
+    return launch_c2f<D, 1, 3>(k, j, o, nblk, st);
+#else
+    return j->p == 3 ? launch_c2f<D, 1, 3>(k, j, o, nblk, st) : launch_c2f<D, 1, 2>(k, j, o, nblk, st);
+#endif
+}
+template <int D>
+hipError_t entry_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
+#ifdef SSPP_DEV_ONLY
+    (void)k; (void)j; (void)o; (void)nblk; (void)st;
+    return hipErrorInvalidValue;
+#else
+    if (j->nm == 2) {
+        if constexpr (D == 9) return j->p == 3 ? launch_sspp<9, 2, 3>(k, j, o, nblk, st) : launch_sspp<9, 2, 2>(k, j, o, nblk, st);
+        return hipErrorInvalidValue;
+    }
+    return j->p == 3 ? launch_sspp<D, 1, 3>(k, j, o, nblk, st) : launch_sspp<D, 1, 2>(k, j, o, nblk, st);
+#endif
+}
+// TaskSpacePlanner evaluation (k_tsp), its own translation unit (SSPK_D = 0)
+template <int Unused>
+hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* mean, const double* sigma,
+                     const double* d_vias, double* d_vias_out, double* d_L, double* d_Cnf, double* d_Cwf,
+                     double* d_cost, uint8_t* d_status, sspp_best* d_best, hipStream_t st) {
+    const SceneT tt = scene_t(j->scene);
+#define SSPP_LAUNCH_TSP(OG, CBV)                                                                   \
+    hipLaunchKernelGGL((k_tsp<1, OG, CBV>), dim3(nblk), dim3(kBlock), j->lds, st, k, tt, j->d_tab, \
+                       j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
+                       d_status, j->d_part, j->d_sync, d_best)
+    const bool og = k.sc.onegeom && k.sc.npairs > 0;
+    if (og && k.sc.cylbox) SSPP_LAUNCH_TSP(true, true);
+    else if (og) SSPP_LAUNCH_TSP(true, false);
+    else if (k.sc.cylbox) SSPP_LAUNCH_TSP(false, true);
+    else SSPP_LAUNCH_TSP(false, false);
+#undef SSPP_LAUNCH_TSP
+    return hipGetLastError();
+}
+
+#define SSPK_ENTRY_DECL(X, D)                                                                             \
+    X template hipError_t entry_wq<D>(const SsppWQ&, sspp_job*, const SsppPtrs&, size_t, hipStream_t);    \
+    X template hipError_t entry_c2f<D>(const SsppC2F&, const sspp_job*, const SsppPtrs&, int, hipStream_t); \
+    X template hipError_t entry_sspp<D>(const SsppK&, const sspp_job*, const SsppPtrs&, int, hipStream_t);
+#define SSPK_TSP_DECL(X)                                                                                  \
+    X template hipError_t entry_tsp<0>(const TspK&, const sspp_job*, int, const double*, const double*,    \
+                                       const double*, double*, double*, double*, double*, double*, uint8_t*, \
+                                       sspp_best*, hipStream_t);
+
+}  // namespace sspk

@@ -15,6 +15,7 @@ from ._lib import (Best, CesBuffers, CesConfig, CesInfo, CesState, ModelView, Sc
                    SsppArgs, TspArgs, check, lib)
 
 DEFAULT_SEED = 0x5EED
+SAMPLER_FP64, SAMPLER_FP32 = 0, 1  # sspp_sspp_args::sampler
 
 
 def _dptr(a):
@@ -203,9 +204,11 @@ class SsppJob(_Job):
     """SamplingPathPlanner::plan's candidate loop on the GPU (include/sspp.h:194-225)."""
 
     def __init__(self, scene, knots, degree, init_ctrl, sigma, limits, check_points,
-                 seed=DEFAULT_SEED, max_batch=4096, arc_all=False):
+                 seed=DEFAULT_SEED, max_batch=4096, arc_all=False, sampler=SAMPLER_FP64):
         """arc_all=False follows the reference: arc length only for collision-free candidates
-        (findBestPath scores only successful paths), +inf for the others."""
+        (findBestPath scores only successful paths), +inf for the others.  sampler: FP64
+        Box-Muller normals (default, as std::normal_distribution<double>) or the opt-in FP32
+        quads (SAMPLER_FP32)."""
         init_ctrl = np.ascontiguousarray(np.asarray(init_ctrl, dtype=np.float64))
         n, D = init_ctrl.shape
         self.knots = _f64(knots, n + degree + 1)
@@ -215,7 +218,9 @@ class SsppJob(_Job):
         self.max_batch = int(max_batch)
         a = SsppArgs(knots=_dptr(self.knots), degree=self.degree, init_ctrl=_dptr(init_ctrl),
                      n_ctrl=n, dof=D, sigma=float(sigma), limits=_dptr(self.limits),
-                     check_points=self.W, seed=int(seed) & (2 ** 64 - 1), arc_all=int(bool(arc_all)))
+                     check_points=self.W, seed=int(seed) & (2 ** 64 - 1), arc_all=int(bool(arc_all)),
+                     sampler=int(sampler))
+        self.sampler = int(sampler)
         h = C.c_void_p()
         check(lib().sspp_job_create_sspp(scene.handle if scene is not None else None, C.byref(a),
                                          self.max_batch, C.byref(h)), "job create (sspp)")
@@ -478,4 +483,5 @@ def device_count():
 
 __all__ = ["Model", "Scene", "SsppJob", "TspJob", "CesPlanner", "SsppSteps", "reduce_best_steps", "all_gather_records",
            "torch_stream", "interpolate", "spline_eval", "best_tensor",
-           "decode_best", "reduce_best", "reduce_best_device", "device_count", "DEFAULT_SEED", "math"]
+           "decode_best", "reduce_best", "reduce_best_device", "device_count", "DEFAULT_SEED",
+           "SAMPLER_FP64", "SAMPLER_FP32", "math"]

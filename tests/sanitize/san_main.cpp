@@ -76,7 +76,8 @@ int main(int argc, char** argv) {
         CHECK(sspp_spline_eval(knots.data(), n + p + 1, p, ctrl0.data(), dof, 0.37, e) == 0);
         std::vector<double> limits(dof, 1.0), ctrl((size_t)B * n * dof), arc(B);
         std::vector<uint8_t> feas(B);
-        or_sample_sspp(ctrl0.data(), n, dof, p, 0.08, limits.data(), 0x5EED, 0, B, ctrl.data());
+        or_sample_sspp(ctrl0.data(), n, dof, p, 0.08, limits.data(), 0x5EED, 0, B, ctrl.data(), 0);
+        or_sample_sspp(ctrl0.data(), n, dof, p, 0.08, limits.data(), 0x5EED, 0, B, ctrl.data(), 1);
         if (s) {
             CHECK(or_sspp_score(s, knots.data(), n + p + 1, p, ctrl.data(), n, dof, B, W, 0, 0, 2, 0,
                                 arc.data(), feas.data()) == 0);

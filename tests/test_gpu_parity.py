@@ -55,10 +55,28 @@ def run_sspp(job, B, first=0, with_ctrl=True):
     return res
 
 
-# scoring kernels: (SSPP_KERNEL, SSPP_G1) — coarse-to-fine k_sspp_c2f with several phase-1
-# lane-group sizes, and the one-waypoint-per-lane k_sspp
-KERNELS = [("1", "4", "64"), ("1", "8", "64"), ("1", "16", "256"), ("1", "4", "256"), ("1", "64", "64"),
-           ("1", "16", "128"), ("1", "16", "64"), ("0", "16", "256")]
+# scoring kernels: ("2", candidates per tile, pair groups per item) — the work-queue k_sspp_wq
+# (default); ("1", SSPP_G1, SSPP_NT) — coarse-to-fine k_sspp_c2f with several phase-1 lane-group
+# sizes; ("0", ...) — the one-waypoint-per-lane k_sspp
+KERNELS = [("2", "16", "1"), ("2", "4", "2"), ("2", "1", "3"), ("2", "16", "4"),
+           ("1", "4", "64"), ("1", "8", "64"), ("1", "16", "256"), ("1", "64", "64"),
+           ("1", "16", "128"), ("0", "16", "256")]
+
+
+def set_kernel(monkeypatch, kernel, a, b):
+    monkeypatch.setenv("SSPP_KERNEL", kernel)
+    if kernel == "2":
+        monkeypatch.setenv("SSPP_WQ_CPW", a)
+        monkeypatch.setenv("SSPP_WQ_NPG", b)
+    else:
+        monkeypatch.setenv("SSPP_G1", a)
+        monkeypatch.setenv("SSPP_NT", b)
+
+
+def wq_error(job):
+    """k_sspp_wq's spin-timeout word (0: every wait of the hand-off protocol was satisfied)."""
+    import sspp_amd._lib as L
+    return int(L.lib().sspp_debug_job_error(job._h))
 
 
 @pytest.mark.parametrize("arc_all", [False, True])
@@ -66,17 +84,15 @@ KERNELS = [("1", "4", "64"), ("1", "8", "64"), ("1", "16", "256"), ("1", "4", "2
 @pytest.mark.parametrize("B,W", [(4096, 128), (257, 128), (1, 128), (300, 50), (100, 256), (64, 2)])
 def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g1, nt, B, W, arc_all):
     import sspp_amd as S
-    monkeypatch.setenv("SSPP_KERNEL", kernel)
-    monkeypatch.setenv("SSPP_G1", g1)
-    monkeypatch.setenv("SSPP_NT", nt)
+    set_kernel(monkeypatch, kernel, g1, nt)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=0x5EED, max_batch=B,
                     arc_all=arc_all)
     r = run_sspp(job, B, first=1000)
-    # sampling parity (Philox + Box-Muller restated on the host)
+    # sampling parity (Philox + FP64 Box-Muller restated on the host): bit-identical
     ctrl_o = O.sample_sspp(ctrl0, 3, 0.08, np.ones(7), 0x5EED, 1000, B)
-    assert np.abs(r["ctrl"] - ctrl_o).max() <= 1e-12
+    assert np.array_equal(r["ctrl"], ctrl_o)
     # scoring parity on the exact control points the GPU scored
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], W, arc_all=arc_all)
     np.testing.assert_array_equal(r["feasible"], feas_o)
@@ -88,6 +104,7 @@ def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g
     assert idx == (idx_o + 1000 if idx_o >= 0 else -1)
     if idx_o >= 0:
         assert abs(cost - best_o) <= COST_TOL
+    assert wq_error(job) == 0
 
 
 def test_robocrane_config2_is_nontrivial(robocrane):
@@ -106,9 +123,7 @@ def test_score_ctrl_mode_matches_oracle(robocrane, monkeypatch, kernel, g1, nt):
     """Caller-supplied splines (checkCollision + computeArcLength on arbitrary ctrl)."""
     import sspp_amd as S
     import torch
-    monkeypatch.setenv("SSPP_KERNEL", kernel)
-    monkeypatch.setenv("SSPP_G1", g1)
-    monkeypatch.setenv("SSPP_NT", nt)
+    set_kernel(monkeypatch, kernel, g1, nt)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     rng = np.random.default_rng(7)
@@ -185,9 +200,7 @@ def test_stacking_tsp_matches_oracle(cuda, B, cp, K):
 def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1, nt):
     """planner.xml: block1 (free) vs static wall/block2, 7-DoF window, path through the wall."""
     import sspp_amd as S
-    monkeypatch.setenv("SSPP_KERNEL", kernel)
-    monkeypatch.setenv("SSPP_G1", g1)
-    monkeypatch.setenv("SSPP_NT", nt)
+    set_kernel(monkeypatch, kernel, g1, nt)
     model = S.Model(PLANNER)
     scene = S.Scene(model, 0, 7)
     oscene = O.Scene(mjcf_ref.load(PLANNER), 0, 7)
@@ -205,25 +218,83 @@ def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1, nt):
 
 @pytest.mark.parametrize("kernel,g1,nt", KERNELS)
 def test_cylinder_box_sspp(robocrane, monkeypatch, kernel, g1, nt):
-    """The block grazing the gripper's col_mount cylinder cap (and col_base box): k_sspp_c2f
-    decides cylinder-box pairs the 7 SAT axes leave open in phase 2b (exact, out of the pair
-    loop); feasibility, arcs and the argmin must equal the oracle's exact test."""
+    """The block grazing the gripper's col_mount cylinder cap (and col_base box): the scan loops
+    leave cylinder-box pairs that pass the bounding-sphere test undecided, and the exact test
+    settles them — k_sspp_wq in the survivor's last item (out of line), k_sspp_c2f in the
+    k_sspp_cbfix launch queued after it (candidates written as feasible = 2 until then).
+    Feasibility, arcs and the argmin must equal the oracle's exact test."""
     import sspp_amd as S
-    monkeypatch.setenv("SSPP_KERNEL", kernel)
-    monkeypatch.setenv("SSPP_G1", g1)
-    monkeypatch.setenv("SSPP_NT", nt)
+    set_kernel(monkeypatch, kernel, g1, nt)
     _, scene, oscene = robocrane
-    start = np.array([1.8, 2.2, 0.656, 1, 0, 0, 0])
-    end = np.array([2.2, 2.2, 0.656, 1, 0, 0, 0])
-    knots, ctrl0 = linear_init(start, end, 10)
-    job = S.SsppJob(scene, knots, 3, ctrl0, 0.01, np.array([1, 1, 1, .2, .2, .2, .2]), 128,
-                    seed=11, max_batch=2048)
+    knots, ctrl0 = linear_init(GRAZE_START, GRAZE_END, 10)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.01, GRAZE_LIMITS, 128, seed=11, max_batch=2048)
     r = run_sspp(job, 2048)
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 128)
     np.testing.assert_array_equal(r["feasible"], feas_o)
     assert 0 < feas_o.sum() < 2048
     assert arc_err(r["arc"], arc_o) <= COST_TOL
     assert r["best"][1] == O.argmin(arc_o, feas_o)[0]
+    assert wq_error(job) == 0
+    # the cylinder-box pair decides some candidates: without it they would be feasible
+    oscene_nocyl = O.Scene(mjcf_ref.load(ROBOCRANE), 0, 7, skip_types=(5,))
+    _, feas_nc = O.sspp_score(oscene_nocyl, knots, 3, r["ctrl"], 128)
+    assert (feas_nc.astype(int) - feas_o.astype(int)).max() == 1
+
+
+GRAZE_START = np.array([1.8, 2.2, 0.656, 1, 0, 0, 0])
+GRAZE_END = np.array([2.2, 2.2, 0.656, 1, 0, 0, 0])
+GRAZE_LIMITS = np.array([1, 1, 1, .2, .2, .2, .2])
+
+
+@pytest.mark.parametrize("kernel,insample", [("2", "1"), ("1", "1"), ("1", "0")])
+@pytest.mark.parametrize("spl", [3, 16])
+def test_cylinder_box_multistep(robocrane, monkeypatch, kernel, insample, spl):
+    """The grazing cylinder-box workload through the step executor (SsppSteps, G = 19 steps,
+    spl steps per launch, 2 streams): step > 0 indexing of the exact cylinder-box decisions
+    (k_sspp_wq items / k_sspp_c2f's k_sspp_cbfix merge into per-step records), both sampler
+    paths of k_sspp_c2f.  Every step's argmin record and its per-candidate feasibility equal the
+    oracle on that step's candidates, and some candidates turn on the cylinder-box pair."""
+    import sspp_amd as S
+    import torch
+    monkeypatch.setenv("SSPP_KERNEL", kernel)
+    monkeypatch.setenv("SSPP_INSAMPLE", insample)
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(GRAZE_START, GRAZE_END, 10)
+    B, G, stride, first = 1024, 19, 3 * 1024, 7 * 1024
+    jobs = [S.SsppJob(scene, knots, 3, ctrl0, 0.01, GRAZE_LIMITS, 128, seed=11, max_batch=B) for _ in range(2)]
+    arcs = [torch.empty(spl * B, dtype=torch.float64, device="cuda") for _ in jobs]
+    feas = [torch.empty(spl * B, dtype=torch.uint8, device="cuda") for _ in jobs]
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    ex = S.SsppSteps(jobs, streams, B, arcs, feas, steps_per_launch=spl)
+    best = torch.zeros((G, 4), dtype=torch.int64, device="cuda")
+    ex.enqueue(G, first, stride, best)
+    torch.cuda.synchronize()
+    got = best.cpu()
+    oscene_nocyl = O.Scene(mjcf_ref.load(ROBOCRANE), 0, 7, skip_types=(5,))
+    turned = 0
+    for i in range(G):
+        ctrl = O.sample_sspp(ctrl0, 3, 0.01, GRAZE_LIMITS, 11, first + i * stride, B)
+        arc_o, feas_o = O.sspp_score(oscene, knots, 3, ctrl, 128)
+        idx_o, best_o = O.argmin(arc_o, feas_o)
+        cost, idx, cnt = S.decode_best(got[i])
+        assert cnt == int(feas_o.sum()), i
+        assert idx == (idx_o + first + i * stride if idx_o >= 0 else -1), i
+        if idx_o >= 0:
+            assert abs(cost - best_o) <= COST_TOL
+        _, feas_nc = O.sspp_score(oscene_nocyl, knots, 3, ctrl, 128)
+        turned += int((feas_nc.astype(int) - feas_o.astype(int)).max() == 1)
+        if i % (2 * spl) < spl and i // spl == (G - 1) // spl:  # the last launch of branch 0
+            pass
+    assert turned > 0
+    # per-candidate feasibility of the last launch on branch 0 (its scratch outputs)
+    last0 = max(l for l in range((G + spl - 1) // spl) if l % 2 == 0)
+    for k in range(min(spl, G - last0 * spl)):
+        i = last0 * spl + k
+        ctrl = O.sample_sspp(ctrl0, 3, 0.01, GRAZE_LIMITS, 11, first + i * stride, B)
+        _, feas_o = O.sspp_score(oscene, knots, 3, ctrl, 128)
+        np.testing.assert_array_equal(feas[0][k * B:(k + 1) * B].cpu().numpy(), feas_o)
+    for j in jobs:
+        assert wq_error(j) == 0
 
 
 @pytest.mark.parametrize("kernel", ["0", "1"])
@@ -259,7 +330,7 @@ def test_fused_argmin_back_to_back(robocrane, monkeypatch, insample, kernel):
     assert np.abs(r["ctrl"] - O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 0x5EED, 77, 257)).max() <= 1e-12
 
 
-@pytest.mark.parametrize("spl", [1, 3, 16])
+@pytest.mark.parametrize("spl", [1, 3, 16, 20, 32])
 def test_step_executor_matches_eager(robocrane, spl):
     """C++ step executor: G steps, spl per launch, launches round robin over 3 streams; every
     step's argmin record equals a single eager launch on the same candidate ids."""
@@ -282,6 +353,27 @@ def test_step_executor_matches_eager(robocrane, spl):
         jobs[0].sample_score(first + i * stride, B, ref["arc"], ref["feasible"], ref["best"])
         torch.cuda.synchronize()
         assert S.decode_best(got[i]) == S.decode_best(ref["best"]), i
+    for j in jobs:
+        assert wq_error(j) == 0
+
+
+@pytest.mark.parametrize("kernel", ["2", "1"])
+def test_fp32_sampler_opt_in(robocrane, monkeypatch, kernel):
+    """The opt-in FP32 Box-Muller quads (sampler = 1): candidates bit-identical to the oracle's
+    or_normal_quad, scoring parity as with the FP64 default, and the two samplers differ."""
+    import sspp_amd as S
+    monkeypatch.setenv("SSPP_KERNEL", kernel)
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    B = 1500
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=B, sampler=S.SAMPLER_FP32)
+    r = run_sspp(job, B, first=321)
+    want = O.sample_sspp(ctrl0, 3, 0.08, np.ones(7), 0x5EED, 321, B, sampler=O.SAMPLER_FP32)
+    assert np.array_equal(r["ctrl"], want)
+    assert not np.array_equal(want, O.sample_sspp(ctrl0, 3, 0.08, np.ones(7), 0x5EED, 321, B))
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 128)
+    np.testing.assert_array_equal(r["feasible"], feas_o)
+    assert arc_err(r["arc"], arc_o) <= COST_TOL
 
 
 def test_reduce_best_steps(cuda):

@@ -115,9 +115,35 @@ def test_philox_known_answer():
 
 
 def test_normal_sampler_statistics():
-    z = np.array([O.normal_pair(7, g, m, 0) for g in range(2000) for m in range(4)]).ravel()
-    assert abs(z.mean()) < 0.03
-    assert abs(z.std() - 1.0) < 0.03
+    """FP64 Box-Muller pairs (the default sampler of both planners): moments, tails, pairing."""
+    z = np.array([O.normal_pair(7, g, m, 0) for g in range(20000) for m in range(2)]).ravel()
+    assert abs(z.mean()) < 0.01
+    assert abs(z.std() - 1.0) < 0.01
+    assert abs(np.mean(z ** 4) - 3.0) < 0.1
+    for q, x in ((0.5, 0.0), (0.8413, 1.0), (0.9772, 2.0), (0.99865, 3.0)):
+        assert abs((z < x).mean() - q) < 0.01
+    assert abs(np.corrcoef(z[0::2], z[1::2])[0, 1]) < 0.02
+
+
+def test_normal_pair64_accuracy():
+    """The written-out FP64 ln / sincos polynomials of the default sampler agree with libm to a
+    few ulp over 200k normals (std::normal_distribution<double> precision class), the maximum
+    |z| is reachable (u1 = 2^-53 -> sqrt(-2 ln 2^-53) = 8.5717) and u1 = 1 gives exactly 0."""
+    worst = 0.0
+    for g in range(50000):
+        for m in range(2):
+            a = np.array(O.normal_pair(3, g, m, 0))
+            b = np.array(O.normal_pair(3, g, m, 0, libm=True))
+            worst = max(worst, float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-3))))
+    assert worst < 2e-15, worst
+    import ctypes as C
+    lib = O.lib()
+    lib.or_bm_log64_test.restype = C.c_double
+    lib.or_bm_log64_test.argtypes = [C.c_double]
+    for u in (2.0 ** -53, 1e-9, 0.3, 0.70710678118654757, 0.7071067811865476, 0.5, 0.999999, 1.0):
+        assert abs(lib.or_bm_log64_test(u) - np.log(u)) <= 2.5e-16 * max(1.0, abs(np.log(u)))
+    assert lib.or_bm_log64_test(1.0) == 0.0
+    assert abs(np.sqrt(-2.0 * lib.or_bm_log64_test(2.0 ** -53)) - 8.5717) < 1e-4
 
 
 def test_normal_quad_statistics():

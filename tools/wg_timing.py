@@ -16,7 +16,8 @@ from sspp_amd import _lib  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 out_path = sys.argv[2] if len(sys.argv) > 2 else None
-sys.argv = ["bench.py", "--steps", str(steps), "--warmup", "5", "--no-cpu-baseline"]
+sys.argv = ["bench.py", "--steps", str(steps), "--warmup", "5", "--no-cpu-baseline",
+            "--steps-per-launch", str(min(steps, 32))]
 args = bench.parse()
 device = torch.device("cuda", 0)
 B, step, kernel_only, bytes_per, flops_per, meta, ctx = bench.setup_robocrane(args, device)
@@ -25,7 +26,8 @@ run(5)
 torch.cuda.synchronize()
 run(steps)
 torch.cuda.synchronize()
-nwg = steps * (B // (64 // int(os.environ.get("SSPP_G1", "4"))))  # NT = 64: cpb = 64 / G1
+nt, g1 = int(os.environ.get("SSPP_NT", "64")), int(os.environ.get("SSPP_G1", "4"))
+nwg = steps * (B // (nt // g1))  # candidates per workgroup: NT / G1
 buf = (C.c_ulonglong * (4 * nwg))()
 _lib.lib().__getattr__("sspp_debug_wg_times")(buf, 4 * nwg)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 4).astype(np.int64)
