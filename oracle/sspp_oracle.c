@@ -688,10 +688,13 @@ static int col_plane_box(const double* pp, const double* pm, const double* bp, c
     for (int j = 0; j < 3; ++j) { col3(bm, j, ax); a[j] = dot3(n, ax) * e[j]; }
     int nc = 0, nd = 0;
     for (int k = 0; k < 8; ++k) {
-        double t = d0 + ((k & 1) ? a[0] : -a[0]);
-        t = t + ((k & 2) ? a[1] : -a[1]);
-        t = t + ((k & 4) ? a[2] : -a[2]);
-        if (t < margin && nc < 4) { nc++; if (t < DEEP) nd++; }
+        double l = (k & 1) ? a[0] : -a[0];  // corner height over the box centre (MuJoCo's ldist)
+        l = l + ((k & 2) ? a[1] : -a[1]);
+        l = l + ((k & 4) ? a[2] : -a[2]);
+        const double t = d0 + l;
+        // mjc_PlaneBox: a corner counts unless dist + ldist > margin or ldist > 0 (the corners
+        // of the half turned away from the plane never count), at most 4
+        if (!(t > margin) && !(l > 0.0) && nc < 4) { nc++; if (t < DEEP) nd++; }
     }
     *ndeep = nd;
     return nc;
@@ -704,27 +707,28 @@ static int col_plane_sphere(const double* pp, const double* pm, const double* sp
     d[0] = sp[0] - pp[0]; d[1] = sp[1] - pp[1]; d[2] = sp[2] - pp[2];
     double dist = dot3(d, n) - r;
     *ndeep = dist < DEEP;
-    return dist < margin;
+    return dist <= margin;  // mjc_PlaneSphere: no contact only when dist > margin
 }
 
 static int col_plane_cyl(const double* pp, const double* pm, const double* cp, const double* cm,
                          const double* sz, double margin, int* ndeep) {
+    // mjc_PlaneCylinder: the deepest rim point of the cap nearer the plane (p1) decides whether
+    // there is any contact (dist <= margin); then the matching rim point of the far cap (p2) and
+    // two "triangle" points on the near cap at +-120 degrees from p1 (pt, height -prjvec / 2),
+    // each counted when within the margin: up to 4 contacts
     double n[3], a[3], d[3];
     col3(pm, 2, n);
     col3(cm, 2, a);
     d[0] = cp[0] - pp[0]; d[1] = cp[1] - pp[1]; d[2] = cp[2] - pp[2];
-    double dn = dot3(d, n), na = dot3(n, a);
-    double s = 1.0 - na * na;
-    double rim = sz[0] * sqrt(s > 0.0 ? s : 0.0);
-    double ha = sz[1] * na;
-    int nc = 0, nd = 0;
-    for (int c = 0; c < 2; ++c) {
-        double t = (c == 0) ? dn - ha : dn + ha;
-        t = t - rim;
-        if (t < margin) { nc++; if (t < DEEP) nd++; }
-    }
-    *ndeep = nd;
-    return nc;
+    const double dn = dot3(d, n), na = dot3(n, a);
+    const double s = 1.0 - na * na;
+    const double rim = sz[0] * sqrt(s > 0.0 ? s : 0.0);
+    const double ha = sz[1] * fabs(na);
+    const double nearc = dn - ha;
+    const double p1 = nearc - rim, p2 = (dn + ha) - rim, pt = nearc + 0.5 * rim;
+    if (p1 > margin) { *ndeep = 0; return 0; }
+    *ndeep = (p1 < DEEP) + (p2 < DEEP) + 2 * (pt < DEEP);
+    return 1 + (p2 <= margin) + 2 * (pt <= margin);
 }
 
 static int col_sphere_sphere(const double* p1, double r1, const double* p2, double r2,
@@ -732,7 +736,7 @@ static int col_sphere_sphere(const double* p1, double r1, const double* p2, doub
     double d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
     double dist = sqrt(dot3(d, d)) - (r1 + r2);
     *ndeep = dist < DEEP;
-    return dist < margin;
+    return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 
 static int col_sphere_box(const double* sp, double r, const double* bp, const double* bm,
@@ -750,7 +754,7 @@ static int col_sphere_box(const double* sp, double r, const double* bp, const do
     }
     double dist = inside ? (-mind - r) : (sqrt(out2) - r);
     *ndeep = dist < DEEP;
-    return dist < margin;
+    return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 
 static int col_sphere_cyl(const double* sp, double r, const double* cp, const double* cm,
@@ -768,7 +772,7 @@ static int col_sphere_cyl(const double* sp, double r, const double* cp, const do
         dist = sqrt(fma(orr, orr, oz * oz)) - r;
     }
     *ndeep = dist < DEEP;
-    return dist < margin;
+    return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 
 /* Separating-axis test for two boxes: dist = max over the 15 axes of the signed

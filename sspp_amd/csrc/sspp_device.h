@@ -165,10 +165,13 @@ SSPP_HD int col_plane_box(const double* pp, const double* pm, const double* bp, 
     int nc = 0, ndd = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        double t = d0 + ((k & 1) ? a[0] : -a[0]);
-        t = t + ((k & 2) ? a[1] : -a[1]);
-        t = t + ((k & 4) ? a[2] : -a[2]);
-        if (t < margin && nc < 4) { nc++; if (t < kDeep) ndd++; }
+        double l = (k & 1) ? a[0] : -a[0];  // corner height over the box centre (MuJoCo's ldist)
+        l = l + ((k & 2) ? a[1] : -a[1]);
+        l = l + ((k & 4) ? a[2] : -a[2]);
+        const double t = d0 + l;
+        // mjc_PlaneBox: a corner counts unless dist + ldist > margin or ldist > 0 (the corners
+        // of the half turned away from the plane never count), at most 4
+        if (!(t > margin) && !(l > 0.0) && nc < 4) { nc++; if (t < kDeep) ndd++; }
     }
     *nd = ndd;
     return nc;
@@ -180,34 +183,34 @@ SSPP_HD int col_plane_sphere(const double* pp, const double* pm, const double* s
     d[0] = sp[0] - pp[0]; d[1] = sp[1] - pp[1]; d[2] = sp[2] - pp[2];
     double dist = dot3(d, n) - r;
     *nd = dist < kDeep;
-    return dist < margin;
+    return dist <= margin;  // mjc_PlaneSphere: no contact only when dist > margin
 }
 SSPP_HD int col_plane_cyl(const double* pp, const double* pm, const double* cp, const double* cm,
                           const double* sz, double margin, int* nd) {
+    // mjc_PlaneCylinder: the deepest rim point of the cap nearer the plane (p1) decides whether
+    // there is any contact (dist <= margin); then the matching rim point of the far cap (p2) and
+    // two "triangle" points on the near cap at +-120 degrees from p1 (pt, height -prjvec / 2),
+    // each counted when within the margin: up to 4 contacts
     double n[3], a[3], d[3];
     col3(pm, 2, n);
     col3(cm, 2, a);
     d[0] = cp[0] - pp[0]; d[1] = cp[1] - pp[1]; d[2] = cp[2] - pp[2];
-    double dn = dot3(d, n), na = dot3(n, a);
-    double s = 1.0 - na * na;
-    double rim = sz[0] * sqrt(s > 0.0 ? s : 0.0);
-    double ha = sz[1] * na;
-    int nc = 0, ndd = 0;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        double t = (c == 0) ? dn - ha : dn + ha;
-        t = t - rim;
-        if (t < margin) { nc++; if (t < kDeep) ndd++; }
-    }
-    *nd = ndd;
-    return nc;
+    const double dn = dot3(d, n), na = dot3(n, a);
+    const double s = 1.0 - na * na;
+    const double rim = sz[0] * sqrt(s > 0.0 ? s : 0.0);
+    const double ha = sz[1] * fabs(na);
+    const double nearc = dn - ha;
+    const double p1 = nearc - rim, p2 = (dn + ha) - rim, pt = nearc + 0.5 * rim;
+    if (p1 > margin) { *nd = 0; return 0; }
+    *nd = (p1 < kDeep) + (p2 < kDeep) + 2 * (pt < kDeep);
+    return 1 + (p2 <= margin) + 2 * (pt <= margin);
 }
 SSPP_HD int col_sphere_sphere(const double* p1, double r1, const double* p2, double r2,
                               double margin, int* nd) {
     double d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
     double dist = sqrt(dot3(d, d)) - (r1 + r2);
     *nd = dist < kDeep;
-    return dist < margin;
+    return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 SSPP_HD int col_sphere_box(const double* sp, double r, const double* bp, const double* bm,
                            const double* e, double margin, int* nd) {
@@ -225,7 +228,7 @@ SSPP_HD int col_sphere_box(const double* sp, double r, const double* bp, const d
     }
     double dist = inside ? (-mind - r) : (sqrt(out2) - r);
     *nd = dist < kDeep;
-    return dist < margin;
+    return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 SSPP_HD int col_sphere_cyl(const double* sp, double r, const double* cp, const double* cm,
                            const double* sz, double margin, int* nd) {
@@ -242,9 +245,13 @@ SSPP_HD int col_sphere_cyl(const double* sp, double r, const double* cp, const d
         dist = sqrt(fma(orr, orr, oz * oz)) - r;
     }
     *nd = dist < kDeep;
-    return dist < margin;
+    return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 
+// Overlap witness for two boxes: the centre of one strictly inside the other.  Then every SAT
+// axis L has |T.L| < ra(L) (T = sum t_k A_k with |t_k| < e_k), so each separation is below
+// -rb < 0 <= margin and sat_box_box reports the contact too; this settles the deep penetrations
+// of colliding candidates with 3 dot products instead of the 15-axis test.
 // Separating-axis test, two boxes: true iff every one of the 15 axis separations < thr.
 // Rows of R = A^T B are formed lazily so that an early separating face of A (the common
 // case: the moving box hovering over a static box) skips the rest.  Edge axes compare the

@@ -1147,7 +1147,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     // ---- prologue: control points (+ sampleWithNoise) in LDS.  Every independent global read
     // of the prologue and phase 1 (the initial spline, the limits, this lane's phase-1 basis row)
     // is issued here, so their L2 round trips overlap instead of following one another.
-    const int g_p1 = tid >> lg1, l_p1 = tid & (g1 - 1);
+    const int l_p1 = tid & (g1 - 1);
     const int row_p1 = l_p1 < a.npts ? l_p1 : 0;
     double N_p1[P1];
 #pragma unroll
@@ -1185,10 +1185,12 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         const int npert = (n - 2 * P) * D;
         const int nq = sample_items(a.sampler, npert);
         const int total = nvalid * nq;
-        for (int t = tid; t < total; t += NT) {
-            const int sl = t / nq, m = t - sl * nq;
-            sample_item(a.sampler, a.seed, (unsigned long long)(first_id + cand0 + sl), m, npert, D, a.sigma,
-                        s_lim, s_ctrl + sl * ndof + P * D);
+        {
+            for (int t = tid; t < total; t += NT) {
+                const int sl = t / nq, m = t - sl * nq;
+                sample_item(a.sampler, a.seed, (unsigned long long)(first_id + cand0 + sl), m, npert, D, a.sigma,
+                            s_lim, s_ctrl + sl * ndof + P * D);
+            }
         }
         __syncthreads();
     }
@@ -2381,8 +2383,8 @@ template <int D, int NM, int P>
 hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
                              hipStream_t st) {
     if (k.nt == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
-#ifdef SSPP_DEV_ONLY  // variant builds for experiments: robocrane shape only (fast compile)
-    return hipErrorInvalidValue;
+#ifdef SSPP_DEV_ONLY  // variant builds for experiments: robocrane shapes only (fast compile)
+    return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
 #else
     if (k.nt == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st);
     return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);

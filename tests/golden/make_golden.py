@@ -85,6 +85,23 @@ def main():
     tc = bs.knot_vector(7, 3)
     out["const_vals"] = np.array([bs.bspline(x, tc, np.ones((7, 9)), 3) for x in th])
 
+    # (vi) the reference's robot path pipeline (scripts/main_bspline.py:198-209): 7 via points
+    # in 9-D (7 robocrane joints + 2 passive zeros), k = 2, compute_control_points -> ctr_pts,
+    # knot_vec.  Its saved bspline_params.npy is a pickled dict that the safe loader refuses
+    # (numpy.load(allow_pickle=False)), so the via points here are seeded joint-angle-like values;
+    # the knot vector is the one SURVEY §8c recorded from that file.  Outputs: bspline() on the
+    # arc-length grid of 128 check points and its arc length.
+    rng = np.random.default_rng(2025)
+    via = np.zeros((7, 9))
+    via[:, :7] = np.cumsum(rng.uniform(-0.35, 0.35, size=(7, 7)), axis=0)
+    ctrl, t = bs.compute_control_points(via, 2)
+    W = 128
+    u = np.array([i / (W - 1) for i in range(W)])
+    pts = np.array([bs.bspline(ui, t, ctrl, 2) for ui in u])
+    chords = np.linalg.norm(pts[1:] - pts[:-1], axis=1)
+    out.update(robot_via=via, robot_ctrl=ctrl, robot_knots=np.asarray(t, np.float64), robot_u=u,
+               robot_pts=pts, robot_arc=np.array([sum(float(c) for c in chords)]))
+
     # (v) CubicPath
     cp = cpm.CubicPath()
     start, viap, end = np.array([0.0, 0.5, 1.0]), np.array([0.7, 1.2, 0.3]), np.array([2.0, 0.0, 0.5])

@@ -55,7 +55,9 @@ def test_box_on_plane_corner_contacts():
     assert (n, nd) == (4, 4)
     assert cost == pytest.approx(4 * -1.0 / (0.25 + 1e-4), rel=1e-15)
     assert contacts([FLOOR], [box], (0, 0, 0.2995))[:3:2] == (4, 0)  # shallow: contact, not deep
-    assert contacts([FLOOR], [box], (0, 0, 0.3))[0] == 0  # touching: dist == 0 is not < margin
+    # touching: MuJoCo's colliders drop a contact only when dist > margin (dist == 0 counts)
+    assert contacts([FLOOR], [box], (0, 0, 0.3))[0] == 4
+    assert contacts([FLOOR], [box], (0, 0, 0.3001))[0] == 0
     assert contacts([FLOOR], [box], (0, 0, 0.0))[0] == 4  # fully below: capped at 4 (MuJoCo)
     tilted = contacts([FLOOR], [box], (0, 0, 0.3), quat_axis([1, 0, 0], 0.1))
     assert tilted[0] == 2  # one edge dips below
@@ -72,9 +74,74 @@ def test_sphere_and_cylinder_on_plane():
     assert contacts([FLOOR], [sph], (0, 0, 0.05))[:3:2] == (1, 1)
     assert contacts([FLOOR], [sph], (0, 0, 0.11))[0] == 0
     cyl = (CYL, (0.05, 0.1), (0, 0, 0), (1, 0, 0, 0))
-    assert contacts([FLOOR], [cyl], (0, 0, 0.09))[:3:2] == (1, 1)  # lower cap only
+    # standing 1 cm deep: the lower cap's "deepest rim point" (any, the rim is level) and the two
+    # triangle points of mjc_PlaneCylinder, all 1 cm deep
+    assert contacts([FLOOR], [cyl], (0, 0, 0.09))[:3:2] == (3, 3)
     lying = quat_axis([1, 0, 0], math.pi / 2)
-    assert contacts([FLOOR], [cyl], (0, 0, 0.04), lying)[:3:2] == (2, 2)  # both cap rims
+    # lying 1 cm deep: both caps' lowest rim points; the triangle points sit 2.5 cm above
+    assert contacts([FLOOR], [cyl], (0, 0, 0.04), lying)[:3:2] == (2, 2)
+    assert contacts([FLOOR], [cyl], (0, 0, 0.0495), lying)[:3:2] == (2, 0)  # 0.5 mm: 2 contacts, not deep
+
+
+def mj_plane_box_count(h, R, e, margin):
+    """Contacts of a box over the z = 0 plane by the rule of MuJoCo's published mjc_PlaneBox
+    (centre height h, rotation R, half extents e): corners in bit order, skip when
+    dist + ldist > margin or ldist > 0, at most 4; returns (count, deep count)."""
+    n = d = 0
+    for i in range(8):
+        v = np.array([e[0] if i & 1 else -e[0], e[1] if i & 2 else -e[1], e[2] if i & 4 else -e[2]])
+        ld = (R @ v)[2]
+        if h + ld > margin or ld > 0:
+            continue
+        n += 1
+        d += (h + ld) < -1e-3
+        if n >= 4:
+            break
+    return n, d
+
+
+def mj_plane_cyl_count(h, axis, r, hh, margin):
+    """Contacts of a cylinder over the z = 0 plane by the rule of MuJoCo's published
+    mjc_PlaneCylinder: the near cap's deepest rim point first (none at all when it is above the
+    margin), the far cap's, and two triangle points on the near cap at -prjvec / 2."""
+    nrm = np.array([0.0, 0.0, 1.0])
+    axis = np.asarray(axis, float)
+    pa = nrm @ axis
+    if pa > 0:
+        axis, pa = -axis, -pa
+    vec = axis * pa - nrm
+    ln = np.linalg.norm(vec)
+    prjvec = (vec * (r / ln)) @ nrm if ln > 1e-15 else 0.0
+    pa *= hh
+    pts = [h + pa + prjvec, h - pa + prjvec, h + pa - 0.5 * prjvec, h + pa - 0.5 * prjvec]
+    if pts[0] > margin:
+        return 0, 0
+    keep = [pts[0]] + ([pts[1]] if pts[1] <= margin else []) + (pts[2:] if pts[2] <= margin else [])
+    return len(keep), sum(p < -1e-3 for p in keep)
+
+
+def test_plane_box_and_cylinder_match_mujoco_rules():
+    """Random boxes and cylinders around the floor: the oracle's contact and deep-contact counts
+    equal the published MuJoCo plane colliders' rules restated independently above (counts,
+    margin boundary, the corner half turned away from the plane, the cylinder triangle points)."""
+    rng = np.random.default_rng(5)
+    for trial in range(300):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        w, x, y, z = q
+        R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                      [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+        margin = [0.0, 0.002][trial % 2]
+        e = rng.uniform(0.02, 0.2, size=3)
+        h = rng.uniform(-0.3, 0.3)
+        box = (BOX, tuple(e), (0, 0, 0), (1, 0, 0, 0), margin)
+        got = contacts([FLOOR], [box], (0, 0, h), tuple(q))
+        assert (got[0], got[2]) == mj_plane_box_count(h, R, e, margin), trial
+        r, hh = rng.uniform(0.02, 0.1), rng.uniform(0.02, 0.2)
+        cyl = (CYL, (r, hh), (0, 0, 0), (1, 0, 0, 0), margin)
+        got = contacts([FLOOR], [cyl], (0, 0, h), tuple(q))
+        assert (got[0], got[2]) == mj_plane_cyl_count(h, R[:, 2], r, hh, margin), trial
 
 
 def test_box_box_axis_aligned():
@@ -188,7 +255,9 @@ def test_stacking_tsp_cost(robocrane):
     s = O.Scene(m, 1, 1)  # block1
     assert s.npairs() == (3, 3)  # block1 vs floor/block2/block3; block2-floor, block3-floor, 2-3
     n, cost, nd = s.contacts(np.array([0.205, 0.0, 0.12, 0.0]))
-    assert (n, cost) == (0, 0.0)
+    # block1 clear of everything; block2 and block3 rest on the floor at distance exactly 0,
+    # which MuJoCo's plane-box collider counts (4 corners each, none deep): no cost
+    assert (n, cost, nd) == (8, 0.0, 0)
     # overlapping block2 by 50 mm in x, face to face: the manifold's 4 corners are all deep
     # (Collision.h:89-101 adds one term per contact), centre distance 0.15
     n, cost, nd = s.contacts(np.array([0.15, 0.0, 0.1, 0.0]))

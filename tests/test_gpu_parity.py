@@ -157,6 +157,26 @@ def test_config1_bsplines_golden(cuda, golden):
     assert _np(out["feasible"]).all()
 
 
+def test_robot_path_d9_p2_golden(cuda, golden):
+    """The reference's robot path pipeline (scripts/main_bspline.py:198-209): a degree-2 spline
+    through 7 via points in 9-D (knots [0,0,0,.2,.4,.6,.8,1,1,1]); control points from the
+    reference's compute_control_points, arc length on 128 points from its bspline().  The GPU's
+    computeArcLength of that spline equals the reference's to 1e-12 and the oracle's exactly."""
+    import sspp_amd as S
+    import torch
+    knots, ctrl = golden["robot_knots"], golden["robot_ctrl"]
+    job = S.SsppJob(None, knots, 2, ctrl, 0.0, np.ones(9), 128, max_batch=3)
+    out = job.alloc(3)
+    cands = np.stack([ctrl, ctrl * 0.5, ctrl[::-1]])
+    job.score_ctrl(torch.from_numpy(np.ascontiguousarray(cands)).cuda(), 0, out["arc"], out["feasible"], out["best"])
+    torch.cuda.synchronize()
+    arc = _np(out["arc"])
+    assert abs(arc[0] - golden["robot_arc"][0]) <= 1e-12
+    arc_o, _ = O.sspp_score(None, knots, 2, cands, 128)
+    assert np.array_equal(arc, arc_o)
+    assert _np(out["feasible"]).all()
+
+
 def stacking_problem(B, cp=128, seed=0x5EED, K=1):
     import sspp_amd as S
     model = S.Model(STACKING)

@@ -182,3 +182,13 @@ def test_sample_tsp_rules():
     assert (v[:, 3] < 0).any()  # wrapped around
     fixed = O.sample_tsp(mean, sig, np.array([-1, -1, 0, 0.3]), np.array([1, 1, 1, 0.3]), 0, 3, 0, 10)
     np.testing.assert_array_equal(fixed[:, 0, 3], 1.5)  # lo == hi: yaw = mean
+
+
+def test_robot_path_d9_p2_golden(golden):
+    """Degree-2, 9-D robot path of the reference's main_bspline.py pipeline: the oracle's spline
+    evaluation (A2.1/A2.2 basis) reproduces the reference bspline() points and arc length."""
+    knots, ctrl, u = golden["robot_knots"], golden["robot_ctrl"], golden["robot_u"]
+    pts = np.array([O.spline_eval(knots, 2, ctrl, x) for x in u])
+    assert np.abs(pts - golden["robot_pts"]).max() <= 1e-13
+    arc, _ = O.sspp_score(None, knots, 2, ctrl[None], 128)
+    assert abs(arc[0] - golden["robot_arc"][0]) <= 1e-12
