@@ -51,16 +51,24 @@ def parse():
     ap.add_argument("--roofline-launches", type=int, default=200)
     ap.add_argument("--streams", type=int, default=4,
                     help="independent batches in flight (one job + stream/graph branch each)")
-    ap.add_argument("--mode", default="native", choices=["native", "eager", "dropin"],
+    ap.add_argument("--mode", default="native", choices=["native", "eager", "dropin", "tsp-anytime"],
                     help="native: the C++ step executor enqueues --chunk steps per call "
                          "(robocrane); eager: one Python-level launch per step; dropin: "
                          "per-call latency of the reference's entry point "
-                         "_sspp.SamplingPathPlanner7.plan (src/sspp_bindings.cpp:43-50)")
+                         "_sspp.SamplingPathPlanner7.plan (src/sspp_bindings.cpp:43-50); "
+                         "tsp-anytime: the reference's ICRA anytime loop over "
+                         "_tsp.TaskSpacePlanner.plan (src/main_icra_benchmark.cpp:67-89)")
+    ap.add_argument("--sampler", default="fp64", choices=["fp64", "fp32"],
+                    help="robocrane sampleWithNoise normals: fp64 Box-Muller (default, bit-exact "
+                         "oracle) or the opt-in fp32 quad sampler")
+    ap.add_argument("--budgets-ms", default="10,20,50", help="tsp-anytime: wall-clock budgets")
     ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--steps-per-launch", type=int, default=32,
                     help="native mode: independent steps (each its own B candidates, outputs and "
                          "argmin) grouped into one kernel launch")
     a = ap.parse_args()
+    if a.steps is None and a.mode == "tsp-anytime":
+        a.steps = 10  # trials per budget and mode
     if a.steps is None:
         a.steps = {"robocrane": 8192, "stacking": 1024, "multigoal": 128}[a.config]
     if a.warmup is None:
@@ -78,8 +86,9 @@ def setup_robocrane(args, device):
     u = np.array([i / (n - 1) for i in range(n)])
     knots, ctrl0 = S.interpolate(np.array([(1 - t) * start + t * end for t in u]), 3, u)
     B = args.batch or 4096
-    jobs = [S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=S.DEFAULT_SEED, max_batch=B)
-            for _ in range(args.streams)]
+    sampler = S.SAMPLER_FP32 if args.sampler == "fp32" else S.SAMPLER_FP64
+    jobs = [S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=S.DEFAULT_SEED, max_batch=B,
+                      sampler=sampler) for _ in range(args.streams)]
     bufs = [j.alloc(B, device=device) for j in jobs]
     job = jobs[0]
 
@@ -115,7 +124,8 @@ def setup_robocrane(args, device):
     flops_per = (2 * W + 1) * 2 * (p + 1) * D + (W - 1) * (3 * D + 1) + \
         (W + 1) * (40 + 42 + 48 + 8 * 450 + 300)
     meta = dict(workload="robocrane SamplingPathPlanner7 (block_green free joint), sigma 0.08",
-                candidates_per_gpu=B, waypoints=W, init_points=n_, degree=p, dof=D)
+                candidates_per_gpu=B, waypoints=W, init_points=n_, degree=p, dof=D,
+                sampler=args.sampler)
     ctx = dict(kind="sspp", kernel_name="k_sspp_c2f" if os.environ.get("SSPP_KERNEL", "1") != "0" else "k_sspp",
                job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p,
                make_executor=make_executor,
@@ -232,7 +242,8 @@ def cpu_baseline(args, ctx, B, device):
             return O.sspp_score(osc, ctx["knots"], ctx["p"], c, ctx["W"], nthreads=threads)
 
         def sample(first, n):
-            return O.sample_sspp(ctx["ctrl0"], ctx["p"], 0.08, np.ones(7), S.DEFAULT_SEED, first, n)
+            return O.sample_sspp(ctx["ctrl0"], ctx["p"], 0.08, np.ones(7), S.DEFAULT_SEED, first, n,
+                                 sampler=O.SAMPLER_FP32 if args.sampler == "fp32" else O.SAMPLER_FP64)
     else:
         job = ctx["job"]
         osc = O.Scene(model, 1, ctx["body"])
@@ -471,15 +482,145 @@ def run_dropin(args):
         "isolated_step_kernel_us": float(np.median(ks)),
         "dtype": "f64", "data": "synthetic (on-device Philox candidates around a linear init spline)",
         "config": {"workload": "robocrane SamplingPathPlanner7.plan(start, end, 0.08, ones(7), %d, %d, %d)"
-                               % (B, W, n), "call": "_sspp (pybind11) -> sspp_planner_plan (C ABI)"},
+                               % (B, W, n), "call": "_sspp (pybind11) -> sspp_planner_plan (C ABI)",
+                   "sampler": "fp64"},
     }
     print(json.dumps(line))
+
+
+# src/main_icra_benchmark.cpp:151-179: the planner configuration and the start / end points of
+# the reference's ICRA anytime benchmark (robocrane model, 1 via, gripper as the moving body)
+ICRA = dict(stddev_initial=0.2, stddev_min=1e-4, stddev_max=0.5, stddev_increase_factor=1.5,
+            stddev_decay_factor=0.9, elite_fraction=0.3, sample_count=15, check_points=40,
+            gd_iterations=0, init_points=3, collision_weight=1.0, z_min=0.1,
+            limits_min=(0.0, -0.7, 0.1, -1.6), limits_max=(0.7, 0.7, 0.6, 1.6),
+            enable_gradient_descent=False, sigma_floor=0.005, var_ema_beta=0.2, mean_lr=0.5,
+            max_step_norm=0.1, floor_margin=0.01, floor_penalty_scale=10.0)
+ICRA_BODY = "gripper_collision_with_block/"
+
+
+def path_len_xyz(planner, n=50):
+    pts = np.array(planner.get_path_pts(n))[:, :3]
+    return float(np.linalg.norm(np.diff(pts, axis=0), axis=1).sum())
+
+
+def run_tsp_anytime(args):
+    """The reference's anytime benchmark (src/main_icra_benchmark.cpp:67-119, 199-221) on the
+    drop-in `_tsp.TaskSpacePlanner`: per budget, `steps` cold trials (a fresh planner each,
+    construction untimed) and `steps` warm trials (one planner), each trial = plan(q0, qT, False)
+    then plan(q0, qT, True) until the wall-clock budget is spent.  Reports the latency of one
+    plan(..., True) call (host call -> CES iteration on the device -> results back as Python
+    objects) and the iterations each budget holds; the oracle's CES iteration (oracle.ces_plan,
+    same sizes) is timed beside it as the CPU baseline."""
+    from sspp import _tsp
+    import sspp_amd as S
+    xml = os.path.join(S.SCENE_DIR, "robocrane.xml")
+    model = S.Model(xml)
+    q0 = model.body_point("block_green/") + np.array([0, 0, 0.02, 0])
+    qT = model.body_point("block_orange/") + np.array([0, 0, 0.02, 0])
+    budgets = [int(b) for b in args.budgets_ms.split(",") if b]
+    N = args.steps
+
+    def make():
+        return _tsp.TaskSpacePlanner(xml, ICRA_BODY, **ICRA)
+
+    iter_lat = []
+
+    def anytime(pl, budget_ms):
+        t0 = time.perf_counter()
+        deadline = t0 + budget_ms / 1e3
+        ok = len(pl.plan(q0, qT, False)) > 0
+        iters = 1
+        best = path_len_xyz(pl) if ok else float("inf")
+        while time.perf_counter() < deadline:
+            ta = time.perf_counter()
+            now_ok = len(pl.plan(q0, qT, True)) > 0
+            iter_lat.append(time.perf_counter() - ta)
+            iters += 1
+            if now_ok:
+                ok = True
+                best = min(best, path_len_xyz(pl))
+        return (time.perf_counter() - t0) * 1e3, ok, best if ok else 0.0, iters
+
+    for _ in range(max(1, args.warmup)):
+        anytime(make(), 5)
+    iter_lat.clear()
+    res = {}
+    for B in budgets:
+        row = {}
+        for mode in ("cold", "warm"):
+            runs = []
+            pl = make()
+            for _ in range(N):
+                if mode == "cold":
+                    pl = make()
+                runs.append(anytime(pl, B))
+            ms = np.array([r[0] for r in runs])
+            succ = [r for r in runs if r[1]]
+            row[mode] = {"succ": len(succ), "trials": N, "mean_ms": float(ms.mean()),
+                         "std_ms": float(ms.std()), "min_ms": float(ms.min()), "max_ms": float(ms.max()),
+                         "avg_iters": float(np.mean([r[3] for r in runs])),
+                         "avg_len_m": float(np.mean([r[2] for r in succ])) if succ else None}
+        res[str(B)] = row
+    lat_us = np.array(iter_lat) * 1e6
+    # plan(..., True) alone, back to back (no path-length bookkeeping between the calls)
+    pl = make()
+    pl.plan(q0, qT, False)
+    t0 = time.perf_counter()
+    for _ in range(200):
+        pl.plan(q0, qT, True)
+    tight_us = (time.perf_counter() - t0) / 200 * 1e6
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline_anytime(args, model, q0, qT)
+    line = {
+        "metric": "TaskSpacePlanner.plan(q0, qT, True) latency, ICRA anytime benchmark size",
+        "value": float(np.median(lat_us)), "unit": "us/iteration (median, inside the anytime loop)",
+        "n_gpus": 1, "steps": N, "warmup": args.warmup, "higher_is_better": False,
+        "latency_us": {"median": float(np.median(lat_us)), "p10": float(np.percentile(lat_us, 10)),
+                       "p90": float(np.percentile(lat_us, 90)), "back_to_back": tight_us},
+        "iterations_per_budget": {b: {m: r[m]["avg_iters"] for m in r} for b, r in res.items()},
+        "budgets": res, "dtype": "f64", "data": "robocrane.xml, block_green/ -> block_orange/ (+2 cm z)",
+        "config": {"workload": "ICRA anytime (src/main_icra_benchmark.cpp:151-179): 15 samples x 40 "
+                               "checks, 1 via, body %s" % ICRA_BODY,
+                   "call": "_tsp (pybind11) -> sspp_ces_plan + sspp_ces_read (C ABI)"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+
+
+def cpu_baseline_anytime(args, model, q0, qT):
+    """oracle.ces_plan (test infrastructure) at the ICRA size: seconds per CES iteration on the
+    host, single-threaded (the reference's scorer is OpenMP over 17 candidates)."""
+    from oracle import mjcf_ref
+    from oracle import oracle as O
+    osc = O.Scene(mjcf_ref.load(model.path), 1, model.body_id(ICRA_BODY))
+    cfg = dict(frac=ICRA["elite_fraction"], inc=ICRA["stddev_increase_factor"],
+               dec=ICRA["stddev_decay_factor"], sigma_floor=ICRA["sigma_floor"],
+               var_beta=ICRA["var_ema_beta"], mean_lr=ICRA["mean_lr"], sd_min=ICRA["stddev_min"],
+               sd_max=ICRA["stddev_max"], dist_z_min=ICRA["stddev_initial"],
+               lo=ICRA["limits_min"], hi=ICRA["limits_max"])
+    its = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < min(args.cpu_seconds, 5.0):
+        O.ces_plan(osc, q0, qT, 20, ICRA["sample_count"], ICRA["check_points"], z_min=ICRA["z_min"],
+                   nthreads=1, **cfg)
+        its += 20
+    dt = time.perf_counter() - t0
+    return dict(value=dt / its * 1e6, unit="us/iteration", cores=1, kind="port",
+                sample="%d CES iterations (20-iteration oracle.ces_plan runs) in %.1f s" % (its, dt),
+                iterations_per_budget={str(b): b * 1e3 / (dt / its * 1e6)
+                                       for b in [int(x) for x in args.budgets_ms.split(",") if x]},
+                **cpu_info())
 
 
 def main():
     args = parse()
     if args.mode == "dropin":
         run_dropin(args)
+        return
+    if args.mode == "tsp-anytime":
+        run_tsp_anytime(args)
         return
     import torch
     import torch.distributed as dist

@@ -321,7 +321,10 @@ int sspp_best_reduce_steps(const sspp_best* d_parts, int R, int G, sspp_best* d_
  * sspp_plan_sspp  <- SamplingPathPlanner::plan (include/sspp.h:194-225) in one call:
  *   initializePath (linear vias, degree 3, init_points) + sample_count candidates scored on the
  *   GPU.  Outputs: knots [init_points+4], ctrl [sample_count][init_points][dof] (nullable),
- *   feasible [sample_count], arc [sample_count], best.                                   */
+ *   feasible [sample_count], arc [sample_count], best.  Runs on a process-wide sspp_planner
+ *   cached per (scene, dof) — job, buffers and stream reused, async copies into pinned memory
+ *   and one stream synchronisation per call; calls are serialised by a mutex;
+ *   sspp_scene_free releases the scene's cached planners.                                */
 int sspp_plan_sspp(const sspp_scene* scene, int dof, const double* start, const double* end,
                    double sigma, const double* limits, int sample_count, int check_points,
                    int init_points, uint64_t seed, double* knots_out, double* ctrl_out,

@@ -190,10 +190,13 @@ __global__ __launch_bounds__(256) void k_ces_scatter(int nslots, const double* _
     rank[s] = 0;  // re-armed for the next update
 }
 
-// Distribution::update + best pick + adapt on the ranked elites, one workgroup.
+// Distribution::update + best pick + adapt on the ranked elites, one workgroup.  With
+// fused != 0 (n_slots <= kCesThreads: the ICRA-sized lists) the workgroup ranks the successes
+// itself, one slot per thread against every other slot in LDS, so an update is one launch
+// instead of rank + scatter + update.
 __global__ __launch_bounds__(kCesThreads) void k_ces_update(
-    CesK c, const double* __restrict__ cost, const int* __restrict__ by_rank,
-    int* nsucc_p, const double* __restrict__ vias,
+    CesK c, int fused, const unsigned char* __restrict__ status, const double* __restrict__ cost,
+    const int* __restrict__ by_rank, int* nsucc_p, const double* __restrict__ vias,
     const double* __restrict__ LT, const double* __restrict__ LH, CesHdr* h, double* mean,
     double* sigma, double* lbest, int* elite_out) {
     __shared__ double s_wt[kEliteCap];
@@ -203,7 +206,25 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
     const int tid = threadIdx.x;
     const int K = c.K, KD = 4 * K;
     for (int e = tid; e < 2 * KD; e += kCesThreads) s_ms[e] = e < KD ? mean[e] : sigma[e - KD];
-    const int nsucc = *nsucc_p;
+    int nsucc;
+    if (fused) {
+        unsigned long long* s_key = (unsigned long long*)s_wt;  // dead until the weights
+        const int ns = c.nslots;
+        const unsigned long long ks = (tid < ns && status[tid]) ? okey(cost[tid]) : kNoKey;
+        s_key[tid] = ks;
+        nsucc = __syncthreads_count(ks != kNoKey);
+        if (ks != kNoKey) {
+            int r = 0;
+            for (int q = 0; q < ns; ++q) {
+                const unsigned long long kj = s_key[q];
+                r += (kj < ks) || (kj == ks && q < tid);
+            }
+            s_idx[r] = tid;
+        }
+        __syncthreads();
+    } else {
+        nsucc = *nsucc_p;
+    }
     if (nsucc == 0) {  // adapt(false)
         if (tid < KD) sigma[tid] = clamp_sd(sigma[tid] * c.inc, c);
         if (tid == 0) { h->nsucc = 0; h->nelite = 0; h->best_slot = -1; h->best_cost = INFINITY; h->iter++; }
@@ -211,9 +232,11 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
     }
     int k = (int)((double)nsucc * c.frac) < 1 ? 1 : (int)((double)nsucc * c.frac);
     if (k > nsucc) k = nsucc;  // frac <= 1 is enforced at creation; never read past the ranks
-    for (int j = tid; j < k; j += kCesThreads) s_idx[j] = by_rank[j];
-    __syncthreads();
-    if (tid == 0) *nsucc_p = 0;  // re-armed for the next update (every thread has read it)
+    if (!fused) {
+        for (int j = tid; j < k; j += kCesThreads) s_idx[j] = by_rank[j];
+        __syncthreads();
+        if (tid == 0) *nsucc_p = 0;  // re-armed for the next update (every thread has read it)
+    }
 
     // ---- CES log weights (tsp_elites.h:24-32): w_j = log(k + 0.5) - log(j + 1), normalised.
     // Every sum below is the canonical 512-lane order of or_canon_sum(x, n, 512): thread t
@@ -339,6 +362,50 @@ __global__ __launch_bounds__(256) void k_ces_unpack(int n, int KD, const double*
     }
 }
 
+// sspp_ces_read's staging: header, per-slot results, distribution and elites written straight
+// into the planner's pinned host buffer (one launch, then one stream synchronisation)
+constexpr size_t kStageHdr = 64;
+__global__ __launch_bounds__(256) void k_ces_stage(int n, int KD, int cap, const CesHdr* __restrict__ h,
+                                                   const double* L, const double* Cnf, const double* Cwf,
+                                                   const double* cost, const double* vias, const double* mean,
+                                                   const double* sigma, const double* lbest,
+                                                   const int* __restrict__ elite,
+                                                   const unsigned char* __restrict__ st,
+                                                   unsigned char* out) {
+    const long long nv = (long long)n * KD, nd = 4LL * n + nv + 3LL * KD;
+    double* od = (double*)(out + kStageHdr);
+    int* oi = (int*)(od + nd);
+    unsigned char* ob = (unsigned char*)(oi + cap);
+    const int nel = h->nelite;
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
+    if (gid < (long long)(sizeof(CesHdr) / 8))
+        ((long long*)out)[gid] = ((const long long*)h)[gid];
+    for (long long e = gid; e < nd + cap + n; e += stride) {
+        if (e < nd) {
+            const double* src;
+            long long i = e;
+            if (i < 4LL * n) {
+                const int f = (int)(i / n);
+                src = f == 0 ? L : f == 1 ? Cnf : f == 2 ? Cwf : cost;
+                i -= (long long)f * n;
+            } else if ((i -= 4LL * n) < nv) {
+                src = vias;
+            } else {
+                i -= nv;
+                const int f = (int)(i / KD);
+                src = f == 0 ? mean : f == 1 ? sigma : lbest;
+                i -= (long long)f * KD;
+            }
+            od[e] = src[i];
+        } else if (e < nd + cap) {
+            const int j = (int)(e - nd);
+            if (j < nel) oi[j] = elite[j];
+        } else {
+            ob[e - nd - cap] = st[e - nd - cap];
+        }
+    }
+}
+
 int hip_err(hipError_t e, const char* what) {
     return sspp::set_error(SSPP_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -361,6 +428,9 @@ struct sspp_ces {
     int* d_by_rank = nullptr;  // [n_slots] slot of rank r
     int* d_nsucc = nullptr;
     double *d_LT = nullptr, *d_LH = nullptr;
+    hipStream_t last = nullptr;         // stream of the last enqueued operation (sspp_ces_read waits on it)
+    unsigned char* h_stage = nullptr;   // pinned: k_ces_stage's output
+    size_t stage_bytes = 0;
 };
 
 static CesK ces_k(const sspp_ces* p) {
@@ -385,6 +455,7 @@ void sspp_ces_free(sspp_ces* p) {
                     (void*)p->d_LT, (void*)p->d_LH, (void*)p->d_rank, (void*)p->d_by_rank,
                     (void*)p->d_nsucc})
         if (q) (void)hipFree(q);
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
     delete p;
 }
 
@@ -454,7 +525,9 @@ int sspp_ces_create(const sspp_scene* scene, const sspp_ces_config* cfg, int wor
         (e = hipMemset(p->d_status, 0, ns)) != hipSuccess ||
         (e = hipMemset(p->d_rank, 0, sizeof(int) * ns)) != hipSuccess ||
         (e = hipMemset(p->d_by_rank, 0, sizeof(int) * ns)) != hipSuccess ||
-        (e = hipMemset(p->d_nsucc, 0, sizeof(int))) != hipSuccess) {
+        (e = hipMemset(p->d_nsucc, 0, sizeof(int))) != hipSuccess ||
+        (p->stage_bytes = kStageHdr + sizeof(double) * (4 * ns + ns * kd + 3 * kd) + sizeof(int) * (size_t)cap + ns,
+         (e = hipHostMalloc((void**)&p->h_stage, p->stage_bytes, hipHostMallocDefault)) != hipSuccess)) {
         rc = hip_err(e, "sspp_ces_create allocation");
         sspp_ces_free(p);
         return rc;
@@ -499,6 +572,7 @@ int sspp_ces_begin(sspp_ces* p, const double* start, const double* end, int iter
         s = s < p->cfg.sigma_floor ? p->cfg.sigma_floor : s;
         r.sigma0 = s;
     }
+    p->last = (hipStream_t)stream;
     hipLaunchKernelGGL(k_ces_begin, dim3(1), dim3(128), 0, (hipStream_t)stream, ces_k(p), iterate ? 1 : 0,
                        r, p->d_hdr, p->d_mean, p->d_sigma, p->d_lbest, p->d_fixed);
     hipError_t e = hipGetLastError();
@@ -517,6 +591,7 @@ int sspp_ces_eval(sspp_ces* p, int rank, void* stream) {
     ev.first_id = p->iter * (long long)p->cfg.samples;
     for (int i = 0; i < 4; ++i) { ev.start[i] = p->start[i]; ev.end[i] = p->end[i]; }
     const size_t o = (size_t)rank * p->spr;
+    p->last = (hipStream_t)stream;
     return sspp::tsp_eval_ces(p->job, &ev, p->spr, p->d_L + o, p->d_Cnf + o, p->d_Cwf + o,
                               p->d_status + o, p->d_cost + o, p->d_vias + o * 4 * p->K, stream);
 }
@@ -526,12 +601,16 @@ int sspp_ces_update(sspp_ces* p, void* stream) {
     if (!p) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_update: null planner");
     const int nt = (p->nslots + kRankTile - 1) / kRankTile;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_ces_rank, dim3(nt, nt), dim3(kRankTile), 0, st, p->nslots, p->d_cost,
-                       p->d_status, p->d_rank, p->d_nsucc);
-    hipLaunchKernelGGL(k_ces_scatter, dim3(nt), dim3(256), 0, st, p->nslots, p->d_cost, p->d_status,
-                       p->d_rank, p->d_by_rank);
-    hipLaunchKernelGGL(k_ces_update, dim3(1), dim3(kCesThreads), 0, st, ces_k(p), p->d_cost,
-                       p->d_by_rank, p->d_nsucc, p->d_vias, p->d_LT, p->d_LH, p->d_hdr, p->d_mean,
+    p->last = st;
+    const int fused = p->nslots <= kCesThreads && !std::getenv("SSPP_CES_UNFUSED");
+    if (!fused) {
+        hipLaunchKernelGGL(k_ces_rank, dim3(nt, nt), dim3(kRankTile), 0, st, p->nslots, p->d_cost,
+                           p->d_status, p->d_rank, p->d_nsucc);
+        hipLaunchKernelGGL(k_ces_scatter, dim3(nt), dim3(256), 0, st, p->nslots, p->d_cost, p->d_status,
+                           p->d_rank, p->d_by_rank);
+    }
+    hipLaunchKernelGGL(k_ces_update, dim3(1), dim3(kCesThreads), 0, st, ces_k(p), fused, p->d_status,
+                       p->d_cost, p->d_by_rank, p->d_nsucc, p->d_vias, p->d_LT, p->d_LH, p->d_hdr, p->d_mean,
                        p->d_sigma, p->d_lbest, p->d_elite);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "k_ces_update launch");
@@ -571,6 +650,7 @@ int sspp_ces_unpack(sspp_ces* p, const double* d_in, void* stream) {
     const int KD = 4 * p->K;
     const long long tot = (long long)p->nslots * (5 + KD);
     const int g = (int)std::min<long long>((tot + 255) / 256, 1024);
+    p->last = (hipStream_t)stream;
     hipLaunchKernelGGL(k_ces_unpack, dim3(g), dim3(256), 0, (hipStream_t)stream, p->nslots, KD, d_in,
                        p->d_L, p->d_Cnf, p->d_Cwf, p->d_cost, p->d_status, p->d_vias);
     hipError_t e = hipGetLastError();
@@ -591,10 +671,18 @@ int sspp_ces_read(sspp_ces* p, sspp_ces_state* st, double* L, double* Cnf, doubl
                   int32_t* elites) {
     sspp::clear_error();
     if (!p || !st) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_read: null argument");
-    hipError_t e = hipDeviceSynchronize();
-    if (e != hipSuccess) return hip_err(e, "sspp_ces_read synchronize");
+    // one staging launch behind the planner's last operation, one wait on that stream
+    const int n = p->nslots, KD = 4 * p->K;
+    const long long tot = 4LL * n + (long long)n * KD + 3LL * KD + p->cap + n;
+    const int g = (int)std::min<long long>((tot + 255) / 256, 256);
+    hipLaunchKernelGGL(k_ces_stage, dim3(g), dim3(256), 0, p->last, n, KD, p->cap, p->d_hdr, p->d_L,
+                       p->d_Cnf, p->d_Cwf, p->d_cost, p->d_vias, p->d_mean, p->d_sigma, p->d_lbest,
+                       p->d_elite, p->d_status, p->h_stage);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(p->last);
+    if (e != hipSuccess) return hip_err(e, "sspp_ces_read");
     CesHdr h;
-    if ((e = hipMemcpy(&h, p->d_hdr, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess) return hip_err(e, "read header");
+    std::memcpy(&h, p->h_stage, sizeof h);
     st->n_fixed = h.nfixed;
     st->n_candidates = h.nfixed + p->cfg.samples;
     st->n_success = h.nsucc;
@@ -603,15 +691,18 @@ int sspp_ces_read(sspp_ces* p, sspp_ces_state* st, double* L, double* Cnf, doubl
     st->best_slot = h.best_slot;
     st->best_cost = h.best_cost;
     st->iteration = p->iter;
-    const size_t n = (size_t)st->n_candidates, kd = (size_t)4 * p->K;
+    const size_t m = (size_t)st->n_candidates, kd = (size_t)KD;
+    const double* sd = (const double*)(p->h_stage + kStageHdr);
+    const size_t ov = 4 * (size_t)n, om = ov + (size_t)n * kd, oe = om + 3 * kd;
+    const int32_t* si = (const int32_t*)(sd + oe);
+    const uint8_t* sb = (const uint8_t*)(si + p->cap);
     struct { void* dst; const void* src; size_t bytes; } cp[] = {
-        {L, p->d_L, 8 * n}, {Cnf, p->d_Cnf, 8 * n}, {Cwf, p->d_Cwf, 8 * n}, {cost, p->d_cost, 8 * n},
-        {status, p->d_status, n}, {vias, p->d_vias, 8 * n * kd}, {mean, p->d_mean, 8 * kd},
-        {sigma, p->d_sigma, 8 * kd}, {last_best, p->d_lbest, 8 * kd},
-        {elites, p->d_elite, sizeof(int32_t) * (size_t)(h.nelite > 0 ? h.nelite : 0)}};
+        {L, sd, 8 * m}, {Cnf, sd + n, 8 * m}, {Cwf, sd + 2 * (size_t)n, 8 * m}, {cost, sd + 3 * (size_t)n, 8 * m},
+        {status, sb, m}, {vias, sd + ov, 8 * m * kd}, {mean, sd + om, 8 * kd},
+        {sigma, sd + om + kd, 8 * kd}, {last_best, sd + om + 2 * kd, 8 * kd},
+        {elites, si, sizeof(int32_t) * (size_t)(h.nelite > 0 ? h.nelite : 0)}};
     for (auto& c : cp)
-        if (c.dst && c.bytes && (e = hipMemcpy(c.dst, c.src, c.bytes, hipMemcpyDeviceToHost)) != hipSuccess)
-            return hip_err(e, "sspp_ces_read copy");
+        if (c.dst && c.bytes) std::memcpy(c.dst, c.src, c.bytes);
     return SSPP_OK;
 }
 

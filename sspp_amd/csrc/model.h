@@ -33,8 +33,10 @@ int span_of(double u, int p, const double* knots, int nknots);
 void basis_funcs(double u, int p, const double* knots, int nknots, double* N);
 int interpolate(const double* pts, int n, int D, int p, const double* u, double* knots,
                 double* ctrl);
-// collocation inverse for fixed parameters u (PathModel::fromVias precompute)
-int collocation_inverse(const double* u, int n, int p, double* knots, double* Minv);
+// Householder QR "program" of the collocation matrix for fixed parameters u (PathModel::fromVias
+// precompute): [n][n] reflectors | [n] |v|^2 | [n][n] R; qr_apply replays it on B [n][D]
+int qr_program(const double* u, int n, int p, double* knots, double* prog);
+void qr_apply(const double* prog, int n, double* B, int D);
 
 // CES slot-mode evaluation of a TaskSpacePlanner job (sspp_kernels.hip; used by ces.hip)
 struct TspCesEval {
@@ -50,4 +52,6 @@ struct TspCesEval {
 int tsp_eval_ces(sspp_job* j, const TspCesEval* e, int64_t n, double* d_L, double* d_Cnf,
                  double* d_Cwf, uint8_t* d_status, double* d_cost, double* d_vias_out,
                  void* stream);
+// sspp_plan_sspp's cached planners (planner.hip): dropped when their scene is freed
+void planner_cache_drop(const sspp_scene* scene);
 }  // namespace sspp

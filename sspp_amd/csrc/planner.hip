@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -176,14 +177,12 @@ extern "C" int sspp_planner_create(const sspp_scene* scene, int dof, sspp_planne
 
 extern "C" void sspp_planner_free(sspp_planner* p) { delete p; }
 
-extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const double* end, double sigma,
-                                 const double* limits, int sample_count, int check_points,
-                                 int init_points, uint64_t seed, int64_t first_id, double* knots_out,
-                                 int64_t* n_feasible, int64_t* feasible_ids, double* feasible_arc,
-                                 double* feasible_ctrl, sspp_best* best_out) {
-    sspp::clear_error();
-    if (!p || !start || !end || !limits || !knots_out || !n_feasible || !best_out)
-        return sspp::set_error(SSPP_E_INVAL, "sspp_planner_plan: null argument");
+// plan()'s common front: initializePath on the host, then the job of this shape created (first
+// call / new shape / larger batch) or re-targeted asynchronously, then one scoring launch on the
+// planner's stream.  ctrl_dev: the sampled control points are written to d_ctrl.
+static int plan_enqueue(sspp_planner* p, const double* start, const double* end, double sigma,
+                        const double* limits, int sample_count, int check_points, int init_points,
+                        uint64_t seed, int64_t first_id, double* knots_out, bool ctrl_dev) {
     const int n = init_points, D = p->D, deg = 3;
     if (sample_count < 1) return sspp::set_error(SSPP_E_INVAL, "sample_count must be >= 1");
     if (n < deg + 1) return sspp::set_error(SSPP_E_INVAL, "init_points must be >= 4 for a cubic spline");
@@ -216,9 +215,24 @@ extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const dou
     } else if ((rc = sspp_job_update_sspp(p->plan_job.j, ctrl0.data(), sigma, limits, seed, p->stream))) {
         return rc;
     }
-    if ((rc = sspp_job_sample_score(p->plan_job.j, first_id, B, p->d_arc.p, p->d_feas.p, p->d_ctrl.p,
-                                    p->d_best.p, p->stream)))
+    return sspp_job_sample_score(p->plan_job.j, first_id, B, p->d_arc.p, p->d_feas.p,
+                                 ctrl_dev ? p->d_ctrl.p : nullptr, p->d_best.p, p->stream);
+}
+
+extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const double* end, double sigma,
+                                 const double* limits, int sample_count, int check_points,
+                                 int init_points, uint64_t seed, int64_t first_id, double* knots_out,
+                                 int64_t* n_feasible, int64_t* feasible_ids, double* feasible_arc,
+                                 double* feasible_ctrl, sspp_best* best_out) {
+    sspp::clear_error();
+    if (!p || !start || !end || !limits || !knots_out || !n_feasible || !best_out)
+        return sspp::set_error(SSPP_E_INVAL, "sspp_planner_plan: null argument");
+    int rc;
+    if ((rc = plan_enqueue(p, start, end, sigma, limits, sample_count, check_points, init_points, seed,
+                           first_id, knots_out, true)))
         return rc;
+    const size_t nd = (size_t)init_points * p->D;
+    const int64_t B = sample_count;
     CompactHdr* hh = p->h_hdr.dev();
     long long* hi = p->h_ids.dev();
     double* ha = p->h_arc.dev();
@@ -234,6 +248,73 @@ extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const dou
     if (feasible_ids) std::memcpy(feasible_ids, p->h_ids.p, sizeof(long long) * cnt);
     if (feasible_arc) std::memcpy(feasible_arc, p->h_arc.p, sizeof(double) * cnt);
     if (feasible_ctrl) std::memcpy(feasible_ctrl, p->h_ctrl.p, sizeof(double) * cnt * nd);
+    return SSPP_OK;
+}
+
+// ---- sspp_plan_sspp: the blocking all-candidates form of plan() on a cached planner per
+// (scene, dof).  The cache lives for the process; sspp_scene_free drops a scene's planners.
+namespace {
+struct PlannerCache {
+    std::mutex mu;  // one plan at a time through the cache (a planner is not re-entrant)
+    struct Entry { const sspp_scene* scene; int D; sspp_planner* p; };
+    std::vector<Entry> entries;
+};
+PlannerCache& planner_cache() {
+    static PlannerCache* c = new PlannerCache();  // never destroyed: no teardown-order hazards
+    return *c;
+}
+}  // namespace
+
+void sspp::planner_cache_drop(const sspp_scene* scene) {
+    PlannerCache& c = planner_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    for (size_t i = 0; i < c.entries.size();) {
+        if (c.entries[i].scene == scene) {
+            sspp_planner_free(c.entries[i].p);
+            c.entries.erase(c.entries.begin() + i);
+        } else {
+            ++i;
+        }
+    }
+}
+
+extern "C" int sspp_plan_sspp(const sspp_scene* scene, int dof, const double* start,
+                              const double* end, double sigma, const double* limits,
+                              int sample_count, int check_points, int init_points, uint64_t seed,
+                              double* knots_out, double* ctrl_out, uint8_t* feasible_out,
+                              double* arc_out, sspp_best* best_out) {
+    sspp::clear_error();
+    if (!start || !end || !limits || !knots_out || !feasible_out || !arc_out || !best_out)
+        return sspp::set_error(SSPP_E_INVAL, "sspp_plan_sspp: null argument");
+    PlannerCache& c = planner_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    sspp_planner* p = nullptr;
+    for (auto& e : c.entries)
+        if (e.scene == scene && e.D == dof) p = e.p;
+    int rc;
+    if (!p) {
+        if ((rc = sspp_planner_create(scene, dof, &p))) return rc;
+        c.entries.push_back({scene, dof, p});
+    }
+    if ((rc = plan_enqueue(p, start, end, sigma, limits, sample_count, check_points, init_points, seed, 0,
+                           knots_out, ctrl_out != nullptr)))
+        return rc;
+    // every candidate's outputs through the pinned staging (async copies, one stream sync)
+    const int64_t B = sample_count;
+    const size_t nd = (size_t)init_points * dof;
+    if ((rc = p->h_sarc.reserve(B)) || (rc = p->h_sfeas.reserve(B)) || (rc = p->h_sbest.reserve(1)))
+        return rc;
+    if ((rc = hipck(hipMemcpyAsync(p->h_sarc.p, p->d_arc.p, sizeof(double) * B, hipMemcpyDeviceToHost, p->stream), "copy arc")) ||
+        (rc = hipck(hipMemcpyAsync(p->h_sfeas.p, p->d_feas.p, (size_t)B, hipMemcpyDeviceToHost, p->stream), "copy feasible")) ||
+        (rc = hipck(hipMemcpyAsync(p->h_sbest.p, p->d_best.p, sizeof(sspp_best), hipMemcpyDeviceToHost, p->stream), "copy best")) ||
+        (ctrl_out && (rc = hipck(hipMemcpyAsync(p->h_ctrl.p, p->d_ctrl.p, sizeof(double) * B * nd,
+                                                hipMemcpyDeviceToHost, p->stream), "copy ctrl"))) ||
+        (rc = hipck(hipStreamSynchronize(p->stream), "plan")))
+        return rc;
+    std::memcpy(arc_out, p->h_sarc.p, sizeof(double) * B);
+    std::memcpy(feasible_out, p->h_sfeas.p, (size_t)B);
+    *best_out = *p->h_sbest.p;
+    if (ctrl_out) std::memcpy(ctrl_out, p->h_ctrl.p, sizeof(double) * B * nd);
     return SSPP_OK;
 }
 

@@ -3,8 +3,11 @@
 // Reference call sites: include/sspp.h:95 (SplineFitting::Interpolate, degree 3, parameters
 // u_i = i/(n-1)), include/sspp/tsp_path_model.h:25-28,38-42 (degree 2).  The knot vector is
 // Eigen's KnotAveraging; rows of the collocation matrix are Piegl & Tiller A2.2 basis values at
-// the parameters with A(0,0) = A(n-1,n-1) = 1; the system is solved by LU with partial
-// pivoting (Eigen uses HouseholderQR: same solution up to rounding).
+// the parameters with A(0,0) = A(n-1,n-1) = 1; the system is solved by Householder QR as Eigen's
+// SplineFitting::Interpolate does (HouseholderQR), in exactly the operation order of
+// oracle/sspp_oracle.c::qr_solve.  The factorisation depends only on the parameters, so it is
+// kept as a "QR program" (reflectors + R) that the TaskSpacePlanner kernel replays per
+// candidate: device and oracle control points agree bit for bit.
 #include <cmath>
 #include <vector>
 
@@ -67,55 +70,82 @@ static void collocation(const double* u, int n, int p, const double* knots, std:
     A[(size_t)(n - 1) * n + n - 1] = 1.0;
 }
 
-// Solve A X = B in place (A n x n, B n x m), partial pivoting.
-static int lu_solve(std::vector<double>& A, double* B, int n, int m) {
+// Householder QR of A (oracle qr_solve, A part): prog = [n][n] reflectors v_k (row k, entries
+// k..n-1) | [n] |v_k|^2 (0 = no reflection at step k) | [n][n] R.
+static int qr_factor(std::vector<double>& A, int n, double* prog) {
+    double* V = prog;
+    double* vn_out = prog + (size_t)n * n;
+    double* R = vn_out + n;
+    std::vector<double> v((size_t)n);
+    for (size_t e = 0; e < (size_t)n * n; ++e) V[e] = 0.0;
     for (int k = 0; k < n; ++k) {
-        int piv = k;
-        double best = std::fabs(A[(size_t)k * n + k]);
-        for (int i = k + 1; i < n; ++i) {
-            double v = std::fabs(A[(size_t)i * n + k]);
-            if (v > best) { best = v; piv = i; }
+        vn_out[k] = 0.0;
+        double norm = 0.0;
+        for (int i = k; i < n; ++i) norm = std::fma(A[(size_t)i * n + k], A[(size_t)i * n + k], norm);
+        norm = std::sqrt(norm);
+        if (norm == 0.0) continue;
+        const double alpha = A[(size_t)k * n + k] > 0 ? -norm : norm;
+        for (int i = k; i < n; ++i) v[i] = A[(size_t)i * n + k];
+        v[k] -= alpha;
+        double vn = 0.0;
+        for (int i = k; i < n; ++i) vn = std::fma(v[i], v[i], vn);
+        if (vn == 0.0) continue;
+        for (int j = k; j < n; ++j) {
+            double s = 0.0;
+            for (int i = k; i < n; ++i) s = std::fma(v[i], A[(size_t)i * n + j], s);
+            s = 2.0 * s / vn;
+            for (int i = k; i < n; ++i) A[(size_t)i * n + j] -= s * v[i];
         }
-        if (best == 0.0) return -1;
-        if (piv != k) {
-            for (int j = 0; j < n; ++j) std::swap(A[(size_t)k * n + j], A[(size_t)piv * n + j]);
-            for (int j = 0; j < m; ++j) std::swap(B[(size_t)k * m + j], B[(size_t)piv * m + j]);
-        }
-        for (int i = k + 1; i < n; ++i) {
-            double f = A[(size_t)i * n + k] / A[(size_t)k * n + k];
-            if (f == 0.0) continue;
-            for (int j = k; j < n; ++j) A[(size_t)i * n + j] -= f * A[(size_t)k * n + j];
-            for (int j = 0; j < m; ++j) B[(size_t)i * m + j] -= f * B[(size_t)k * m + j];
-        }
+        vn_out[k] = vn;
+        for (int i = k; i < n; ++i) V[(size_t)k * n + i] = v[i];
     }
-    for (int j = 0; j < m; ++j) {
-        for (int i = n - 1; i >= 0; --i) {
-            double s = B[(size_t)i * m + j];
-            for (int c = i + 1; c < n; ++c) s -= A[(size_t)i * n + c] * B[(size_t)c * m + j];
-            B[(size_t)i * m + j] = s / A[(size_t)i * n + i];
-        }
-    }
+    for (size_t e = 0; e < (size_t)n * n; ++e) R[e] = A[e];
+    for (int i = 0; i < n; ++i)
+        if (R[(size_t)i * n + i] == 0.0) return -2;
     return 0;
+}
+
+void qr_apply(const double* prog, int n, double* B, int D) {
+    const double* V = prog;
+    const double* vn = prog + (size_t)n * n;
+    const double* R = vn + n;
+    for (int k = 0; k < n; ++k) {
+        if (vn[k] == 0.0) continue;
+        const double* v = V + (size_t)k * n;
+        for (int j = 0; j < D; ++j) {
+            double s = 0.0;
+            for (int i = k; i < n; ++i) s = std::fma(v[i], B[(size_t)i * D + j], s);
+            s = 2.0 * s / vn[k];
+            for (int i = k; i < n; ++i) B[(size_t)i * D + j] -= s * v[i];
+        }
+    }
+    for (int j = 0; j < D; ++j) {
+        for (int i = n - 1; i >= 0; --i) {
+            double s = B[(size_t)i * D + j];
+            for (int c = i + 1; c < n; ++c) s -= R[(size_t)i * n + c] * B[(size_t)c * D + j];
+            B[(size_t)i * D + j] = s / R[(size_t)i * n + i];
+        }
+    }
 }
 
 int interpolate(const double* pts, int n, int D, int p, const double* u, double* knots,
                 double* ctrl) {
     if (n < p + 1 || p < 1 || p > 15 || D < 1) return -1;
     knot_averaging(u, n, p, knots);
-    std::vector<double> A;
+    std::vector<double> A, prog((size_t)2 * n * n + n);
     collocation(u, n, p, knots, A);
+    if (qr_factor(A, n, prog.data()) != 0) return -1;
     for (size_t k = 0; k < (size_t)n * D; ++k) ctrl[k] = pts[k];
-    return lu_solve(A, ctrl, n, D);
+    qr_apply(prog.data(), n, ctrl, D);
+    return 0;
 }
 
-int collocation_inverse(const double* u, int n, int p, double* knots, double* Minv) {
+int qr_program(const double* u, int n, int p, double* knots, double* prog) {
     if (n < p + 1 || p < 1 || p > 15) return -1;
     knot_averaging(u, n, p, knots);
     std::vector<double> A;
     collocation(u, n, p, knots, A);
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) Minv[(size_t)i * n + j] = (i == j) ? 1.0 : 0.0;
-    return lu_solve(A, Minv, n, n);
+    return qr_factor(A, n, prog);
 }
 
 }  // namespace sspp

@@ -1,8 +1,8 @@
 // sspp_hostapi.cpp — host-synchronous conveniences over the job API (host buffers in/out).
 //
-// These back the pybind11 drop-in (`from sspp import _sspp`): the reference's plan() is a
-// blocking call on host data (include/sspp.h:194-225, bound at src/sspp_bindings.cpp:43-50).
-// The candidate work still runs entirely in the HIP kernels; this file only stages buffers.
+// One-shot scoring / sampling of host splines (tests and the oracle comparisons); the blocking
+// plan() form, sspp_plan_sspp, lives in planner.hip on a cached sspp_planner.  The candidate
+// work still runs entirely in the HIP kernels; this file only stages buffers.
 #include <hip/hip_runtime_api.h>
 
 #include <cmath>
@@ -78,30 +78,6 @@ int run_job_host(const sspp_scene* scene, const double* knots, int degree, const
 }
 
 }  // namespace
-
-extern "C" int sspp_plan_sspp(const sspp_scene* scene, int dof, const double* start,
-                              const double* end, double sigma, const double* limits,
-                              int sample_count, int check_points, int init_points, uint64_t seed,
-                              double* knots_out, double* ctrl_out, uint8_t* feasible_out,
-                              double* arc_out, sspp_best* best_out) {
-    sspp::clear_error();
-    if (!start || !end || !limits || !knots_out || !feasible_out || !arc_out || !best_out)
-        return sspp::set_error(SSPP_E_INVAL, "sspp_plan_sspp: null argument");
-    if (sample_count < 1) return sspp::set_error(SSPP_E_INVAL, "sample_count must be >= 1");
-    const int n = init_points, p = 3;
-    if (n < p + 1) return sspp::set_error(SSPP_E_INVAL, "init_points must be >= 4 for a cubic spline");
-    // initializePath (include/sspp.h:82-97): linear via points at t_i = i/(n-1)
-    std::vector<double> u((size_t)n), pts((size_t)n * dof), ctrl0((size_t)n * dof);
-    for (int i = 0; i < n; ++i) {
-        double t = (double)i / (n - 1);
-        u[i] = t;
-        for (int d = 0; d < dof; ++d) pts[(size_t)i * dof + d] = (1 - t) * start[d] + t * end[d];
-    }
-    if (sspp::interpolate(pts.data(), n, dof, p, u.data(), knots_out, ctrl0.data()) != 0)
-        return sspp::set_error(SSPP_E_INVAL, "initializePath: interpolation failed");
-    return run_job_host(scene, knots_out, p, ctrl0.data(), n, dof, sigma, limits, check_points,
-                        seed, 0, sample_count, nullptr, ctrl_out, arc_out, feasible_out, best_out);
-}
 
 extern "C" int sspp_score_ctrl_host(const sspp_scene* scene, const double* knots, int degree,
                                     const double* ctrl, int64_t B, int n, int D, int W,

@@ -2016,7 +2016,8 @@ __global__ __launch_bounds__(64, SSPP_WQ2_WAVES_PER_EU) void k_sspp_wq2(
 }
 
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
-// tab: (cp+1) rows of 3 basis values at u = i * (1/cp); Minv: collocation inverse (n x n).
+// tab: (cp+1) rows of 3 basis values at u = i * (1/cp); Minv: the collocation matrix's QR
+// program (spline_host.cpp qr_program: [n][n] reflectors | [n] |v|^2 | [n][n] R).
 #ifndef SSPP_TSP_WAVES_PER_EU
 #define SSPP_TSP_WAVES_PER_EU 3
 #endif
@@ -2116,13 +2117,30 @@ __global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WA
             vias_out[(cand0 + s) * K * D + r] = s_V[s * ndof + D + r];
         }
     }
-    // PathModel::fromVias: ctrl = A^-1 V (collocation inverse precomputed on the host)
-    for (int e = tid; e < cpb * ndof; e += kBlock) {
-        const int s = e / ndof, r = e - s * ndof, j = r / D, d = r - j * D;
+    // PathModel::fromVias: SplineFitting::Interpolate's Householder QR solve, replayed from the
+    // host-factored program (reflectors, |v|^2, R) in oracle qr_solve's operation order, one
+    // lane per (candidate, dimension): control points bit-identical to the oracle's
+    for (int e = tid; e < cpb * D; e += kBlock) {
+        const int s = e / D, d = e - s * D;
         const double* Vs = s_V + s * ndof;
-        double acc = Minv[j * n] * Vs[d];
-        for (int i = 1; i < n; ++i) acc = fma(Minv[j * n + i], Vs[i * D + d], acc);
-        s_ctrl[e] = acc;
+        double* c = s_ctrl + s * ndof;
+        for (int i = 0; i < n; ++i) c[i * D + d] = Vs[i * D + d];
+        const double* vn = Minv + n * n;
+        const double* R = vn + n;
+        for (int k = 0; k < n; ++k) {
+            const double q = vn[k];
+            if (q == 0.0) continue;
+            const double* v = Minv + k * n;
+            double sd = 0.0;
+            for (int i = k; i < n; ++i) sd = fma(v[i], c[i * D + d], sd);
+            sd = 2.0 * sd / q;
+            for (int i = k; i < n; ++i) c[i * D + d] = c[i * D + d] - sd * v[i];
+        }
+        for (int i = n - 1; i >= 0; --i) {
+            double t = c[i * D + d];
+            for (int cc = i + 1; cc < n; ++cc) t = t - R[i * n + cc] * c[cc * D + d];
+            c[i * D + d] = t / R[i * n + i];
+        }
     }
     __syncthreads();
 
@@ -2274,9 +2292,13 @@ struct sspp_job {
     WqEnt* d_wlist = nullptr;      // feasible lists [wq_cap]
     int64_t wq_cap = 0;            // candidates per launch the buffers hold
     int wq_occ = 0, wq_occ_lds = -1;  // resident k_sspp_wq2 workgroups (all CUs) at that LDS size
-    std::vector<double> h_knots;   // host copies: the knot vector, and the staging of
-    std::vector<double> h_stage;   // sspp_job_update_sspp's asynchronous uploads (init | limits)
+    std::vector<double> h_knots;   // host copies: the knot vector, and the values the device
+    std::vector<double> h_stage;   // holds (init | limits; sspp_job_update_sspp skips equal updates)
     std::vector<DPair> h_pairs, h_pairs_s;
+    unsigned char* h_pin = nullptr;  // pinned source of sspp_job_update_sspp's async copies
+    size_t h_pin_bytes = 0;
+    hipEvent_t upd_ev = nullptr;     // recorded after those copies: the next update waits on it
+    bool upd_pending = false;
     double start[4], end[4], lo[4], hi[4];
     double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
 };

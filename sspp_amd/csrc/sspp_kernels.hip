@@ -342,6 +342,7 @@ int sspp_scene_get_info(const sspp_scene* s, sspp_scene_info* out) {
 
 void sspp_scene_free(sspp_scene* s) {
     if (!s) return;
+    sspp::planner_cache_drop(s);
     if (s->d_geoms) (void)hipFree(s->d_geoms);
     if (s->d_pairs) (void)hipFree(s->d_pairs);
     if (s->d_movers) (void)hipFree(s->d_movers);
@@ -470,7 +471,8 @@ static void table_flags(const sspp_scene* sc, const std::vector<DPair>& t, int* 
 // (re)build the job's two pair tables for its current initial spline / sigma / limits: the full
 // table ordered for the mean path (pairs_for_job) and its sample-mode subset (reachable_pairs);
 // stream == nullptr: synchronous upload into fresh buffers, else asynchronous into the existing ones
-static int set_job_pairs(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, void* stream);
+static int set_job_pairs(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, bool create,
+                         void* stream, size_t pin_off = 0);
 
 // Coarse-to-fine order of the collision waypoints 0..W: breadth-first interval bisection, so
 // every prefix is spread evenly over the path (k_sspp_c2f phase 1 tests a prefix).
@@ -505,7 +507,11 @@ static int upload_basis(const std::vector<double>& us, int p, const double* knot
     return upload(d_span, sp.data(), sp.size());
 }
 
-static int set_job_pairs(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, void* stream) {
+// The job's pair tables (ordered; the sampled candidates' reachable subset).  create: allocate
+// and copy synchronously; otherwise queue the copies on `stream` from the pinned staging at
+// byte offset `pin_off` (the caller sized it for both tables).
+static int set_job_pairs(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, bool create,
+                         void* stream, size_t pin_off) {
     const sspp_scene* sc = j->scene;
     const char* po = getenv("SSPP_PAIR_ORDER");  // 0 = scene order (profiling)
     j->h_pairs = (po && atoi(po) == 0) ? sc->pairs : pairs_for_job(sc, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D);
@@ -514,20 +520,21 @@ static int set_job_pairs(sspp_job* j, const double* init_ctrl, double sigma, con
                                          : reachable_pairs(sc, j->h_pairs, init_ctrl, j->n, j->D, j->p, sigma, limits, j->sampler);
     table_flags(sc, j->h_pairs, &j->np_full, &j->cb_full, &j->og_full);
     table_flags(sc, j->h_pairs_s, &j->np_samp, &j->cb_samp, &j->og_samp);
-    const size_t bytes = sizeof(DPair) * j->h_pairs.size();
-    if (!stream) {
+    const size_t bytes = sizeof(DPair) * j->h_pairs.size(), bytes_s = sizeof(DPair) * j->h_pairs_s.size();
+    if (create) {
         int rc;
         if ((rc = upload(&j->d_pairs, j->h_pairs.data(), j->h_pairs.size()))) return rc;
         HIPCHK(hipMalloc((void**)&j->d_pairs_s, std::max<size_t>(bytes, sizeof(DPair))));
-        if (!j->h_pairs_s.empty())
-            HIPCHK(hipMemcpy(j->d_pairs_s, j->h_pairs_s.data(), sizeof(DPair) * j->h_pairs_s.size(), hipMemcpyHostToDevice));
+        if (bytes_s) HIPCHK(hipMemcpy(j->d_pairs_s, j->h_pairs_s.data(), bytes_s, hipMemcpyHostToDevice));
         return SSPP_OK;
     }
+    if (pin_off + bytes + bytes_s > j->h_pin_bytes) return sspp::set_error(SSPP_E_NOMEM, "pair staging too small");
     hipStream_t st = (hipStream_t)stream;
-    HIPCHK(hipMemcpyAsync(j->d_pairs, j->h_pairs.data(), bytes, hipMemcpyHostToDevice, st));
-    if (!j->h_pairs_s.empty())
-        HIPCHK(hipMemcpyAsync(j->d_pairs_s, j->h_pairs_s.data(), sizeof(DPair) * j->h_pairs_s.size(),
-                              hipMemcpyHostToDevice, st));
+    unsigned char* pa = j->h_pin + pin_off;
+    std::memcpy(pa, j->h_pairs.data(), bytes);
+    std::memcpy(pa + bytes, j->h_pairs_s.data(), bytes_s);
+    HIPCHK(hipMemcpyAsync(j->d_pairs, pa, bytes, hipMemcpyHostToDevice, st));
+    if (bytes_s) HIPCHK(hipMemcpyAsync(j->d_pairs_s, pa + bytes, bytes_s, hipMemcpyHostToDevice, st));
     return SSPP_OK;
 }
 
@@ -574,6 +581,8 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
         sspp_job_free(j);
         return rc;
     }
+    j->h_stage.assign(a->init_ctrl, a->init_ctrl + (size_t)n * D);
+    j->h_stage.insert(j->h_stage.end(), a->limits, a->limits + D);
     j->npert = (n - 2 * p) * D;
     if (j->npert < 0) j->npert = 0;
     {  // 1: k_sspp_c2f (default), 2: k_sspp_wq1 + k_sspp_wq2, 0: k_sspp
@@ -610,7 +619,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
             sspp_job_free(j);
             return rc;
         }
-        if (scene && !scene->pairs.empty() && (rc = set_job_pairs(j, a->init_ctrl, a->sigma, a->limits, nullptr))) {
+        if (scene && !scene->pairs.empty() && (rc = set_job_pairs(j, a->init_ctrl, a->sigma, a->limits, true, nullptr))) {
             sspp_job_free(j);
             return rc;
         }
@@ -857,16 +866,42 @@ extern "C" int sspp_job_update_sspp(sspp_job* j, const double* init_ctrl, double
     if (!j || j->kind != 0 || !init_ctrl || !limits) return sspp::set_error(SSPP_E_INVAL, "sspp_job_update_sspp: bad argument");
     const size_t nd = (size_t)j->n * j->D;
     hipStream_t st = (hipStream_t)stream;
+    j->seed = seed;  // a kernel argument: nothing to upload
+    // the device tables depend only on (init_ctrl, sigma, limits): an update that repeats the
+    // values the device holds (a planning loop re-planning the same query) uploads nothing
+    if (j->h_stage.size() == nd + (size_t)j->D && j->sigma == sigma &&
+        std::memcmp(j->h_stage.data(), init_ctrl, sizeof(double) * nd) == 0 &&
+        std::memcmp(j->h_stage.data() + nd, limits, sizeof(double) * j->D) == 0)
+        return SSPP_OK;
+    const bool pairs = j->d_pairs && j->scene && !j->h_knots.empty();
+    const size_t vbytes = sizeof(double) * (nd + j->D);
+    const size_t need = vbytes + (pairs ? 2 * sizeof(DPair) * j->scene->pairs.size() : 0);
+    // the pinned staging is the source of the previous update's copies until they complete
+    if (j->upd_pending) {
+        HIPCHK(hipEventSynchronize(j->upd_ev));
+        j->upd_pending = false;
+    }
+    if (need > j->h_pin_bytes) {
+        if (j->h_pin) HIPCHK(hipHostFree(j->h_pin));
+        j->h_pin = nullptr;
+        j->h_pin_bytes = 0;
+        HIPCHK(hipHostMalloc((void**)&j->h_pin, need, hipHostMallocDefault));
+        j->h_pin_bytes = need;
+    }
+    if (!j->upd_ev) HIPCHK(hipEventCreateWithFlags(&j->upd_ev, hipEventDisableTiming));
     j->h_stage.assign(init_ctrl, init_ctrl + nd);
     j->h_stage.insert(j->h_stage.end(), limits, limits + j->D);
     j->sigma = sigma;
-    j->seed = seed;
-    HIPCHK(hipMemcpyAsync(j->d_init, j->h_stage.data(), sizeof(double) * nd, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(j->d_limits, j->h_stage.data() + nd, sizeof(double) * j->D, hipMemcpyHostToDevice, st));
-    if (j->d_pairs && j->scene && !j->h_knots.empty()) {
-        const int rc = set_job_pairs(j, init_ctrl, sigma, limits, stream);
+    std::memcpy(j->h_pin, j->h_stage.data(), vbytes);
+    const double* pv = (const double*)j->h_pin;
+    HIPCHK(hipMemcpyAsync(j->d_init, pv, sizeof(double) * nd, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(j->d_limits, pv + nd, sizeof(double) * j->D, hipMemcpyHostToDevice, st));
+    if (pairs) {
+        const int rc = set_job_pairs(j, init_ctrl, sigma, limits, false, stream, vbytes);
         if (rc) return rc;
     }
+    HIPCHK(hipEventRecord(j->upd_ev, st));
+    j->upd_pending = true;
     return SSPP_OK;
 }
 
@@ -898,9 +933,9 @@ extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args*
     j->cpb = kBlock / j->lpc;
     j->lds = sizeof(double) * ((size_t)2 * j->cpb * n * 4 + 3 * (kBlock / 64) + 4) + sizeof(int) * j->cpb;
     if (j->lds > 160 * 1024) { delete j; return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS"); }
-    std::vector<double> u(n), knots(n + 3), Minv((size_t)n * n);
+    std::vector<double> u(n), knots(n + 3), Minv((size_t)2 * n * n + n);  // QR program
     for (int i = 0; i < n; ++i) u[i] = (double)i / (n - 1);
-    if (sspp::collocation_inverse(u.data(), n, 2, knots.data(), Minv.data()) != 0) {
+    if (sspp::qr_program(u.data(), n, 2, knots.data(), Minv.data()) != 0) {
         delete j;
         return sspp::set_error(SSPP_E_INVAL, "singular collocation matrix");
     }
@@ -1016,6 +1051,11 @@ extern "C" void sspp_job_free(sspp_job* j) {
     if (j->d_wspert) (void)hipFree(j->d_wspert);
     if (j->d_wqueue) (void)hipFree(j->d_wqueue);
     if (j->d_wlist) (void)hipFree(j->d_wlist);
+    if (j->upd_ev) {
+        (void)hipEventSynchronize(j->upd_ev);
+        (void)hipEventDestroy(j->upd_ev);
+    }
+    if (j->h_pin) (void)hipHostFree(j->h_pin);
     delete j;
 }
 

@@ -22,6 +22,7 @@
 #include <cmath>
 #include <iostream>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -120,6 +121,7 @@ public:
         if (sample_count < 1) throw py::value_error("sample_count must be >= 1");
         if (init_points < 4) throw py::value_error("init_points must be >= 4");
         if (check_points < 2) throw py::value_error("check_points must be >= 2");
+        auto lk = lock();  // held until the shared buffers below have been read
         ensure_planner();
         const int n = init_points;
         const size_t nd = (size_t)n * N;
@@ -186,6 +188,7 @@ public:
     bool checkCollision(const Spline<N>& s, int num_samples, py::object /*data*/) {
         if (num_samples < 1) throw py::value_error("num_samples must be >= 1");
         if (s.ctrl.empty()) throw py::value_error("checkCollision on an empty spline");
+        auto lk = lock();
         ensure_planner();
         double arc;
         uint8_t feas;
@@ -204,6 +207,7 @@ public:
     double computeArcLength(const Spline<N>& s, int check_points) {
         if (check_points < 2) throw py::value_error("check_points must be >= 2");
         if (s.ctrl.empty()) throw py::value_error("computeArcLength on an empty spline");
+        auto lk = lock();
         ensure_planner();
         double arc;
         uint8_t feas;
@@ -229,6 +233,7 @@ public:
             std::vector<double> arc(paths.size());
             std::vector<uint8_t> feas(paths.size());
             sspp_best b;
+            auto lk = lock();
             ensure_planner();
             ck(sspp_planner_score(planner_.get(), f.knots.data(), 3, all.data(), (int64_t)paths.size(),
                                   f.n(), check_points, 0, arc.data(), feas.data(), &b),
@@ -261,6 +266,17 @@ private:
     struct SceneDel { void operator()(sspp_scene* s) const { sspp_scene_free(s); } };
     struct PlannerDel { void operator()(sspp_planner* p) const { sspp_planner_free(p); } };
 
+    // One call at a time per object: plan / checkCollision / computeArcLength / findBestPath
+    // share the sspp_planner's device and pinned buffers and this object's host buffers.  The
+    // mutex is taken with the GIL released (a thread holding it re-acquires the GIL after its
+    // device call, so waiting for it while holding the GIL would deadlock).
+    std::unique_lock<std::mutex> lock() {
+        std::unique_lock<std::mutex> lk(mu_, std::defer_lock);
+        py::gil_scoped_release nogil;
+        lk.lock();
+        return lk;
+    }
+
     void ensure_planner() {
         if (planner_) return;
         if (!scene_) {
@@ -280,6 +296,7 @@ private:
     std::vector<double> knots_buf_, arc_buf_, ctrl_buf_;
     std::vector<int64_t> ids_buf_;
     Spline<N> path_;
+    std::mutex mu_;
 };
 
 template <int N>

@@ -337,6 +337,64 @@ def test_config5_multigoal_full_size_each_iteration(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("unfused", [0, 1])
+def test_icra_anytime_size_each_iteration(cuda, monkeypatch, unfused):
+    """The reference's ICRA anytime configuration (src/main_icra_benchmark.cpp:151-179: 15
+    samples x 40 checks, 1 via, gripper on robocrane.xml, block_green -> block_orange): 20
+    iterations, each against the oracle.  17 slots take the one-launch update (ranking inside
+    k_ces_update); SSPP_CES_UNFUSED=1 forces rank + scatter + update — both bit-identical."""
+    import bench
+    import sspp_amd as S
+    if unfused:
+        monkeypatch.setenv("SSPP_CES_UNFUSED", "1")
+    cfg = bench.ICRA
+    model = S.Model(ROBOCRANE)
+    body = model.body_id(bench.ICRA_BODY)
+    scene = S.Scene(model, 1, body)
+    osc = O.Scene(mjcf_ref.load(ROBOCRANE), 1, body)
+    lo, hi = cfg["limits_min"], cfg["limits_max"]
+    st = model.body_point("block_green/") + np.array([0, 0, 0.02, 0])
+    en = model.body_point("block_orange/") + np.array([0, 0, 0.02, 0])
+    kw = {k: cfg[k] for k in ("stddev_initial", "stddev_min", "stddev_max", "stddev_increase_factor",
+                              "stddev_decay_factor", "elite_fraction", "sample_count", "check_points",
+                              "init_points", "collision_weight", "z_min", "sigma_floor", "var_ema_beta",
+                              "mean_lr")}
+    pl = S.CesPlanner(scene, limits_min=lo, limits_max=hi, **kw)
+    ocfg = dict(frac=cfg["elite_fraction"], inc=cfg["stddev_increase_factor"],
+                dec=cfg["stddev_decay_factor"], sigma_floor=cfg["sigma_floor"], var_beta=cfg["var_ema_beta"],
+                mean_lr=cfg["mean_lr"], sd_min=cfg["stddev_min"], sd_max=cfg["stddev_max"],
+                dist_z_min=cfg["stddev_initial"], lo=lo, hi=hi)
+    samples, z_min = cfg["sample_count"], cfg["z_min"]
+    m_in, s_in = O.ces_reset(st, en, 3, z_min, cfg["stddev_initial"], 0.3, cfg["stddev_min"],
+                             cfg["stddev_max"], cfg["sigma_floor"], lo, hi)
+    lb_in, hb_in = np.zeros((1, 4)), False
+    succ = 0
+    for t in range(20):
+        pl.step(st, en, iterate=t > 0)
+        r = pl.read()
+        nfx = 2 if (t > 0 and hb_in) else 1
+        assert r["n_fixed"] == nfx and r["n_candidates"] == nfx + samples
+        np.testing.assert_array_equal(r["vias"][0], np.where(np.arange(4) == 2, np.maximum(m_in, z_min), m_in))
+        smp = O.sample_tsp(m_in, s_in, lo, hi, z_min, S.DEFAULT_SEED, t * samples, samples)
+        assert np.abs(r["vias"][nfx:] - smp).max() <= 1e-12
+        L, Cnf, Cwf, stt, cost = O.tsp_score(osc, st, en, r["vias"], cfg["check_points"])
+        np.testing.assert_array_equal(r["status"], stt)
+        fin = np.isfinite(cost)
+        for a, b in ((r["cost"][fin], cost[fin]), (r["L"], L), (r["C_nf"], Cnf), (r["C_wf"], Cwf)):
+            assert (np.abs(a - b) <= 1e-12 * np.maximum(1.0, np.abs(b))).all()
+        m, s, lb, hb, ns, el, bs = O.ces_update(r["cost"], r["status"], r["vias"], m_in, s_in, lb_in, hb_in,
+                                                **ocfg)
+        assert r["n_success"] == ns and r["best_slot"] == bs and r["has_best"] == hb
+        np.testing.assert_array_equal(r["elites"], el)
+        np.testing.assert_array_equal(r["mean"], m)
+        np.testing.assert_array_equal(r["sigma"], s)
+        np.testing.assert_array_equal(r["last_best"], lb)
+        succ += ns > 0
+        m_in, s_in, lb_in, hb_in = m, s, lb, hb
+    assert succ >= 10
+
+
+@pytest.mark.gpu
 def test_elite_fraction_above_one_rejected(cuda):
     """tsp_elites.h:15-19 would partial_sort past the end for frac > 1: rejected at creation."""
     import sspp_amd as S

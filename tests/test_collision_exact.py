@@ -140,6 +140,59 @@ def test_box_box_manifold_tilted_edge_and_edge_edge():
     assert (n, nd) == (1, 0)
 
 
+def _clip_convex(P, Q):
+    """Sutherland-Hodgman: convex polygon P (CCW, k x 2) clipped to convex polygon Q (CCW)."""
+    out = [np.asarray(p, float) for p in P]
+    for i in range(len(Q)):
+        a, b = np.asarray(Q[i], float), np.asarray(Q[(i + 1) % len(Q)], float)
+        side = lambda p: (b[0] - a[0]) * (p[1] - a[1]) - (b[1] - a[1]) * (p[0] - a[0])  # noqa: E731
+        inp, out = out, []
+        for j in range(len(inp)):
+            cur, nxt = inp[j], inp[(j + 1) % len(inp)]
+            sc, sn = side(cur), side(nxt)
+            if sc >= 0:
+                out.append(cur)
+            if (sc >= 0) != (sn >= 0):
+                out.append(cur + (nxt - cur) * (sc / (sc - sn)))
+    return out
+
+
+def _rect(cx, cy, a, b, yaw):
+    c, s = math.cos(yaw), math.sin(yaw)
+    return [(cx + c * x - s * y, cy + s * x + c * y) for x, y in ((-a, -b), (a, -b), (a, b), (-a, b))]
+
+
+def test_box_box_manifold_non_square_overlap():
+    """Face-on-face contacts whose overlap is not the incident face itself: a thin rectangle,
+    yawed, sunk 5 mm into the big box's top face across the face's edge.  Every clipped point
+    is 5 mm deep, so the deep count is the number of vertices of the exact intersection of the
+    two rectangles (computed independently here by polygon clipping)."""
+    q = lambda yaw: (math.cos(yaw / 2), 0, 0, math.sin(yaw / 2))  # noqa: E731
+    # yawed 30 deg, one corner past x = 0.3: three corners + two points on the edge
+    assert _deep((0.1, 0.02, 0.05), (0.21, 0, 0.145), q(math.pi / 6))[2] == 5
+    # the big face's corner (0.3, 0.3) inside the rectangle: that corner, the points where the
+    # rectangle's edges cross x = 0.3 and y = 0.3, and the rectangle's two corners inside the face
+    ref = _rect(0, 0, 0.3, 0.3, 0.0)
+    inc = _rect(0.27, 0.27, 0.1, 0.05, math.pi / 4)
+    want = len(_clip_convex(inc, ref))
+    assert want == 5
+    assert _deep((0.1, 0.05, 0.05), (0.27, 0.27, 0.145), q(math.pi / 4))[2] == want
+    rng = np.random.default_rng(5)
+    seen = set()
+    for _ in range(300):
+        a, b = rng.uniform(0.02, 0.15), rng.uniform(0.01, 0.15)
+        yaw = rng.uniform(-math.pi, math.pi)
+        cx, cy = rng.uniform(0.15, 0.29, 2) * rng.choice([-1, 1], 2)
+        inc = _rect(cx, cy, a, b, yaw)
+        # skip near-degenerate placements (a corner within 1e-6 of the face's edge lines)
+        if min(abs(abs(c) - 0.3) for p in inc for c in p) < 1e-6:
+            continue
+        want = len(_clip_convex(inc, ref))
+        assert _deep((a, b, 0.05), (cx, cy, 0.145), q(yaw))[2] == want, (a, b, yaw, cx, cy)
+        seen.add(want)
+    assert {4, 5, 6} <= seen
+
+
 def _box_sat_distance(pa, Ma, ea, pb, Mb, eb):
     """exact signed distance of two boxes: max separation over the 15 SAT axes"""
     axes = [Ma[:, i] for i in range(3)] + [Mb[:, j] for j in range(3)]

@@ -29,6 +29,12 @@ def _problem():
     return O.Scene(m, 0, 7), knots, ctrl0
 
 
+# Philox seed of the sampled batch: chosen so that the batch mixes feasible and infeasible
+# candidates (asserted in the test; round 2 moved it from 11 when the sampler changed and the
+# old seed's batch became all-infeasible)
+SEED = 12
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -38,7 +44,7 @@ def _worker(rank, world, port, q):
     scene, knots, ctrl0 = _problem()
     per = B_ // world
     first = rank * per
-    ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 12, first, per)
+    ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), SEED, first, per)
     arc, feas = O.sspp_score(scene, knots, 3, ctrl, W_, nthreads=1)
     idx, cost = O.argmin(arc, feas)
     rec = torch.tensor([np.float64(cost).view(np.int64), idx + first if idx >= 0 else -1,
@@ -64,7 +70,7 @@ def test_sharded_argmin_equals_global(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     scene, knots, ctrl0 = _problem()
-    ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), 12, 0, B_)
+    ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), SEED, 0, B_)
     arc, feas = O.sspp_score(scene, knots, 3, ctrl, W_, nthreads=1)
     idx, cost = O.argmin(arc, feas)
     assert feas.any() and not feas.all()

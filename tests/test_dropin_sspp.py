@@ -154,3 +154,43 @@ def test_plan_cached_state_across_shapes(sp, capfd):
             assert abs(planner.last_best_cost - best) <= 1e-12
             np.testing.assert_allclose(planner.get_ctrl_pts().T, ctrl[idx], atol=1e-12)
     capfd.readouterr()
+
+
+def test_plan_sspp_c_abi_cached(cuda):
+    """sspp_plan_sspp (the blocking all-candidates plan() of the C ABI) on
+    its cached planner: repeated calls, a shape change and a freed-and-recreated scene, each
+    against the oracle on the same Philox candidates."""
+    import ctypes as C
+    import sspp_amd as S
+    from sspp_amd._lib import Best, lib
+    L = lib()
+    osc = O.Scene(mjcf_ref.load(ROBOCRANE), 0, 7)
+    start = np.array([0.5, 0.15, 0.136, 0.707, 0, 0, 0.707])
+    end = np.array([0.5, -0.05, 0.136, 0.707, 0, 0, 0.707])
+    lim = np.ones(7)
+    p = lambda a, t=C.c_double: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    nfeas = 0
+    for round_ in range(2):
+        scene = S.Scene(S.Model(ROBOCRANE), 0, 7)
+        for B, W, n, seed in ((2000, 64, 10, 7), (2000, 64, 10, 8), (777, 48, 6, 9), (1500, 64, 10, 10)):
+            knots, ctrl = np.zeros(n + 4), np.zeros((B, n, 7))
+            feas, arc, best = np.zeros(B, np.uint8), np.zeros(B), Best()
+            rc = L.sspp_plan_sspp(scene.handle, 7, p(start), p(end), C.c_double(0.08), p(lim), B, W, n,
+                                  C.c_uint64(seed), p(knots), p(ctrl), p(feas, C.c_uint8), p(arc), C.byref(best))
+            assert rc == 0, L.sspp_last_error()
+            u = np.array([i / (n - 1) for i in range(n)])
+            k0, c0 = O.interpolate(np.array([(1 - t) * start + t * end for t in u]), 3, u)
+            np.testing.assert_allclose(knots, k0, rtol=0, atol=1e-15)
+            want = O.sample_sspp(c0, 3, 0.08, lim, seed, 0, B)
+            assert np.abs(ctrl - want).max() <= 1e-12
+            oarc, ofeas = O.sspp_score(osc, knots, 3, ctrl, W)
+            np.testing.assert_array_equal(feas, ofeas)
+            fin = ofeas.astype(bool)
+            nfeas += int(fin.sum())
+            if fin.any():
+                assert np.abs(arc[fin] - oarc[fin]).max() <= 1e-12
+                assert best.index == O.argmin(oarc, ofeas)[0]
+            else:
+                assert best.index == -1
+        del scene  # sspp_scene_free drops the cached planner of this scene
+    assert nfeas > 0
