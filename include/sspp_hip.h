@@ -275,12 +275,13 @@ int sspp_job_update_sspp(sspp_job* job, const double* init_ctrl /* [n][D] */, do
  * One object per `_sspp.SamplingPathPlannerN` (src/sspp_bindings.cpp:24-50): it owns a HIP
  * stream, the job of the last plan() shape (init_points, check_points, capacity) and the
  * device / pinned buffers, so a plan() call is: initializePath on the host, an asynchronous
- * job update, one scoring launch, one compaction launch that writes the feasible candidates
- * (ids, arc lengths, control points — in candidate order) straight into pinned host memory,
- * and one stream synchronisation.  Not re-entrant per object (as the reference's planner).
+ * job update (skipped when the query repeats), one scoring launch that writes arc lengths,
+ * feasibility, the argmin record and the feasible candidates' control points straight into
+ * mapped pinned host memory, one stream synchronisation, and a host gather of the feasible
+ * rows in candidate order.  Not re-entrant per object (as the reference's planner).
  *   sspp_planner_plan  <- SamplingPathPlanner::plan (include/sspp.h:194-225): writes
- *     knots [init_points+4], *n_feasible, feasible ids / arc / ctrl [n_feasible][n][D]
- *     (caller buffers sized for sample_count) and the argmin record.
+ *     knots [init_points+4], *n_feasible, feasible ids (first_id + index) / arc / ctrl
+ *     [n_feasible][n][D] (caller buffers sized for sample_count) and the argmin record.
  *   sspp_planner_score <- checkCollision / computeArcLength / findBestPath on host splines
  *     sharing one knot vector (include/sspp.h:132-192); with_collision = 0: arc length only. */
 typedef struct sspp_planner sspp_planner;

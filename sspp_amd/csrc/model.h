@@ -52,6 +52,8 @@ struct TspCesEval {
 int tsp_eval_ces(sspp_job* j, const TspCesEval* e, int64_t n, double* d_L, double* d_Cnf,
                  double* d_Cwf, uint8_t* d_status, double* d_cost, double* d_vias_out,
                  void* stream);
+// k_sspp_c2f writes ctrl_out rows only for feasible candidates (drop-in planner, planner.hip)
+void job_set_ctrl_feasible_only(sspp_job* j, int on);
 // sspp_plan_sspp's cached planners (planner.hip): dropped when their scene is freed
 void planner_cache_drop(const sspp_scene* scene);
 }  // namespace sspp

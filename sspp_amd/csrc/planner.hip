@@ -5,11 +5,14 @@
 // lifetime (initializeDataCopies, include/sspp.h:235-244); here the planner keeps, per object:
 // a HIP stream, the job of the last plan() shape (its basis tables, pair table and argmin
 // counters stay on the device), the candidate buffers, and pinned host memory that the
-// compaction kernel writes the feasible candidates into.  A plan() call is therefore
-//   initializePath (host, µs) -> sspp_job_update_sspp (3 small async copies)
-//   -> k_sspp_c2f (sample + score + fused argmin) -> k_compact_feasible -> stream sync
-// with no allocation, no device-wide synchronisation and no copy of infeasible candidates
-// (plan() returns only the feasible splines, include/sspp.h:215-216).
+// scoring kernel writes its outputs into.  A plan() call is therefore
+//   initializePath (host, µs) -> sspp_job_update_sspp (async copies; none when the query
+//   repeats) -> k_sspp_c2f (sample + score + fused argmin; arc / feasible / the argmin record
+//   and the control points of the feasible candidates only, straight into pinned host memory)
+//   -> stream sync -> the feasible rows gathered on the host in candidate order
+// with no allocation, no device-wide synchronisation, no second launch and no copy of
+// infeasible candidates' control points (plan() returns only the feasible splines,
+// include/sspp.h:215-216).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -20,64 +23,6 @@
 #include "model.h"
 
 namespace {
-
-constexpr int kCompactThreads = 1024;
-
-// Pinned-memory header the compaction kernel fills (host reads it after the stream sync).
-struct CompactHdr {
-    long long count;
-    long long pad;
-    sspp_best best;
-};
-
-// Stable compaction of the feasible candidates in candidate order (findBestPath's input,
-// include/sspp.h:215-216): one workgroup walks the batch in chunks of 1024; a chunk's
-// positions come from wave ballots + per-wave prefix counts in LDS; the feasible rows are then
-// copied cooperatively.  Outputs go to pinned host memory (written once, read after the sync).
-__global__ __launch_bounds__(kCompactThreads) void k_compact_feasible(
-    const unsigned char* __restrict__ feas, const double* __restrict__ arc,
-    const double* __restrict__ ctrl, long long B, int nd, const sspp_best* __restrict__ best,
-    CompactHdr* hdr, long long* ids, double* arc_out, double* ctrl_out) {
-    __shared__ int s_wave[kCompactThreads / 64 + 1];
-    __shared__ int s_pos[kCompactThreads];
-    __shared__ long long s_base;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    for (long long c0 = 0; c0 < B; c0 += kCompactThreads) {
-        const long long i = c0 + tid;
-        const bool f = i < B && feas[i] != 0;
-        const unsigned long long m = __ballot(f);
-        if (lane == 0) s_wave[w] = __popcll(m);
-        __syncthreads();
-        if (tid == 0) {
-            int acc = 0;
-            for (int k = 0; k < kCompactThreads / 64; ++k) { const int t = s_wave[k]; s_wave[k] = acc; acc += t; }
-            s_wave[kCompactThreads / 64] = acc;
-        }
-        __syncthreads();
-        const int nf = s_wave[kCompactThreads / 64];
-        const long long base = s_base;
-        if (f) {
-            const int pos = s_wave[w] + __popcll(m & ((1ull << lane) - 1ull));
-            s_pos[pos] = tid;
-            ids[base + pos] = i;
-            arc_out[base + pos] = arc[i];
-        }
-        __syncthreads();
-        for (long long e = tid; e < (long long)nf * nd; e += kCompactThreads) {
-            const int r = (int)(e / nd), k = (int)(e - (long long)r * nd);
-            ctrl_out[(base + r) * nd + k] = ctrl[(c0 + s_pos[r]) * nd + k];
-        }
-        __syncthreads();
-        if (tid == 0) s_base = base + nf;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        hdr->count = s_base;
-        hdr->best = *best;
-    }
-}
 
 int hipck(hipError_t e, const char* what) {
     if (e == hipSuccess) return SSPP_OK;
@@ -140,9 +85,9 @@ struct sspp_planner {
     Dev<double> d_arc, d_ctrl;
     Dev<unsigned char> d_feas;
     Dev<sspp_best> d_best;
-    Pinned<CompactHdr> h_hdr;
-    Pinned<long long> h_ids;
-    Pinned<double> h_arc, h_ctrl;
+    Pinned<double> h_arc, h_ctrl;      // plan(): the scoring kernel's outputs (mapped)
+    Pinned<unsigned char> h_feas;
+    Pinned<sspp_best> h_best;
     // score(): job keyed on (knots, n, W, collision)
     JobRef score_job;
     std::vector<double> score_knots;
@@ -179,10 +124,13 @@ extern "C" void sspp_planner_free(sspp_planner* p) { delete p; }
 
 // plan()'s common front: initializePath on the host, then the job of this shape created (first
 // call / new shape / larger batch) or re-targeted asynchronously, then one scoring launch on the
-// planner's stream.  ctrl_dev: the sampled control points are written to d_ctrl.
+// planner's stream.  pinned_out: arc / feasible / best and the feasible candidates' control
+// points go straight to the mapped pinned buffers (plan()); otherwise to device memory, the
+// control points of every candidate only with all_ctrl (sspp_plan_sspp).
 static int plan_enqueue(sspp_planner* p, const double* start, const double* end, double sigma,
                         const double* limits, int sample_count, int check_points, int init_points,
-                        uint64_t seed, int64_t first_id, double* knots_out, bool ctrl_dev) {
+                        uint64_t seed, int64_t first_id, double* knots_out, bool pinned_out,
+                        bool all_ctrl = false) {
     const int n = init_points, D = p->D, deg = 3;
     if (sample_count < 1) return sspp::set_error(SSPP_E_INVAL, "sample_count must be >= 1");
     if (n < deg + 1) return sspp::set_error(SSPP_E_INVAL, "init_points must be >= 4 for a cubic spline");
@@ -207,16 +155,26 @@ static int plan_enqueue(sspp_planner* p, const double* start, const double* end,
         if ((rc = sspp_job_create_sspp(p->scene, &a, B, &p->plan_job.j))) return rc;
         p->plan_n = n; p->plan_W = check_points; p->plan_cap = B;
         if ((rc = p->d_arc.reserve(B)) || (rc = p->d_feas.reserve(B)) || (rc = p->d_best.reserve(1)) ||
-            (rc = p->d_ctrl.reserve(B * nd)) || (rc = p->h_hdr.reserve(1)) || (rc = p->h_ids.reserve(B)) ||
-            (rc = p->h_arc.reserve(B)) || (rc = p->h_ctrl.reserve(B * nd))) {
+            (rc = p->d_ctrl.reserve(B * nd)) || (rc = p->h_arc.reserve(B)) || (rc = p->h_feas.reserve(B)) ||
+            (rc = p->h_best.reserve(1)) || (rc = p->h_ctrl.reserve(B * nd))) {
             p->plan_job.reset();
             return rc;
         }
     } else if ((rc = sspp_job_update_sspp(p->plan_job.j, ctrl0.data(), sigma, limits, seed, p->stream))) {
         return rc;
     }
-    return sspp_job_sample_score(p->plan_job.j, first_id, B, p->d_arc.p, p->d_feas.p,
-                                 ctrl_dev ? p->d_ctrl.p : nullptr, p->d_best.p, p->stream);
+    // pinned_out: outputs straight into the mapped pinned buffers, control points of the
+    // feasible candidates only; otherwise every candidate's outputs to device memory
+    sspp::job_set_ctrl_feasible_only(p->plan_job.j, pinned_out ? 1 : 0);
+    if (!pinned_out)
+        return sspp_job_sample_score(p->plan_job.j, first_id, B, p->d_arc.p, p->d_feas.p,
+                                     all_ctrl ? p->d_ctrl.p : nullptr, p->d_best.p, p->stream);
+    double* ha = p->h_arc.dev();
+    unsigned char* hf = p->h_feas.dev();
+    sspp_best* hb = p->h_best.dev();
+    double* hc = p->h_ctrl.dev();
+    if (!ha || !hf || !hb || !hc) return sspp::set_error(SSPP_E_HIP, "hipHostGetDevicePointer failed");
+    return sspp_job_sample_score(p->plan_job.j, first_id, B, ha, hf, hc, hb, p->stream);
 }
 
 extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const double* end, double sigma,
@@ -229,25 +187,22 @@ extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const dou
         return sspp::set_error(SSPP_E_INVAL, "sspp_planner_plan: null argument");
     int rc;
     if ((rc = plan_enqueue(p, start, end, sigma, limits, sample_count, check_points, init_points, seed,
-                           first_id, knots_out, true)))
+                           first_id, knots_out, true)) ||
+        (rc = hipck(hipStreamSynchronize(p->stream), "plan")))
         return rc;
+    // the feasible candidates in candidate order (findBestPath's input, include/sspp.h:215-216)
     const size_t nd = (size_t)init_points * p->D;
-    const int64_t B = sample_count;
-    CompactHdr* hh = p->h_hdr.dev();
-    long long* hi = p->h_ids.dev();
-    double* ha = p->h_arc.dev();
-    double* hc = p->h_ctrl.dev();
-    if (!hh || !hi || !ha || !hc) return sspp::set_error(SSPP_E_HIP, "hipHostGetDevicePointer failed");
-    hipLaunchKernelGGL(k_compact_feasible, dim3(1), dim3(kCompactThreads), 0, p->stream, p->d_feas.p,
-                       p->d_arc.p, p->d_ctrl.p, (long long)B, (int)nd, p->d_best.p, hh, hi, ha, hc);
-    if ((rc = hipck(hipGetLastError(), "k_compact_feasible launch"))) return rc;
-    if ((rc = hipck(hipStreamSynchronize(p->stream), "plan"))) return rc;
-    const long long cnt = p->h_hdr.p->count;
+    const unsigned char* f = p->h_feas.p;
+    long long cnt = 0;
+    for (int64_t i = 0; i < sample_count; ++i) {
+        if (f[i] != 1) continue;
+        if (feasible_ids) feasible_ids[cnt] = first_id + i;
+        if (feasible_arc) feasible_arc[cnt] = p->h_arc.p[i];
+        if (feasible_ctrl) std::memcpy(feasible_ctrl + cnt * nd, p->h_ctrl.p + i * nd, sizeof(double) * nd);
+        ++cnt;
+    }
     *n_feasible = cnt;
-    *best_out = p->h_hdr.p->best;
-    if (feasible_ids) std::memcpy(feasible_ids, p->h_ids.p, sizeof(long long) * cnt);
-    if (feasible_arc) std::memcpy(feasible_arc, p->h_arc.p, sizeof(double) * cnt);
-    if (feasible_ctrl) std::memcpy(feasible_ctrl, p->h_ctrl.p, sizeof(double) * cnt * nd);
+    *best_out = *p->h_best.p;
     return SSPP_OK;
 }
 
@@ -297,7 +252,7 @@ extern "C" int sspp_plan_sspp(const sspp_scene* scene, int dof, const double* st
         c.entries.push_back({scene, dof, p});
     }
     if ((rc = plan_enqueue(p, start, end, sigma, limits, sample_count, check_points, init_points, seed, 0,
-                           knots_out, ctrl_out != nullptr)))
+                           knots_out, false, ctrl_out != nullptr)))
         return rc;
     // every candidate's outputs through the pinned staging (async copies, one stream sync)
     const int64_t B = sample_count;

@@ -248,10 +248,6 @@ SSPP_HD int col_sphere_cyl(const double* sp, double r, const double* cp, const d
     return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 
-// Overlap witness for two boxes: the centre of one strictly inside the other.  Then every SAT
-// axis L has |T.L| < ra(L) (T = sum t_k A_k with |t_k| < e_k), so each separation is below
-// -rb < 0 <= margin and sat_box_box reports the contact too; this settles the deep penetrations
-// of colliding candidates with 3 dot products instead of the 15-axis test.
 // Separating-axis test, two boxes: true iff every one of the 15 axis separations < thr.
 // Rows of R = A^T B are formed lazily so that an early separating face of A (the common
 // case: the moving box hovering over a static box) skips the rest.  Edge axes compare the
@@ -311,76 +307,13 @@ SSPP_HD bool sat_box_box(const double* pa, const double* ma, const double* ea, c
     return true;
 }
 
-// Box-box deep contacts (TaskSpacePlanner cost: Collision.h:89-101 adds one term per contact
-// with dist < -1e-3, and MuJoCo's box-box collider reports up to 8).  One pass:
-// * the 15-axis SAT at thr = -1e-3 exactly as sat_box_box (returns 0 at the first axis whose
-//   separation reaches it: not deep);
-// * otherwise MuJoCo-style (DESIGN.md §4): an edge-edge axis whose separation exceeds every face
-//   axis's by more than 1e-12 gives one contact; else the face axis of least penetration makes
-//   that face the reference face and the most anti-parallel face of the other box the incident
-//   face, and the contacts are the vertices of the incident face clipped to the reference face's
-//   rectangle (<= 8), dist = -(depth below the reference face): every incident edge's clipped
-//   segment (Liang-Barsky, boundary inclusive) gives its entry point and, if it leaves early,
-//   its exit point; reference corners strictly inside the incident face are vertices too.
-// Returns the number of those with dist < -1e-3, at least 1 (no clipped point is deeper than the
-// SAT depth).  Every array is indexed with compile-time indices (run-time choices are selects),
-// so everything stays in registers.
-SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double* ea,
-                               const double* pb, const double* mb, const double* eb) {
-    double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
+// The contact polygon of box_box_deep_count's face case (reference face fi: 0-2 faces of A,
+// 3-5 faces of B): the deep vertices of the incident face clipped to the reference rectangle.
+SSPP_HD int bb_clip_count(const double* pa, const double* ma, const double* ea, const double* pb,
+                          const double* mb, const double* eb, int fi) {
+    double A[3][3], Bc[3][3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) { col3(ma, j, A[j]); col3(mb, j, Bc[j]); }
-    T[0] = pb[0] - pa[0]; T[1] = pb[1] - pa[1]; T[2] = pb[2] - pa[2];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        t[i] = dot3(A[i], T);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) { R[i][j] = dot3(A[i], Bc[j]); AR[i][j] = fabs(R[i][j]); }
-    }
-    double best_face = -1e300;
-    int fi = 0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {  // faces of A
-        const double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
-        const double sep = fabs(t[i]) - (ea[i] + rb);
-        if (sep >= kDeep) return 0;
-        if (sep > best_face) { best_face = sep; fi = i; }
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {  // faces of B
-        const double pr = fabs(fma(t[2], R[2][j], fma(t[1], R[1][j], t[0] * R[0][j])));
-        const double ra = fma(ea[2], AR[2][j], fma(ea[1], AR[1][j], ea[0] * AR[0][j]));
-        const double sep = pr - (ra + eb[j]);
-        if (sep >= kDeep) return 0;
-        if (sep > best_face) { best_face = sep; fi = 3 + j; }
-    }
-    bool edge = false;  // some edge axis separates by more than best_face + 1e-12
-    const double fthr = best_face + 1e-12;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {  // edge x edge
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const double v0 = R[0][j], v1 = R[1][j], v2 = R[2][j];
-            double L[3];
-            if (i == 0) { L[0] = 0.0; L[1] = -v2; L[2] = v1; }
-            else if (i == 1) { L[0] = v2; L[1] = 0.0; L[2] = -v0; }
-            else { L[0] = -v1; L[1] = v0; L[2] = 0.0; }
-            const double len2 = dot3(L, L);
-            if (len2 < 1e-12) continue;
-            const double pr = fabs(dot3(t, L));
-            const double ra = fma(ea[2], fabs(L[2]), fma(ea[1], fabs(L[1]), ea[0] * fabs(L[0])));
-            double rb = 0.0;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const double bk[3] = {R[0][k], R[1][k], R[2][k]};
-                rb = fma(eb[k], fabs(dot3(bk, L)), rb);
-            }
-            const double num = pr - (ra + rb), len = sqrt(len2);
-            if (num >= kDeep * len) return 0;
-            edge = edge || num > fthr * len;
-        }
-    }
-    if (edge) return 1;
     auto pick3 = [](int i, double x0, double x1, double x2) { return i == 0 ? x0 : (i == 1 ? x1 : x2); };
     const bool refA = fi < 3;
     const int f = refA ? fi : fi - 3;
@@ -482,6 +415,82 @@ SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double*
         }
     }
     return nd > 0 ? nd : 1;
+}
+
+// Box-box deep contacts (TaskSpacePlanner cost: Collision.h:89-101 adds one term per contact
+// with dist < -1e-3, and MuJoCo's box-box collider reports up to 8).  One pass:
+// * the 15-axis SAT at thr = -1e-3 exactly as sat_box_box (returns 0 at the first axis whose
+//   separation reaches it: not deep);
+// * otherwise MuJoCo-style (DESIGN.md §4): an edge-edge axis whose separation exceeds every face
+//   axis's by more than 1e-12 gives one contact; else the face axis of least penetration makes
+//   that face the reference face and the most anti-parallel face of the other box the incident
+//   face, and the contacts are the vertices of the incident face clipped to the reference face's
+//   rectangle (<= 8), dist = -(depth below the reference face): every incident edge's clipped
+//   segment (Liang-Barsky, boundary inclusive) gives its entry point and, if it leaves early,
+//   its exit point; reference corners strictly inside the incident face are vertices too.
+// Returns the number of those with dist < -1e-3, at least 1 (no clipped point is deeper than the
+// SAT depth).  Every array is indexed with compile-time indices (run-time choices are selects),
+// so everything stays in registers.
+SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double* ea,
+                               const double* pb, const double* mb, const double* eb) {
+    double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { col3(ma, j, A[j]); col3(mb, j, Bc[j]); }
+    T[0] = pb[0] - pa[0]; T[1] = pb[1] - pa[1]; T[2] = pb[2] - pa[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        t[i] = dot3(A[i], T);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) { R[i][j] = dot3(A[i], Bc[j]); AR[i][j] = fabs(R[i][j]); }
+    }
+    double best_face = -1e300;
+    int fi = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // faces of A
+        const double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
+        const double sep = fabs(t[i]) - (ea[i] + rb);
+        if (sep >= kDeep) return 0;
+        if (sep > best_face) { best_face = sep; fi = i; }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // faces of B
+        const double pr = fabs(fma(t[2], R[2][j], fma(t[1], R[1][j], t[0] * R[0][j])));
+        const double ra = fma(ea[2], AR[2][j], fma(ea[1], AR[1][j], ea[0] * AR[0][j]));
+        const double sep = pr - (ra + eb[j]);
+        if (sep >= kDeep) return 0;
+        if (sep > best_face) { best_face = sep; fi = 3 + j; }
+    }
+    bool edge = false;  // some edge axis separates by more than best_face + 1e-12
+    const double fthr = best_face + 1e-12;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // edge x edge
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double v0 = R[0][j], v1 = R[1][j], v2 = R[2][j];
+            double L[3];
+            if (i == 0) { L[0] = 0.0; L[1] = -v2; L[2] = v1; }
+            else if (i == 1) { L[0] = v2; L[1] = 0.0; L[2] = -v0; }
+            else { L[0] = -v1; L[1] = v0; L[2] = 0.0; }
+            const double len2 = dot3(L, L);
+            if (len2 < 1e-12) continue;
+            const double pr = fabs(dot3(t, L));
+            const double ra = fma(ea[2], fabs(L[2]), fma(ea[1], fabs(L[1]), ea[0] * fabs(L[0])));
+            double rb = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double bk[3] = {R[0][k], R[1][k], R[2][k]};
+                rb = fma(eb[k], fabs(dot3(bk, L)), rb);
+            }
+            const double num = pr - (ra + rb), len = sqrt(len2);
+            if (num >= kDeep * len) return 0;
+            edge = edge || num > fthr * len;
+        }
+    }
+    if (edge) return 1;
+#ifdef SSPP_NO_MANIFOLD  // measurement variant only: the SAT decision without the contact polygon
+    return 1;
+#endif
+    return bb_clip_count(pa, ma, ea, pb, mb, eb, fi);
 }
 
 // ---------------------------------------------------------------- cylinder-box, exact

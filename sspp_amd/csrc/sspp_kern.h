@@ -965,6 +965,7 @@ struct SsppC2F {
     unsigned* dfr; // [0]: candidates of this launch left undecided (cylinder-box), [1]: k_sspp_cbfix arrivals
     int nt;        // launch shape (host side): threads per workgroup, dynamic LDS bytes
     int lds;
+    int ctrl_feas; // ctrl_out rows only for candidates with no contact (written at the end)
 };
 
 #ifdef SSPP_C2F_STATS
@@ -1194,7 +1195,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
         __syncthreads();
     }
-    if (ctrl_out) {
+    if (ctrl_out && !a.ctrl_feas) {
         double* dst = ctrl_out + cand0 * ndof;
         for (int e = tid; e < nvalid * ndof; e += NT) dst[e] = s_ctrl[e];
     }
@@ -1402,6 +1403,11 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         arc[c] = s_arc[tid];
         // 2: no contact except cylinder-box pairs left undecided; k_sspp_cbfix writes 0 or 1
         feasible[c] = (unsigned char)(s_feas[tid] == 0 ? 0 : (s_defer[tid] ? 2 : 1));
+    }
+    if (ctrl_out && a.ctrl_feas) {  // the rows a plan() returns: feasible (or undecided) only
+        double* dst = ctrl_out + cand0 * ndof;
+        for (int e = tid; e < nvalid * ndof; e += NT)
+            if (s_feas[e / ndof]) dst[e] = s_ctrl[e];
     }
     // block argmin over the workgroup's feasible candidates: one wave, lexicographic (cost, id)
     // xor butterfly (exact, order independent: the lowest id wins ties like the serial scan).
@@ -2295,6 +2301,7 @@ struct sspp_job {
     std::vector<double> h_knots;   // host copies: the knot vector, and the values the device
     std::vector<double> h_stage;   // holds (init | limits; sspp_job_update_sspp skips equal updates)
     std::vector<DPair> h_pairs, h_pairs_s;
+    int ctrl_feas = 0;               // k_sspp_c2f writes ctrl_out rows of feasible candidates only
     unsigned char* h_pin = nullptr;  // pinned source of sspp_job_update_sspp's async copies
     size_t h_pin_bytes = 0;
     hipEvent_t upd_ev = nullptr;     // recorded after those copies: the next update waits on it

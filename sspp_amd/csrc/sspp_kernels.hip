@@ -820,6 +820,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         c.arc_all = j->arc_all;
         c.hull = j->hull;
         c.dfr = j->d_dfr;
+        c.ctrl_feas = j->ctrl_feas;
         const int nb = nblk * steps;
         e = hipErrorInvalidValue;
         switch (j->D) {
@@ -997,6 +998,10 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_tsp launch");
     return SSPP_OK;
+}
+
+void sspp::job_set_ctrl_feasible_only(sspp_job* j, int on) {
+    if (j) j->ctrl_feas = on ? 1 : 0;
 }
 
 // CES slot-mode evaluation (ces.hip, tsp::Planner::plan eval loop): slots [slot0, slot0 + n)
