@@ -766,7 +766,10 @@ def main():
             "roofline_fp64": {"bound": "fp64_valu", "achieved": ach_exec, "peak": FP64_PEAK_TFLOPS,
                               "unit": "TFLOP/s", "frac": None if ach_exec is None else ach_exec / FP64_PEAK_TFLOPS,
                               "flops_per_candidate_executed": exec_per, "source": exec_src,
-                              "flops_per_candidate_charged": flops_per},
+                              "flops_per_candidate_charged": flops_per,
+                              # the same executed flops at the timed loop's rate (launches overlap)
+                              "steady_state_TFLOPs": None if exec_per is None else
+                              exec_per * value / 1e12 / max(1, world)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

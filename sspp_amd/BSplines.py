@@ -19,7 +19,8 @@ definition, so values agree with the reference bit for bit.  CasADi symbolic twi
 (casadiBspline & co., 138-208) need CasADi, which is not part of the scoring path; they raise
 ImportError when CasADi is absent.
 
-For batched scoring on the GPU use :func:`sspp_amd.batch.arc_lengths` / ``SsppJob``.
+For batched scoring on the GPU use ``sspp_amd.SsppJob`` (``sample_score`` / ``score_ctrl``)
+or the drop-in ``from sspp import _sspp`` planner.
 """
 from __future__ import annotations
 

@@ -78,7 +78,21 @@ def main(src, prefix):
                                    "launch / %d candidates" % (prefix, cfg, PER_LAUNCH[cfg])}
         occ = rows(os.path.join(d, "occ", "p1"), kern)
         if occ:
-            res["occupancy"] = per_launch(occ, {r["Counter_Name"] for r in occ})
+            o = per_launch(occ, {r["Counter_Name"] for r in occ})
+            res["occupancy"] = o
+            if o.get("GRBM_GUI_ACTIVE"):
+                # GRBM_GUI_ACTIVE is summed over the 8 XCDs (each counts the dispatch's busy
+                # cycles; the derived MeanOccupancyPerCU takes the max instead): per-XCD cycles
+                cyc = o["GRBM_GUI_ACTIVE"] / 8.0
+                res["dispatch_cycles"] = cyc
+                # a VALU wave-instruction holds its SIMD's issue for ~4 cycles (wave64, FP64 at
+                # 16 lanes per cycle): issue-slot utilisation per SIMD, 1024 SIMDs
+                res["valu_issue_per_simd"] = 4.0 * o["SQ_INSTS_VALU"] / (cyc * 1024)
+                # resident waves per CU averaged over the dispatch (SQ_WAVE_CYCLES: quad-cycles)
+                res["waves_per_cu_from_wave_cycles"] = 4.0 * o["SQ_WAVE_CYCLES"] / (cyc * 256)
+        occ2 = rows(os.path.join(d, "occ", "p2"), kern)
+        if occ2:
+            res["mean_occupancy_per_cu"] = per_launch(occ2, {r["Counter_Name"] for r in occ2}).get("MeanOccupancyPerCU")
         json.dump(res, open("%s_%s_pmc.json" % (prefix, cfg), "w"), indent=1, sort_keys=True)
         print(cfg, json.dumps(res, sort_keys=True)[:600])
     json.dump(traffic, open(tf, "w"), indent=1)
