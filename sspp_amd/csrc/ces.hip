@@ -190,15 +190,40 @@ __global__ __launch_bounds__(256) void k_ces_scatter(int nslots, const double* _
     rank[s] = 0;  // re-armed for the next update
 }
 
+// Pinned staging layout read by sspp_ces_read: [header, 64 B] [L | C_nf | C_wf | cost : n each]
+// [vias n*KD] [mean | sigma | last_best : KD each] (f64) [elites : cap] (i32) [status : n] (u8)
+constexpr size_t kStageHdr = 64;
+struct StageView {
+    double *L, *Cnf, *Cwf, *cost, *vias, *mean, *sigma, *lbest;
+    int* elites;
+    unsigned char* status;
+    CesHdr* hdr;
+};
+__host__ __device__ inline StageView stage_view(unsigned char* base, int n, int KD, int cap) {
+    StageView v;
+    v.hdr = (CesHdr*)base;
+    double* d = (double*)(base + kStageHdr);
+    v.L = d; v.Cnf = d + n; v.Cwf = d + 2 * (size_t)n; v.cost = d + 3 * (size_t)n;
+    v.vias = d + 4 * (size_t)n;
+    v.mean = v.vias + (size_t)n * KD; v.sigma = v.mean + KD; v.lbest = v.sigma + KD;
+    v.elites = (int*)(v.lbest + KD);
+    v.status = (unsigned char*)(v.elites + cap);
+    return v;
+}
+
 // Distribution::update + best pick + adapt on the ranked elites, one workgroup.  With
 // fused != 0 (n_slots <= kCesThreads: the ICRA-sized lists) the workgroup ranks the successes
 // itself, one slot per thread against every other slot in LDS, so an update is one launch
 // instead of rank + scatter + update.
+// stage != nullptr: the iteration's results also go straight into sspp_ces_read's pinned staging
+// (the values this workgroup writes, from registers; the per-slot results of the evaluation),
+// so reading it back needs no staging launch.
 __global__ __launch_bounds__(kCesThreads) void k_ces_update(
     CesK c, int fused, const unsigned char* __restrict__ status, const double* __restrict__ cost,
     const int* __restrict__ by_rank, int* nsucc_p, const double* __restrict__ vias,
     const double* __restrict__ LT, const double* __restrict__ LH, CesHdr* h, double* mean,
-    double* sigma, double* lbest, int* elite_out) {
+    double* sigma, double* lbest, int* elite_out, const double* __restrict__ Lsl,
+    const double* __restrict__ Cnfsl, const double* __restrict__ Cwfsl, unsigned char* stage) {
     __shared__ double s_wt[kEliteCap];
     __shared__ int s_idx[kEliteCap];
     __shared__ double s_red[4 * kCesWaves];
@@ -206,6 +231,16 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
     const int tid = threadIdx.x;
     const int K = c.K, KD = 4 * K;
     for (int e = tid; e < 2 * KD; e += kCesThreads) s_ms[e] = e < KD ? mean[e] : sigma[e - KD];
+    StageView sv{};
+    if (stage) {
+        const int n = c.nslots;
+        sv = stage_view(stage, n, KD, c.cap);
+        for (int e = tid; e < n; e += kCesThreads) {
+            sv.L[e] = Lsl[e]; sv.Cnf[e] = Cnfsl[e]; sv.Cwf[e] = Cwfsl[e]; sv.cost[e] = cost[e];
+            sv.status[e] = status[e];
+        }
+        for (int e = tid; e < n * KD; e += kCesThreads) sv.vias[e] = vias[e];
+    }
     int nsucc;
     if (fused) {
         unsigned long long* s_key = (unsigned long long*)s_wt;  // dead until the weights
@@ -226,8 +261,20 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
         nsucc = *nsucc_p;
     }
     if (nsucc == 0) {  // adapt(false)
-        if (tid < KD) sigma[tid] = clamp_sd(sigma[tid] * c.inc, c);
-        if (tid == 0) { h->nsucc = 0; h->nelite = 0; h->best_slot = -1; h->best_cost = INFINITY; h->iter++; }
+        if (tid < KD) {
+            const double sg = clamp_sd(sigma[tid] * c.inc, c);
+            sigma[tid] = sg;
+            if (stage) { sv.sigma[tid] = sg; sv.mean[tid] = mean[tid]; sv.lbest[tid] = lbest[tid]; }
+        }
+        if (tid == 0) {
+            h->nsucc = 0; h->nelite = 0; h->best_slot = -1; h->best_cost = INFINITY;
+            const long long it = h->iter + 1;
+            h->iter = it;
+            if (stage) {
+                CesHdr o = {h->nfixed, h->has_best, 0, 0, -1, INFINITY, it, 0};
+                *sv.hdr = o;
+            }
+        }
         return;
     }
     int k = (int)((double)nsucc * c.frac) < 1 ? 1 : (int)((double)nsucc * c.frac);
@@ -309,20 +356,33 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
             sg = clamp_sd(sg * c.dec, c);  // adapt(true)
             mean[4 * v + d] = nm[d];
             sigma[4 * v + d] = sg;
+            if (stage) { sv.mean[4 * v + d] = nm[d]; sv.sigma[4 * v + d] = sg; }
         }
     }
 
     // ---- best = first minimum in slot order (std::min_element): rank 0
     const int b = s_idx[0];
-    for (int e = tid; e < KD; e += kCesThreads) lbest[e] = vias[(long long)b * KD + e];
-    for (int j = tid; j < k; j += kCesThreads) elite_out[j] = s_idx[j];
+    for (int e = tid; e < KD; e += kCesThreads) {
+        const double x = vias[(long long)b * KD + e];
+        lbest[e] = x;
+        if (stage) sv.lbest[e] = x;
+    }
+    for (int j = tid; j < k; j += kCesThreads) {
+        elite_out[j] = s_idx[j];
+        if (stage) sv.elites[j] = s_idx[j];
+    }
     if (tid == 0) {
         h->has_best = 1;
         h->nsucc = nsucc;
         h->nelite = k;
         h->best_slot = b;
         h->best_cost = cost[b];
-        h->iter++;
+        const long long it = h->iter + 1;
+        h->iter = it;
+        if (stage) {
+            CesHdr o = {h->nfixed, 1, nsucc, k, (long long)b, cost[b], it, 0};
+            *sv.hdr = o;
+        }
     }
 }
 
@@ -364,7 +424,6 @@ __global__ __launch_bounds__(256) void k_ces_unpack(int n, int KD, const double*
 
 // sspp_ces_read's staging: header, per-slot results, distribution and elites written straight
 // into the planner's pinned host buffer (one launch, then one stream synchronisation)
-constexpr size_t kStageHdr = 64;
 __global__ __launch_bounds__(256) void k_ces_stage(int n, int KD, int cap, const CesHdr* __restrict__ h,
                                                    const double* L, const double* Cnf, const double* Cwf,
                                                    const double* cost, const double* vias, const double* mean,
@@ -431,6 +490,7 @@ struct sspp_ces {
     hipStream_t last = nullptr;         // stream of the last enqueued operation (sspp_ces_read waits on it)
     unsigned char* h_stage = nullptr;   // pinned: k_ces_stage's output
     size_t stage_bytes = 0;
+    long long staged_iter = -1;         // iteration whose results k_ces_update already staged
 };
 
 static CesK ces_k(const sspp_ces* p) {
@@ -573,6 +633,7 @@ int sspp_ces_begin(sspp_ces* p, const double* start, const double* end, int iter
         r.sigma0 = s;
     }
     p->last = (hipStream_t)stream;
+    p->staged_iter = -1;
     hipLaunchKernelGGL(k_ces_begin, dim3(1), dim3(128), 0, (hipStream_t)stream, ces_k(p), iterate ? 1 : 0,
                        r, p->d_hdr, p->d_mean, p->d_sigma, p->d_lbest, p->d_fixed);
     hipError_t e = hipGetLastError();
@@ -592,6 +653,7 @@ int sspp_ces_eval(sspp_ces* p, int rank, void* stream) {
     for (int i = 0; i < 4; ++i) { ev.start[i] = p->start[i]; ev.end[i] = p->end[i]; }
     const size_t o = (size_t)rank * p->spr;
     p->last = (hipStream_t)stream;
+    p->staged_iter = -1;
     return sspp::tsp_eval_ces(p->job, &ev, p->spr, p->d_L + o, p->d_Cnf + o, p->d_Cwf + o,
                               p->d_status + o, p->d_cost + o, p->d_vias + o * 4 * p->K, stream);
 }
@@ -609,12 +671,15 @@ int sspp_ces_update(sspp_ces* p, void* stream) {
         hipLaunchKernelGGL(k_ces_scatter, dim3(nt), dim3(256), 0, st, p->nslots, p->d_cost, p->d_status,
                            p->d_rank, p->d_by_rank);
     }
+    // small lists: the update also fills sspp_ces_read's pinned staging (no staging launch)
+    unsigned char* stage = fused ? p->h_stage : nullptr;
     hipLaunchKernelGGL(k_ces_update, dim3(1), dim3(kCesThreads), 0, st, ces_k(p), fused, p->d_status,
                        p->d_cost, p->d_by_rank, p->d_nsucc, p->d_vias, p->d_LT, p->d_LH, p->d_hdr, p->d_mean,
-                       p->d_sigma, p->d_lbest, p->d_elite);
+                       p->d_sigma, p->d_lbest, p->d_elite, p->d_L, p->d_Cnf, p->d_Cwf, stage);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "k_ces_update launch");
     p->iter++;
+    p->staged_iter = stage ? p->iter : -1;
     return SSPP_OK;
 }
 
@@ -651,6 +716,7 @@ int sspp_ces_unpack(sspp_ces* p, const double* d_in, void* stream) {
     const long long tot = (long long)p->nslots * (5 + KD);
     const int g = (int)std::min<long long>((tot + 255) / 256, 1024);
     p->last = (hipStream_t)stream;
+    p->staged_iter = -1;
     hipLaunchKernelGGL(k_ces_unpack, dim3(g), dim3(256), 0, (hipStream_t)stream, p->nslots, KD, d_in,
                        p->d_L, p->d_Cnf, p->d_Cwf, p->d_cost, p->d_status, p->d_vias);
     hipError_t e = hipGetLastError();
@@ -671,14 +737,18 @@ int sspp_ces_read(sspp_ces* p, sspp_ces_state* st, double* L, double* Cnf, doubl
                   int32_t* elites) {
     sspp::clear_error();
     if (!p || !st) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_read: null argument");
-    // one staging launch behind the planner's last operation, one wait on that stream
+    // one staging launch behind the planner's last operation (none when the last update staged
+    // its iteration itself), one wait on that stream
     const int n = p->nslots, KD = 4 * p->K;
-    const long long tot = 4LL * n + (long long)n * KD + 3LL * KD + p->cap + n;
-    const int g = (int)std::min<long long>((tot + 255) / 256, 256);
-    hipLaunchKernelGGL(k_ces_stage, dim3(g), dim3(256), 0, p->last, n, KD, p->cap, p->d_hdr, p->d_L,
-                       p->d_Cnf, p->d_Cwf, p->d_cost, p->d_vias, p->d_mean, p->d_sigma, p->d_lbest,
-                       p->d_elite, p->d_status, p->h_stage);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipSuccess;
+    if (p->staged_iter != p->iter) {
+        const long long tot = 4LL * n + (long long)n * KD + 3LL * KD + p->cap + n;
+        const int g = (int)std::min<long long>((tot + 255) / 256, 256);
+        hipLaunchKernelGGL(k_ces_stage, dim3(g), dim3(256), 0, p->last, n, KD, p->cap, p->d_hdr, p->d_L,
+                           p->d_Cnf, p->d_Cwf, p->d_cost, p->d_vias, p->d_mean, p->d_sigma, p->d_lbest,
+                           p->d_elite, p->d_status, p->h_stage);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(p->last);
     if (e != hipSuccess) return hip_err(e, "sspp_ces_read");
     CesHdr h;
@@ -710,6 +780,7 @@ int sspp_ces_set_state(sspp_ces* p, const double* mean, const double* sigma, con
                        int has_best) {
     sspp::clear_error();
     if (!p) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_set_state: null planner");
+    p->staged_iter = -1;  // the staged copy no longer matches the device state
     const size_t kd = (size_t)4 * p->K;
     hipError_t e;
     if ((mean && (e = hipMemcpy(p->d_mean, mean, 8 * kd, hipMemcpyHostToDevice)) != hipSuccess) ||

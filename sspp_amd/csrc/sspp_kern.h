@@ -573,9 +573,13 @@ __device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const doub
 //   the other waypoints give), or when *stop (the candidate's LDS flag, cleared by another
 //   wave of the same candidate) reads 0.  Returns 0 when no lane has a contact.
 // DEEP=true : returns 0, *cost = sum over deep contacts of -1/(center_dist + 1e-4) + static.
-template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true>
+// REC (DEEP only, pairs k < 64): instead of summing, record each deep pair's contact count and
+// cost term — rec_nd[k] = nd, rec_term[k] = -1/(centre distance + 1e-4) — so that pairs split
+// over several lanes can be summed afterwards in pair order (k_tsp_pp), bit-identical to the sum
+template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true, bool REC = false>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
-                             unsigned long long mask, double* cost, int* stop = nullptr) {
+                             unsigned long long mask, double* cost, int* stop = nullptr,
+                             unsigned char* rec_nd = nullptr, double* rec_term = nullptr) {
     static_assert(!ONEGEOM || NM == 1, "single moving geom implies a single mover");
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
@@ -644,10 +648,15 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
             const double cd = sqrt(dot3(dc, dc));
             const double term = -1.0 / (cd + 1e-4);
-            for (int i = 0; i < nd; ++i) acc = acc + term;
+            if (REC) {
+                rec_nd[k] = (unsigned char)nd;
+                rec_term[k] = term;
+            } else {
+                for (int i = 0; i < nd; ++i) acc = acc + term;
+            }
         }
     }
-    if (DEEP) *cost = acc + sc.static_cost;
+    if (DEEP && !REC) *cost = acc + sc.static_cost;
     return 0;
 }
 
@@ -2030,43 +2039,31 @@ __global__ __launch_bounds__(64, SSPP_WQ2_WAVES_PER_EU) void k_sspp_wq2(
 #ifndef SSPP_TSP_WAVES_PER_EU_CB  // with the exact cylinder-box test (its live state doubles)
 #define SSPP_TSP_WAVES_PER_EU_CB 2
 #endif
-// CB: the scene has cylinder-box pairs (without them the exact cylinder-box code is compiled
-// out: it costs registers even when it never runs)
-template <int NM, bool ONEGEOM, bool CB>
-__global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WAVES_PER_EU) void k_tsp(
-    TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
-    const double* __restrict__ Minv, const double* __restrict__ mean,
-    const double* __restrict__ sigma, const double* __restrict__ vias_in,
-    double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
-    double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
-    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int D = 4, P = 2, P1 = 3;
-    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, K = a.K, cp = a.cp;
-    const int slot = tid / lpc, lane = tid - slot * lpc;
-    const long long cand0 = (long long)blockIdx.x * cpb;
-    const int ndof = n * D;
-    double* s_V = smem;                      // [cpb][n][4]
-    double* s_ctrl = s_V + cpb * ndof;       // [cpb][n][4]
-    double* s_wsum = s_ctrl + cpb * ndof;    // [3][4]
-    double* s_best = s_wsum + 3 * (kBlock / 64);
-    int* s_stat = (int*)(s_best + 4);        // [cpb]
-
-    const long long nvalid = min((long long)cpb, a.B - cand0);
-    const long long nfx = a.ces ? (long long)*a.nfixed : 0;  // uniform: scalar load
-    for (int e = tid; e < cpb * 2 * D; e += kBlock) {
+// k_tsp's prologue, shared with k_tsp_pp: the candidates' via sets (given, CES fixed seeds or
+// Sampler::sample_set draws) into s_V [cpb][n][4], vias_out, then PathModel::fromVias into
+// s_ctrl [cpb][n][4].  Every thread of the workgroup calls it (it synchronises).
+__device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __restrict__ Minv,
+                                             const double* __restrict__ mean,
+                                             const double* __restrict__ sigma,
+                                             const double* __restrict__ vias_in,
+                                             double* __restrict__ vias_out, int tid, int nthr, int cpb,
+                                             long long cand0, long long nvalid, long long nfx,
+                                             double* s_V, double* s_ctrl) {
+    constexpr int D = 4;
+    const int n = a.n, K = a.K, ndof = n * D;
+    for (int e = tid; e < cpb * 2 * D; e += nthr) {
         const int s = e / (2 * D), r = e - s * 2 * D;
         if (r < D) s_V[s * ndof + r] = a.start[r];
         else s_V[s * ndof + (n - 1) * D + (r - D)] = a.end[r - D];
     }
     if (vias_in) {
-        for (int e = tid; e < nvalid * K * D; e += kBlock) {
+        for (int e = tid; e < nvalid * K * D; e += nthr) {
             const int s = e / (K * D), r = e - s * K * D;
             s_V[s * ndof + D + r] = vias_in[(cand0 + s) * K * D + r];
         }
     } else {
         // Sampler::sample_set (tsp_sampler.h:12-51) with Philox streams per (candidate, via, dim)
-        for (int e = tid; e < cpb * K * D; e += kBlock) {
+        for (int e = tid; e < cpb * K * D; e += nthr) {
             const int s = e / (K * D), r = e - s * K * D;
             if (s >= nvalid) continue;
             const int v = r / D, i = r - v * D;
@@ -2118,7 +2115,7 @@ __global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WA
     }
     __syncthreads();
     if (vias_out) {
-        for (int e = tid; e < nvalid * K * D; e += kBlock) {
+        for (int e = tid; e < nvalid * K * D; e += nthr) {
             const int s = e / (K * D), r = e - s * K * D;
             vias_out[(cand0 + s) * K * D + r] = s_V[s * ndof + D + r];
         }
@@ -2126,7 +2123,7 @@ __global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WA
     // PathModel::fromVias: SplineFitting::Interpolate's Householder QR solve, replayed from the
     // host-factored program (reflectors, |v|^2, R) in oracle qr_solve's operation order, one
     // lane per (candidate, dimension): control points bit-identical to the oracle's
-    for (int e = tid; e < cpb * D; e += kBlock) {
+    for (int e = tid; e < cpb * D; e += nthr) {
         const int s = e / D, d = e - s * D;
         const double* Vs = s_V + s * ndof;
         double* c = s_ctrl + s * ndof;
@@ -2149,6 +2146,34 @@ __global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WA
         }
     }
     __syncthreads();
+
+}
+
+// CB: the scene has cylinder-box pairs (without them the exact cylinder-box code is compiled
+// out: it costs registers even when it never runs)
+template <int NM, bool ONEGEOM, bool CB>
+__global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WAVES_PER_EU) void k_tsp(
+    TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ Minv, const double* __restrict__ mean,
+    const double* __restrict__ sigma, const double* __restrict__ vias_in,
+    double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
+    double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int D = 4, P = 2, P1 = 3;
+    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, cp = a.cp;
+    const int slot = tid / lpc, lane = tid - slot * lpc;
+    const long long cand0 = (long long)blockIdx.x * cpb;
+    const int ndof = n * D;
+    double* s_V = smem;                      // [cpb][n][4]
+    double* s_ctrl = s_V + cpb * ndof;       // [cpb][n][4]
+    double* s_wsum = s_ctrl + cpb * ndof;    // [3][4]
+    double* s_best = s_wsum + 3 * (kBlock / 64);
+    int* s_stat = (int*)(s_best + 4);        // [cpb]
+
+    const long long nvalid = min((long long)cpb, a.B - cand0);
+    const long long nfx = a.ces ? (long long)*a.nfixed : 0;  // uniform: scalar load
+    tsp_prologue(a, Minv, mean, sigma, vias_in, vias_out, tid, kBlock, cpb, cand0, nvalid, nfx, s_V, s_ctrl);
 
     // Evaluator::eval_one_pass (tsp_evaluator.h:18-32), waypoint i = 1..cp per lane
     const bool valid = slot < nvalid;
@@ -2224,8 +2249,106 @@ __global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WA
     finish_batch(bb, part, sync, best);
 }
 
+// ---------------------------------------------------------------- TaskSpacePlanner, pair-split
+// Latency form of k_tsp for small batches (the anytime CES loop: 17 slots x 40 check points):
+// one workgroup per candidate, G waves; wave g evaluates the pairs k = g, g + G, ... of the
+// candidate's (<= 64) waypoints, one waypoint per lane, so a lane runs ~np/G pair tests instead
+// of np.  Deep pairs are recorded per (waypoint, pair) in LDS; wave 0 then sums each waypoint's
+// terms in pair order and runs k_tsp's epilogue (same lanes, shuffles and reductions), so every
+// output is bit-identical to k_tsp's.  Needs cp <= 64 and np <= 64 (host check).
+template <int NM, bool ONEGEOM, bool CB, int G>
+__global__ __launch_bounds__(64 * G, 2) void k_tsp_pp(
+    TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ Minv, const double* __restrict__ mean,
+    const double* __restrict__ sigma, const double* __restrict__ vias_in,
+    double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
+    double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int D = 4, P = 2, P1 = 3, NT = 64 * G;
+    const int tid = threadIdx.x, n = a.n, cp = a.cp, np = a.sc.npairs;
+    const int g = tid >> 6, lane = tid & 63;
+    const long long cand0 = blockIdx.x;
+    const int ndof = n * D;
+    double* s_V = smem;                       // [n][4]
+    double* s_ctrl = s_V + ndof;              // [n][4]
+    double* s_term = s_ctrl + ndof;           // [64 waypoints][64 pairs]
+    unsigned char* s_nd = (unsigned char*)(s_term + 64 * 64);  // [64][64]
+    const long long nvalid = 1;
+    const long long nfx = a.ces ? (long long)*a.nfixed : 0;
+    for (int e = tid; e < 64 * 64 / 4; e += NT) ((unsigned*)s_nd)[e] = 0u;
+    tsp_prologue(a, Minv, mean, sigma, vias_in, vias_out, tid, NT, 1, cand0, nvalid, nfx, s_V, s_ctrl);
+    const unsigned long long mask = hull_mask<D, NM, 1>(s_ctrl, n, np, (cpair_t)T.pairs,
+                                                        (cgeom_t)T.geoms, (cmover_t)T.movers);
+    // this wave's pairs: k = g (mod G)
+    unsigned long long gm = 0ull;
+    for (int k = g; k < 64; k += G) gm |= 1ull << k;
+    const int i = lane + 1;  // waypoint
+    double pc[4];
+    if (lane < cp) {
+        eval_pt<D, P>(s_ctrl, tab + i * P1, span[i], pc);
+#ifndef SSPP_PROF_NOCOLL
+        if (mask & gm)
+            point_collide<D, NM, 1, true, ONEGEOM, CB, true>(pc, a.sc, T, mask & gm, nullptr, nullptr,
+                                                             s_nd + lane * 64, s_term + lane * 64);
+#endif
+    }
+    __syncthreads();
+    // ---- wave 0: k_tsp's per-lane waypoint epilogue (lpc = 64, one waypoint per lane)
+    double aL = 0.0, aC = 0.0, aW = 0.0;
+    BlockBest bb;
+    if (g == 0) {
+        double pv[4];
+        if (lane < cp) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) pv[d] = pc[d];
+        }
+        // s((i-1)du) is the previous lane's s(i du), as in k_tsp's one-pass form
+#pragma unroll
+        for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pv[d], 1, 64);
+        if (lane < cp) {
+            if (lane == 0) eval_pt<D, P>(s_ctrl, tab + (i - 1) * P1, span[i - 1], pv);
+            aL = aL + dist_nd<D>(pv, pc);
+            double acc = 0.0;
+            const unsigned char* rn = s_nd + lane * 64;
+            const double* rt = s_term + lane * 64;
+            for (int k = 0; k < np; ++k) {
+                const int nd = rn[k];
+                if (nd == 0) continue;
+                const double term = rt[k];
+                for (int r = 0; r < nd; ++r) acc = acc + term;
+            }
+            const double c = acc + a.sc.static_cost;
+            const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
+            const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
+            aC = aC + c;
+            aW = aW + (c + fp);
+        }
+    }
+    if (g == 0) {
+        aL = wave_sum(aL);
+        aC = wave_sum(aC);
+        aW = wave_sum(aW);
+    }
+    if (tid == 0) {
+        double L = aL, Cn = aC, Cw = aW;
+        int st = Cn == 0.0;
+        double cost = L + a.w_col * Cw;
+        if (a.ces && a.slot0 + cand0 >= nfx + a.samples) {  // padding slot
+            st = 0; cost = INFINITY; L = 0.0; Cn = 0.0; Cw = 0.0;
+        }
+        oL[cand0] = L; oCnf[cand0] = Cn; oCwf[cand0] = Cw; ocost[cand0] = cost;
+        ostatus[cand0] = (unsigned char)st;
+        bb.cost = st ? cost : INFINITY; bb.idx = st ? a.first_id + cand0 : -1; bb.count = st; bb.pad = 0;
+    }
+    finish_batch<NT>(bb, part, sync, best);
+}
+
 // ---------------------------------------------------------------- argmin over block results
 
+
+// TaskSpacePlanner batches up to this size take k_tsp_pp (one workgroup per candidate)
+constexpr int64_t kTspPpMaxBatch = 512;
 
 inline int lanes_for(int items) {
     int l = ((items + 63) / 64) * 64;
@@ -2288,8 +2411,8 @@ struct sspp_job {
     unsigned* d_dfr = nullptr;     // k_sspp_c2f -> k_sspp_cbfix counters (SsppC2F::dfr)
     int has_cb = 0;                // the pair table has cylinder-box pairs (k_sspp_cbfix runs)
     int sampler = 0;               // 0 FP64 Box-Muller pairs (default), 1 FP32 quads (opt-in)
-    // work-queue kernel (k_sspp_wq, the default: SSPP_KERNEL=2)
-    int wq = 1;
+    // two-kernel work queue (k_sspp_wq1/2, SSPP_KERNEL=2; measured, not the default)
+    int wq = 0;
     WqCtr* d_wctr = nullptr;       // launch counters
     WqStep* d_wstp = nullptr;      // per-step decision counters [kMaxSteps]
     WqSurv* d_wsurv = nullptr;     // survivor records [wq_cap]
@@ -2504,8 +2627,22 @@ hipError_t entry_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs& o, int 
 template <int Unused>
 hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* mean, const double* sigma,
                      const double* d_vias, double* d_vias_out, double* d_L, double* d_Cnf, double* d_Cwf,
-                     double* d_cost, uint8_t* d_status, sspp_best* d_best, hipStream_t st) {
+                     double* d_cost, uint8_t* d_status, sspp_best* d_best, hipStream_t st, int pp) {
     const SceneT tt = scene_t(j->scene);
+    if (pp) {  // k_tsp_pp: one 8-wave workgroup per candidate (cp <= 64, npairs <= 64)
+        const size_t lds = sizeof(double) * ((size_t)2 * j->n * 4 + 64 * 64) + 64 * 64;
+#define SSPP_LAUNCH_TSPPP(OG, CBV)                                                                       \
+        hipLaunchKernelGGL((k_tsp_pp<1, OG, CBV, 8>), dim3(nblk), dim3(512), lds, st, k, tt, j->d_tab,   \
+                           j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
+                           d_status, j->d_part, j->d_sync, d_best)
+        const bool og = k.sc.onegeom && k.sc.npairs > 0;
+        if (og && k.sc.cylbox) SSPP_LAUNCH_TSPPP(true, true);
+        else if (og) SSPP_LAUNCH_TSPPP(true, false);
+        else if (k.sc.cylbox) SSPP_LAUNCH_TSPPP(false, true);
+        else SSPP_LAUNCH_TSPPP(false, false);
+#undef SSPP_LAUNCH_TSPPP
+        return hipGetLastError();
+    }
 #define SSPP_LAUNCH_TSP(OG, CBV)                                                                   \
     hipLaunchKernelGGL((k_tsp<1, OG, CBV>), dim3(nblk), dim3(kBlock), j->lds, st, k, tt, j->d_tab, \
                        j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
@@ -2526,6 +2663,6 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
 #define SSPK_TSP_DECL(X)                                                                                  \
     X template hipError_t entry_tsp<0>(const TspK&, const sspp_job*, int, const double*, const double*,    \
                                        const double*, double*, double*, double*, double*, double*, uint8_t*, \
-                                       sspp_best*, hipStream_t);
+                                       sspp_best*, hipStream_t, int);
 
 }  // namespace sspk

@@ -954,7 +954,10 @@ extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args*
         sspp_job_free(j);
         return rc;
     }
-    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nblk) != hipSuccess ||
+    // one record per workgroup: k_tsp's blocks, or one per candidate for k_tsp_pp
+    const int64_t nrec = std::max<int64_t>(nblk, std::min<int64_t>(max_batch, kTspPpMaxBatch));
+    j->part_cap = nrec;
+    if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nrec) != hipSuccess ||
         hipMalloc((void**)&j->d_sync, sizeof(ArgminSync)) != hipSuccess ||
         hipMemset(j->d_sync, 0, sizeof(ArgminSync)) != hipSuccess) {
         sspp_job_free(j);
@@ -990,10 +993,15 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
         mean = ces->mean; sigma = ces->sigma;
         for (int i = 0; i < 4; ++i) { k.start[i] = ces->start[i]; k.end[i] = ces->end[i]; }
     }
-    const int nblk = (int)((B + j->cpb - 1) / j->cpb);
+    // small batches (the anytime CES loop) take the pair-split kernel: one workgroup per
+    // candidate, the scene's pairs spread over 8 waves (same outputs, bit for bit)
+    static const int pp_env = getenv("SSPP_TSP_PP") ? atoi(getenv("SSPP_TSP_PP")) : -1;
+    const bool pp_ok = j->cp <= 64 && k.sc.npairs <= 64 && B <= j->part_cap;
+    const bool pp = pp_ok && (pp_env < 0 ? B <= kTspPpMaxBatch : pp_env > 0);
+    const int nblk = pp ? (int)B : (int)((B + j->cpb - 1) / j->cpb);
     hipStream_t st = (hipStream_t)stream;
     hipError_t e0 = entry_tsp<0>(k, j, nblk, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, d_status,
-                                 d_best, st);
+                                 d_best, st, pp ? 1 : 0);
     if (e0 != hipSuccess) return hip_fail(e0, "k_tsp launch");
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_tsp launch");
