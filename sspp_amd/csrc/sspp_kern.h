@@ -233,6 +233,12 @@ struct TspK {
     const double* fixed;    // [2][K][4]
     const int* nfixed;
     long long slot0, samples;
+    // k_tsp_pp2 (several workgroups per candidate): per-candidate deep-pair records and
+    // arrival counters
+    unsigned* rec_nd;       // [B][64 waypoints][64 pairs]
+    double* rec_term;       // [B][64][64]
+    unsigned* arrive;       // [B], zero between launches (the last arriver re-arms it)
+    int npg;                // workgroups per candidate
 };
 
 // ---------------------------------------------------------------- Philox4x32-10 + Box-Muller
@@ -575,11 +581,13 @@ __device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const doub
 // DEEP=true : returns 0, *cost = sum over deep contacts of -1/(center_dist + 1e-4) + static.
 // REC (DEEP only, pairs k < 64): instead of summing, record each deep pair's contact count and
 // cost term — rec_nd[k] = nd, rec_term[k] = -1/(centre distance + 1e-4) — so that pairs split
-// over several lanes can be summed afterwards in pair order (k_tsp_pp), bit-identical to the sum
-template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true, bool REC = false>
+// over several lanes can be summed afterwards in pair order, bit-identical to the sum.  REC 1:
+// rec_nd is unsigned char (LDS, k_tsp_pp); REC 2: rec_nd is unsigned and both are written with
+// write-through agent-scope stores (another workgroup reads them, k_tsp_pp2).
+template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true, int REC = 0>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                              unsigned long long mask, double* cost, int* stop = nullptr,
-                             unsigned char* rec_nd = nullptr, double* rec_term = nullptr) {
+                             void* rec_nd = nullptr, double* rec_term = nullptr) {
     static_assert(!ONEGEOM || NM == 1, "single moving geom implies a single mover");
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
@@ -648,15 +656,19 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
             const double cd = sqrt(dot3(dc, dc));
             const double term = -1.0 / (cd + 1e-4);
-            if (REC) {
-                rec_nd[k] = (unsigned char)nd;
+            if (REC == 1) {
+                ((unsigned char*)rec_nd)[k] = (unsigned char)nd;
                 rec_term[k] = term;
+            } else if (REC == 2) {
+                __hip_atomic_store((unsigned*)rec_nd + k, (unsigned)nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned long long*)rec_term + k, (unsigned long long)__double_as_longlong(term),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 for (int i = 0; i < nd; ++i) acc = acc + term;
             }
         }
     }
-    if (DEEP && !REC) *cost = acc + sc.static_cost;
+    if (DEEP && REC == 0) *cost = acc + sc.static_cost;
     return 0;
 }
 
@@ -2289,8 +2301,8 @@ __global__ __launch_bounds__(64 * G, 2) void k_tsp_pp(
         eval_pt<D, P>(s_ctrl, tab + i * P1, span[i], pc);
 #ifndef SSPP_PROF_NOCOLL
         if (mask & gm)
-            point_collide<D, NM, 1, true, ONEGEOM, CB, true>(pc, a.sc, T, mask & gm, nullptr, nullptr,
-                                                             s_nd + lane * 64, s_term + lane * 64);
+            point_collide<D, NM, 1, true, ONEGEOM, CB, 1>(pc, a.sc, T, mask & gm, nullptr, nullptr,
+                                                          s_nd + lane * 64, s_term + lane * 64);
 #endif
     }
     __syncthreads();
@@ -2342,6 +2354,106 @@ __global__ __launch_bounds__(64 * G, 2) void k_tsp_pp(
         bb.cost = st ? cost : INFINITY; bb.idx = st ? a.first_id + cand0 : -1; bb.count = st; bb.pad = 0;
     }
     finish_batch<NT>(bb, part, sync, best);
+}
+
+// k_tsp_pp over npg workgroups per candidate: workgroup (cand, pg) evaluates pair group
+// pg * G + g (pairs k = that group mod npg * G) on its waves, one waypoint per lane, and stores
+// every (waypoint, pair) of its groups — contact count (0 when not deep) and term — as
+// write-through agent-scope stores; its last arriving workgroup (agent-scope acquire) sums each
+// waypoint in pair order and runs the epilogue.  Same outputs as k_tsp, bit for bit.
+template <int NM, bool ONEGEOM, bool CB, int G>
+__global__ __launch_bounds__(64 * G, 2) void k_tsp_pp2(
+    TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ Minv, const double* __restrict__ mean,
+    const double* __restrict__ sigma, const double* __restrict__ vias_in,
+    double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
+    double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int D = 4, P = 2, P1 = 3, NT = 64 * G;
+    __shared__ int s_last;
+    const int tid = threadIdx.x, n = a.n, cp = a.cp, np = a.sc.npairs, npg = a.npg;
+    const int g = tid >> 6, lane = tid & 63;
+    const long long cand0 = blockIdx.x / npg;
+    const int pg = blockIdx.x - (int)cand0 * npg;
+    const int ngr = npg * G, gg = pg * G + g;  // pair groups in all, this wave's group
+    const int ndof = n * D;
+    double* s_V = smem;           // [n][4]
+    double* s_ctrl = s_V + ndof;  // [n][4]
+    const long long nfx = a.ces ? (long long)*a.nfixed : 0;
+    tsp_prologue(a, Minv, mean, sigma, vias_in, pg == 0 ? vias_out : nullptr, tid, NT, 1, cand0, 1, nfx,
+                 s_V, s_ctrl);
+    const unsigned long long mask = hull_mask<D, NM, 1>(s_ctrl, n, np, (cpair_t)T.pairs,
+                                                        (cgeom_t)T.geoms, (cmover_t)T.movers);
+    unsigned long long gm = 0ull;
+    for (int k = gg; k < np; k += ngr) gm |= 1ull << k;
+    const int i = lane + 1;
+    unsigned* rn = a.rec_nd + (cand0 * 64 + lane) * 64;
+    double* rt = a.rec_term + (cand0 * 64 + lane) * 64;
+    if (lane < cp && gm) {
+        double pc[4];
+        eval_pt<D, P>(s_ctrl, tab + i * P1, span[i], pc);
+        // this lane's groups' entries: 0 unless the pair is deep (then count and term)
+        for (int k = gg; k < np; k += ngr) __hip_atomic_store(rn + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef SSPP_PROF_NOCOLL
+        if (mask & gm)
+            point_collide<D, NM, 1, true, ONEGEOM, CB, 2>(pc, a.sc, T, mask & gm, nullptr, nullptr, rn, rt);
+#endif
+    }
+    // publish: every storing wave drains, the workgroup meets, one lane counts the arrival
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.arrive + cand0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == (unsigned)npg - 1u;
+        if (s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(a.arrive + cand0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (!s_last) return;
+    double aL = 0.0, aC = 0.0, aW = 0.0;
+    BlockBest bb;
+    if (g == 0) {
+        double pc[4], pv[4];
+        if (lane < cp) eval_pt<D, P>(s_ctrl, tab + i * P1, span[i], pc);
+#pragma unroll
+        for (int d = 0; d < D; ++d) pv[d] = __shfl_up(lane < cp ? pc[d] : 0.0, 1, 64);
+        if (lane < cp) {
+            if (lane == 0) eval_pt<D, P>(s_ctrl, tab + (i - 1) * P1, span[i - 1], pv);
+            aL = aL + dist_nd<D>(pv, pc);
+            double acc = 0.0;
+            for (int k = 0; k < np; ++k) {
+                if (!((mask >> k) & 1ull)) continue;  // culled pairs were never evaluated
+                const unsigned nd = __hip_atomic_load(rn + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (nd == 0u) continue;
+                const double term = __hip_atomic_load(rt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (unsigned r = 0; r < nd; ++r) acc = acc + term;
+            }
+            const double c = acc + a.sc.static_cost;
+            const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
+            const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
+            aC = aC + c;
+            aW = aW + (c + fp);
+        }
+        aL = wave_sum(aL);
+        aC = wave_sum(aC);
+        aW = wave_sum(aW);
+    }
+    if (tid == 0) {
+        double L = aL, Cn = aC, Cw = aW;
+        int st = Cn == 0.0;
+        double cost = L + a.w_col * Cw;
+        if (a.ces && a.slot0 + cand0 >= nfx + a.samples) {  // padding slot
+            st = 0; cost = INFINITY; L = 0.0; Cn = 0.0; Cw = 0.0;
+        }
+        oL[cand0] = L; oCnf[cand0] = Cn; oCwf[cand0] = Cw; ocost[cand0] = cost;
+        ostatus[cand0] = (unsigned char)st;
+        bb.cost = st ? cost : INFINITY; bb.idx = st ? a.first_id + cand0 : -1; bb.count = st; bb.pad = 0;
+    }
+    finish_batch<NT>(bb, part, sync, best, (int)a.B, (int)cand0);
 }
 
 // ---------------------------------------------------------------- argmin over block results
@@ -2425,6 +2537,10 @@ struct sspp_job {
     std::vector<double> h_stage;   // holds (init | limits; sspp_job_update_sspp skips equal updates)
     std::vector<DPair> h_pairs, h_pairs_s;
     int ctrl_feas = 0;               // k_sspp_c2f writes ctrl_out rows of feasible candidates only
+    unsigned* d_pp_nd = nullptr;     // k_tsp_pp2 records / arrival counters (allocated on first use)
+    double* d_pp_term = nullptr;
+    unsigned* d_pp_arrive = nullptr;
+    int64_t pp_cap = 0;
     unsigned char* h_pin = nullptr;  // pinned source of sspp_job_update_sspp's async copies
     size_t h_pin_bytes = 0;
     hipEvent_t upd_ev = nullptr;     // recorded after those copies: the next update waits on it
@@ -2629,6 +2745,20 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
                      const double* d_vias, double* d_vias_out, double* d_L, double* d_Cnf, double* d_Cwf,
                      double* d_cost, uint8_t* d_status, sspp_best* d_best, hipStream_t st, int pp) {
     const SceneT tt = scene_t(j->scene);
+    if (pp == 2) {  // k_tsp_pp2: k.npg 8-wave workgroups per candidate (nblk = B * npg)
+        const size_t lds = sizeof(double) * (size_t)2 * j->n * 4;
+#define SSPP_LAUNCH_TSPPP2(OG, CBV)                                                                       \
+        hipLaunchKernelGGL((k_tsp_pp2<1, OG, CBV, 8>), dim3(nblk), dim3(512), lds, st, k, tt, j->d_tab,   \
+                           j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
+                           d_status, j->d_part, j->d_sync, d_best)
+        const bool og = k.sc.onegeom && k.sc.npairs > 0;
+        if (og && k.sc.cylbox) SSPP_LAUNCH_TSPPP2(true, true);
+        else if (og) SSPP_LAUNCH_TSPPP2(true, false);
+        else if (k.sc.cylbox) SSPP_LAUNCH_TSPPP2(false, true);
+        else SSPP_LAUNCH_TSPPP2(false, false);
+#undef SSPP_LAUNCH_TSPPP2
+        return hipGetLastError();
+    }
     if (pp) {  // k_tsp_pp: one 8-wave workgroup per candidate (cp <= 64, npairs <= 64)
         const size_t lds = sizeof(double) * ((size_t)2 * j->n * 4 + 64 * 64) + 64 * 64;
 #define SSPP_LAUNCH_TSPPP(OG, CBV)                                                                       \

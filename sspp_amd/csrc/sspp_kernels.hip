@@ -995,13 +995,33 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     }
     // small batches (the anytime CES loop) take the pair-split kernel: one workgroup per
     // candidate, the scene's pairs spread over 8 waves (same outputs, bit for bit)
-    static const int pp_env = getenv("SSPP_TSP_PP") ? atoi(getenv("SSPP_TSP_PP")) : -1;
+    // and, with more than 8 pairs, ceil(npairs / 8) workgroups per candidate (k_tsp_pp2).
+    // SSPP_TSP_PP: 0 never, 1 single-workgroup form only, 2 the multi-workgroup form when it applies
+    const char* pp_s = getenv("SSPP_TSP_PP");
+    const int pp_env = pp_s ? atoi(pp_s) : -1;
     const bool pp_ok = j->cp <= 64 && k.sc.npairs <= 64 && B <= j->part_cap;
     const bool pp = pp_ok && (pp_env < 0 ? B <= kTspPpMaxBatch : pp_env > 0);
-    const int nblk = pp ? (int)B : (int)((B + j->cpb - 1) / j->cpb);
+    const int npg = (k.sc.npairs + 7) / 8;
+    int mode = pp ? 1 : 0;
+    if (pp && npg > 1 && pp_env != 1 && B <= kTspPpMaxBatch) {
+        if (!j->d_pp_arrive) {
+            const int64_t cap = std::min<int64_t>(j->max_batch, kTspPpMaxBatch);
+            if (hipMalloc((void**)&j->d_pp_nd, sizeof(unsigned) * 4096 * (size_t)cap) != hipSuccess ||
+                hipMalloc((void**)&j->d_pp_term, sizeof(double) * 4096 * (size_t)cap) != hipSuccess ||
+                hipMalloc((void**)&j->d_pp_arrive, sizeof(unsigned) * (size_t)cap) != hipSuccess ||
+                hipMemset(j->d_pp_arrive, 0, sizeof(unsigned) * (size_t)cap) != hipSuccess)
+                return sspp::set_error(SSPP_E_NOMEM, "hipMalloc k_tsp_pp2 records");
+            j->pp_cap = cap;
+        }
+        if (B <= j->pp_cap) {
+            mode = 2;
+            k.rec_nd = j->d_pp_nd; k.rec_term = j->d_pp_term; k.arrive = j->d_pp_arrive; k.npg = npg;
+        }
+    }
+    const int nblk = mode == 2 ? (int)B * npg : mode == 1 ? (int)B : (int)((B + j->cpb - 1) / j->cpb);
     hipStream_t st = (hipStream_t)stream;
     hipError_t e0 = entry_tsp<0>(k, j, nblk, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, d_status,
-                                 d_best, st, pp ? 1 : 0);
+                                 d_best, st, mode);
     if (e0 != hipSuccess) return hip_fail(e0, "k_tsp launch");
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_tsp launch");
@@ -1064,6 +1084,8 @@ extern "C" void sspp_job_free(sspp_job* j) {
     if (j->d_wspert) (void)hipFree(j->d_wspert);
     if (j->d_wqueue) (void)hipFree(j->d_wqueue);
     if (j->d_wlist) (void)hipFree(j->d_wlist);
+    for (void* q : {(void*)j->d_pp_nd, (void*)j->d_pp_term, (void*)j->d_pp_arrive})
+        if (q) (void)hipFree(q);
     if (j->upd_ev) {
         (void)hipEventSynchronize(j->upd_ev);
         (void)hipEventDestroy(j->upd_ev);

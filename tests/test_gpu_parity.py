@@ -502,3 +502,46 @@ def test_gripper_tsp_matches_oracle(cuda, goal):
         assert np.abs(_np(a) - b).max() <= 1e-9
     assert 0 < st.sum() < B  # both outcomes present
     assert S.decode_best(out["best"])[1] == O.tsp_best(cost, st)[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xml,body,B,cp", [("robocrane.xml", "gripper_collision_with_block/", 17, 40),
+                                           ("robocrane.xml", "gripper_collision_with_block/", 300, 64),
+                                           ("stacking.xml", "block1", 200, 48)])
+def test_tsp_kernel_forms_identical(cuda, monkeypatch, xml, body, B, cp):
+    """k_tsp, the single-workgroup pair split (k_tsp_pp) and the multi-workgroup split (k_tsp_pp2,
+    48 gripper pairs over 6 workgroups per candidate) give bit-identical per-candidate results and
+    argmin records, and match the oracle."""
+    import torch
+    import sspp_amd as S
+    path = os.path.join(SCENES, xml)
+    model = S.Model(path)
+    bid = model.body_id(body)
+    scene = S.Scene(model, 1, bid)
+    if xml == "robocrane.xml":
+        start, end = np.array([0.5, 0.15, 0.156, 1.5708]), np.array([0.5, -0.05, 0.156, 1.5708])
+        lo, hi = (0.0, -0.7, 0.1, -1.6), (0.7, 0.7, 0.6, 1.6)
+    else:
+        start = model.body_point("block1") + np.array([0, 0, 0.02, 0])
+        end = model.body_point("block2") + np.array([0, 0, 0.22, 0])
+        lo, hi = (-0.5, -0.5, 0.0, -1.6), (0.5, 0.5, 0.6, 1.6)
+    mean = (start + 0.5 * (end - start)).reshape(1, 4)
+    sigma = np.full((1, 4), 0.15)
+    job = S.TspJob(scene, start, end, 1, cp, mean=mean, sigma=sigma, lo=np.array(lo), hi=np.array(hi),
+                   z_min=0.0, max_batch=B)
+    res = {}
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("SSPP_TSP_PP", mode)
+        q = job.alloc(B, device="cuda", with_vias=True)
+        job.sample_score(0, B, q["L"], q["Cnf"], q["Cwf"], q["status"], q["cost"], q["best"],
+                         vias_out=q["vias"])
+        torch.cuda.synchronize()
+        res[mode] = {k: v.cpu().numpy() for k, v in q.items()}
+    for mode in ("1", "2"):
+        for k in ("L", "Cnf", "Cwf", "cost", "status", "vias", "best"):
+            np.testing.assert_array_equal(res[mode][k], res["0"][k], err_msg="%s %s" % (mode, k))
+    osc = O.Scene(mjcf_ref.load(path), 1, bid)
+    L, Cnf, Cwf, st, cost = O.tsp_score(osc, start, end, res["0"]["vias"], cp)
+    np.testing.assert_array_equal(res["0"]["status"], st)
+    fin = np.isfinite(cost)
+    assert (np.abs(res["0"]["cost"][fin] - cost[fin]) <= 1e-12 * np.maximum(1.0, np.abs(cost[fin]))).all()
