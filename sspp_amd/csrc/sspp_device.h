@@ -493,6 +493,83 @@ SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double*
     return bb_clip_count(pa, ma, ea, pb, mb, eb, fi);
 }
 
+// box_box_deep_count for two UPRIGHT boxes: each rotation has m[2] = m[5] = m[6] = m[7] = 0
+// exactly (z axis = world z up to its sign and length, x / y axes horizontal), which holds for a
+// yaw-only mover (TaskSpacePlanner, utility.h:198-206) against z-aligned static boxes.  Then
+// R = A^T B has R02 = R12 = R20 = R21 = 0 exactly and every product with those zeros drops out
+// of box_box_deep_count's fma chains without changing any other rounding (adding an exact zero
+// is exact), so this returns bit for bit what box_box_deep_count returns on such boxes, with a
+// quarter of the SAT arithmetic: the 8 non-degenerate edge axes are z (4), A's and B's
+// horizontal axes (2 + 2); the ninth (A_z x B_z) has length 0 and is skipped there too.
+SSPP_HD int box_box_deep_count_up(const double* pa, const double* ma, const double* ea,
+                                  const double* pb, const double* mb, const double* eb) {
+    const double T0 = pb[0] - pa[0], T1 = pb[1] - pa[1], T2 = pb[2] - pa[2];
+    const double t0 = fma(ma[3], T1, ma[0] * T0), t1 = fma(ma[4], T1, ma[1] * T0), t2 = ma[8] * T2;
+    const double R00 = fma(ma[3], mb[3], ma[0] * mb[0]), R01 = fma(ma[3], mb[4], ma[0] * mb[1]);
+    const double R10 = fma(ma[4], mb[3], ma[1] * mb[0]), R11 = fma(ma[4], mb[4], ma[1] * mb[1]);
+    const double R22 = ma[8] * mb[8];
+    const double A00 = fabs(R00), A01 = fabs(R01), A10 = fabs(R10), A11 = fabs(R11), A22 = fabs(R22);
+    double best_face, sep;
+    int fi;
+    // faces of A
+    sep = fabs(t0) - (ea[0] + fma(eb[1], A01, eb[0] * A00));
+    if (sep >= kDeep) return 0;
+    best_face = sep; fi = 0;
+    sep = fabs(t1) - (ea[1] + fma(eb[1], A11, eb[0] * A10));
+    if (sep >= kDeep) return 0;
+    if (sep > best_face) { best_face = sep; fi = 1; }
+    sep = fabs(t2) - (ea[2] + eb[2] * A22);
+    if (sep >= kDeep) return 0;
+    if (sep > best_face) { best_face = sep; fi = 2; }
+    // faces of B
+    sep = fabs(fma(t1, R10, t0 * R00)) - (fma(ea[1], A10, ea[0] * A00) + eb[0]);
+    if (sep >= kDeep) return 0;
+    if (sep > best_face) { best_face = sep; fi = 3; }
+    sep = fabs(fma(t1, R11, t0 * R01)) - (fma(ea[1], A11, ea[0] * A01) + eb[1]);
+    if (sep >= kDeep) return 0;
+    if (sep > best_face) { best_face = sep; fi = 4; }
+    sep = fabs(t2 * R22) - (ea[2] * A22 + eb[2]);
+    if (sep >= kDeep) return 0;
+    if (sep > best_face) { best_face = sep; fi = 5; }
+    bool edge = false;
+    const double fthr = best_face + 1e-12;
+    // one edge axis: separation numerator num against thr * |L|, len2 = |L|^2 as formed there
+    auto ax = [&](double len2, double pr, double ra, double rb) -> int {
+        if (len2 < 1e-12) return 1;
+        const double num = pr - (ra + rb), len = sqrt(len2);
+        if (num >= kDeep * len) return 0;
+        edge = edge || num > fthr * len;
+        return 1;
+    };
+    // (i, j) = (0, 0), (0, 1): L = (0, -0, R1j), along z
+    if (!ax(R10 * R10, fabs(t2 * R10), ea[2] * fabs(R10), eb[2] * fabs(R22 * R10))) return 0;
+    if (!ax(R11 * R11, fabs(t2 * R11), ea[2] * fabs(R11), eb[2] * fabs(R22 * R11))) return 0;
+    // (0, 2): L = (0, -R22, 0)
+    if (!ax(R22 * R22, fabs(t1 * -R22), ea[1] * A22,
+            fma(eb[1], fabs(R11 * -R22), eb[0] * fabs(R10 * -R22)))) return 0;
+    // (1, 0), (1, 1): L = (0, 0, -R0j), along z
+    if (!ax(R00 * R00, fabs(t2 * -R00), ea[2] * A00, eb[2] * fabs(R22 * -R00))) return 0;
+    if (!ax(R01 * R01, fabs(t2 * -R01), ea[2] * A01, eb[2] * fabs(R22 * -R01))) return 0;
+    // (1, 2): L = (R22, 0, -0)
+    if (!ax(R22 * R22, fabs(t0 * R22), ea[0] * A22,
+            fma(eb[1], fabs(R01 * R22), eb[0] * fabs(R00 * R22)))) return 0;
+    // (2, 0), (2, 1): L = (-R1j, R0j, 0), horizontal; (2, 2) has L = 0
+    if (!ax(fma(R00, R00, -R10 * -R10), fabs(fma(t1, R00, t0 * -R10)), fma(ea[1], A00, ea[0] * A10),
+            fma(eb[1], fabs(fma(R11, R00, R01 * -R10)), eb[0] * fabs(fma(R10, R00, R00 * -R10))))) return 0;
+    if (!ax(fma(R01, R01, -R11 * -R11), fabs(fma(t1, R01, t0 * -R11)), fma(ea[1], A01, ea[0] * A11),
+            fma(eb[1], fabs(fma(R11, R01, R01 * -R11)), eb[0] * fabs(fma(R10, R01, R00 * -R11))))) return 0;
+    if (edge) return 1;
+#ifdef SSPP_NO_MANIFOLD
+    return 1;
+#endif
+    return bb_clip_count(pa, ma, ea, pb, mb, eb, fi);
+}
+
+// Both rotations upright (see box_box_deep_count_up)?
+SSPP_HD bool upright3(const double* m) {
+    return m[2] == 0.0 && m[5] == 0.0 && m[6] == 0.0 && m[7] == 0.0;
+}
+
 // ---------------------------------------------------------------- cylinder-box, exact
 // The signed distance of two convex bodies is the maximum over directions n of their
 // separation along n (negative: minus the penetration depth), attained at the normal of the
@@ -882,7 +959,8 @@ SSPP_HD bool pair_supported(int t1, int t2) {
 // DEFER (feasibility only): a cylinder-box pair (already past the bounding-sphere test) returns
 // -1, undecided, without any narrowphase; the caller settles it later with the exact test
 // (k_sspp_c2f -> k_sspp_cbfix), so its pair loop carries none of that code.
-template <bool NEED_DEEP, bool CB = true, bool OUTLINE = false, bool DEFER = false>
+// UP (deep counts only): every box-box pair is upright (box_box_deep_count_up; host-checked).
+template <bool NEED_DEEP, bool CB = true, bool OUTLINE = false, bool DEFER = false, bool UP = false>
 SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1, int t2,
                     const double* p2, const double* m2, const double* s2, double margin, int* nd) {
     *nd = 0;
@@ -913,8 +991,12 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
     // box-box: SAT (exact for boxes) decides contact; deep contacts: one pass, SAT + manifold
     if (NEED_DEEP) {
         SSPP_NP_STAT(13);
-        *nd = (margin >= kDeep || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
-                  ? box_box_deep_count(p1, m1, s1, p2, m2, s2) : 0;
+        if (UP)
+            *nd = (margin >= kDeep || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
+                      ? box_box_deep_count_up(p1, m1, s1, p2, m2, s2) : 0;
+        else
+            *nd = (margin >= kDeep || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
+                      ? box_box_deep_count(p1, m1, s1, p2, m2, s2) : 0;
         if (*nd > 0) SSPP_NP_STAT(14);
         return *nd;
     }

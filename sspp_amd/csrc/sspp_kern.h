@@ -45,8 +45,8 @@ __device__ unsigned long long g_wq_i[8 << 16];
 #endif
 #ifdef SSPP_WG_TIMING
 __device__ unsigned long long g_wg_t[1 << 18];
-__device__ unsigned long long g_wg_ph[6 << 16];  // per workgroup: shader clock after each phase
-#define WG_PH(k) do { if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_wg_ph[6 * blockIdx.x + (k)] = clock64(); } while (0)
+__device__ unsigned long long g_wg_ph[8 << 16];  // per workgroup: shader clock after each phase
+#define WG_PH(k) do { if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_wg_ph[8 * blockIdx.x + (k)] = clock64(); } while (0)
 #else
 #define WG_PH(k) do { } while (0)
 #endif
@@ -69,6 +69,7 @@ struct KScene {
     int static_block;   // sspp: env-env contacts counted and present -> nothing feasible
     double static_cost; // tsp: Collision.h cost of env-env contacts, added per waypoint
     int cylbox;         // some moving pair is cylinder-box (selects the kernels that carry that code)
+    int upright;        // tsp: every box-box pair is upright for a yaw-only mover (k_tsp<..., UP>)
 };
 
 // Scene tables are passed as separate __restrict__ kernel arguments: the pair loop is
@@ -584,7 +585,7 @@ __device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const doub
 // over several lanes can be summed afterwards in pair order, bit-identical to the sum.  REC 1:
 // rec_nd is unsigned char (LDS, k_tsp_pp); REC 2: rec_nd is unsigned and both are written with
 // write-through agent-scope stores (another workgroup reads them, k_tsp_pp2).
-template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true, int REC = 0>
+template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true, int REC = 0, bool UP = false>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                              unsigned long long mask, double* cost, int* stop = nullptr,
                              void* rec_nd = nullptr, double* rec_term = nullptr) {
@@ -644,8 +645,8 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                 have_rot = true;
             }
             const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
-            if (gfirst) nc = collide<DEEP, CB, DEEP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
-            else nc = collide<DEEP, CB, DEEP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+            if (gfirst) nc = collide<DEEP, CB, DEEP, false, UP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+            else nc = collide<DEEP, CB, DEEP, false, UP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
         }
         if (!DEEP) {
             // the loop trip is wave-uniform, so every active lane reaches this vote
@@ -1202,6 +1203,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     }
     if (tid < cpb) s_mask[tid] = 0ull;
     __syncthreads();
+    WG_PH(1);
     if (!ctrl_in && a.insample && !(a.ablate & 1)) {
         // sampleWithNoise: item t = (candidate sl, sampler item m), spread over the workgroup
         const int npert = (n - 2 * P) * D;
@@ -1220,7 +1222,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         double* dst = ctrl_out + cand0 * ndof;
         for (int e = tid; e < nvalid * ndof; e += NT) dst[e] = s_ctrl[e];
     }
-    WG_PH(1);
+    WG_PH(2);
 
     const SceneT TT = T;
     const bool collide_on = a.has_scene && !(a.ablate & 2);
@@ -1294,7 +1296,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
     }
     __syncthreads();
-    WG_PH(2);
+    WG_PH(3);
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
     const int R = a.npts - a.n1;
     if (collide_on && R > 0 && !(a.ablate & 8)) {
@@ -1367,7 +1369,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
-    WG_PH(3);
+    WG_PH(4);
     // ---- phase 3: arc length (computeArcLength, include/sspp.h:152-169) of the listed
     // candidates: the collision-free ones (findBestPath scores only successful paths), or all
     // of them with arc_all.  Chords v_j -> v_{j+1} (v_i = s(i/(W-1))) go to LDS, then each
@@ -1416,7 +1418,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
     }
     __syncthreads();
-    WG_PH(4);
+    WG_PH(5);
     if (tid == 0) C2F_STAT(7, nvalid);
     if (tid < nvalid) {
         const long long c = cand0 + tid;
@@ -1451,7 +1453,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         bb.cost = bi < 0 ? INFINITY : bc; bb.idx = bi; bb.count = __popcll(__ballot(f)); bb.pad = 0;
     }
     finish_batch<NT>(bb, part, sync, best, a.nblk_step, blk);
-    WG_PH(5);
+    WG_PH(6);
 #ifdef SSPP_WG_TIMING
     if (tid == 0 && blockIdx.x < (1 << 16)) {
         g_wg_t[4 * blockIdx.x] = wg_t0;
@@ -2163,7 +2165,7 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
 
 // CB: the scene has cylinder-box pairs (without them the exact cylinder-box code is compiled
 // out: it costs registers even when it never runs)
-template <int NM, bool ONEGEOM, bool CB>
+template <int NM, bool ONEGEOM, bool CB, bool UP = false>
 __global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WAVES_PER_EU) void k_tsp(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
@@ -2211,7 +2213,7 @@ __global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WA
             aL = aL + dist_nd<D>(pv, pc);
             double c = 0.0;
 #ifndef SSPP_PROF_NOCOLL  // profiling variant only
-            point_collide<D, NM, 1, true, ONEGEOM, CB>(pc, a.sc, T, mask, &c);
+            point_collide<D, NM, 1, true, ONEGEOM, CB, 0, UP>(pc, a.sc, T, mask, &c);
 #endif
             const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
             const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
@@ -2560,9 +2562,15 @@ inline KScene kscene(const sspp_scene* s, bool tsp) {
     for (const DPair& p : s->pairs) k.onegeom &= (p.gm == s->pairs[0].gm);
     k.static_block = (!tsp && s->count_static && s->static_contacts > 0) ? 1 : 0;
     k.static_cost = tsp ? s->static_cost : 0.0;
+    k.upright = (tsp && !getenv("SSPP_TSP_GENERIC")) ? 1 : 0;  // SSPP_TSP_GENERIC: A/B and tests
     for (const DPair& p : s->pairs) {
-        const int tg = s->geoms[p.gm].type;
+        const DGeom& g = s->geoms[p.gm];
+        const int tg = g.type;
         k.cylbox |= (tg == 5 && p.otype == 6) || (tg == 6 && p.otype == 5);
+        // the mover's yaw rotation keeps m[2] = m[5] = m[6] = m[7] = 0 exactly (mover_poses
+        // MODE 1, geom_rot_t, matmul3 for a moving partner) when the relative rotations have them
+        if (tg == 6 && p.otype == 6)
+            k.upright &= (!g.relrot || sspd::upright3(g.mat)) && sspd::upright3(p.omat);
     }
     return k;
 }
@@ -2773,15 +2781,18 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
 #undef SSPP_LAUNCH_TSPPP
         return hipGetLastError();
     }
-#define SSPP_LAUNCH_TSP(OG, CBV)                                                                   \
-    hipLaunchKernelGGL((k_tsp<1, OG, CBV>), dim3(nblk), dim3(kBlock), j->lds, st, k, tt, j->d_tab, \
+#define SSPP_LAUNCH_TSP(OG, CBV, UPV)                                                                  \
+    hipLaunchKernelGGL((k_tsp<1, OG, CBV, UPV>), dim3(nblk), dim3(kBlock), j->lds, st, k, tt, j->d_tab, \
                        j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
                        d_status, j->d_part, j->d_sync, d_best)
     const bool og = k.sc.onegeom && k.sc.npairs > 0;
-    if (og && k.sc.cylbox) SSPP_LAUNCH_TSP(true, true);
-    else if (og) SSPP_LAUNCH_TSP(true, false);
-    else if (k.sc.cylbox) SSPP_LAUNCH_TSP(false, true);
-    else SSPP_LAUNCH_TSP(false, false);
+    const bool up = k.sc.upright && !k.sc.cylbox;
+    if (og && k.sc.cylbox) SSPP_LAUNCH_TSP(true, true, false);
+    else if (og && up) SSPP_LAUNCH_TSP(true, false, true);
+    else if (og) SSPP_LAUNCH_TSP(true, false, false);
+    else if (k.sc.cylbox) SSPP_LAUNCH_TSP(false, true, false);
+    else if (up) SSPP_LAUNCH_TSP(false, false, true);
+    else SSPP_LAUNCH_TSP(false, false, false);
 #undef SSPP_LAUNCH_TSP
     return hipGetLastError();
 }

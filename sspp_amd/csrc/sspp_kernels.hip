@@ -1206,7 +1206,7 @@ extern "C" int sspp_debug_wg_times(unsigned long long* out, int n) {
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_t), sizeof(unsigned long long) * (size_t)n);
     return 0;
 }
-extern "C" int sspp_debug_wg_phases(unsigned long long* out, int n) {
+extern "C" int sspp_debug_wg_phases(unsigned long long* out, int n) {  // 8 per workgroup
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_ph), sizeof(unsigned long long) * (size_t)n);
     return 0;

@@ -26,7 +26,8 @@ run(5)
 torch.cuda.synchronize()
 run(steps)
 torch.cuda.synchronize()
-nt, g1 = int(os.environ.get("SSPP_NT", "64")), int(os.environ.get("SSPP_G1", "4"))
+nt, g1 = int(os.environ.get("SSPP_NT", "64" if steps * 4096 >= 16384 else "256")), \
+    int(os.environ.get("SSPP_G1", "4" if steps * 4096 >= 16384 else "64"))
 nwg = steps * (B // (nt // g1))  # candidates per workgroup: NT / G1
 buf = (C.c_ulonglong * (4 * nwg))()
 _lib.lib().__getattr__("sspp_debug_wg_times")(buf, 4 * nwg)
@@ -44,11 +45,11 @@ res = {"workgroups": int(nwg), "span_us": float(en.max()),
        "end_us_pcts": {p: float(np.percentile(en, p)) for p in (10, 50, 90, 99, 100)},
        "last_20_end": [[float(st[i]), float(en[i]), int(ns[i])] for i in np.argsort(en)[-20:]],
        "concurrency_at": {t: int(((st <= t) & (en > t)).sum()) for t in (5, 10, 20, 40, 60, 80)}}
-ph = (C.c_ulonglong * (6 * nwg))()
-_lib.lib().__getattr__("sspp_debug_wg_phases")(ph, 6 * nwg)
-ph = np.frombuffer(ph, dtype=np.uint64).reshape(nwg, 6).astype(np.int64)
-d = np.diff(ph, axis=1)  # shader clocks: sampling+ctrl, hull(1)+phase 1, phase 2 (+hull 2), arc, epilogue
-names = ["prologue_sampling", "phase1", "phase2", "phase3_arc", "epilogue_argmin"]
+ph = (C.c_ulonglong * (8 * nwg))()
+_lib.lib().__getattr__("sspp_debug_wg_phases")(ph, 8 * nwg)
+ph = np.frombuffer(ph, dtype=np.uint64).reshape(nwg, 8)[:, :7].astype(np.int64)
+d = np.diff(ph, axis=1)  # shader clocks per phase
+names = ["prologue_ctrl", "sampling", "phase1", "phase2", "phase3_arc", "epilogue_argmin"]
 res["phase_clocks_mean"] = {n: float(d[:, i].mean()) for i, n in enumerate(names)}
 res["phase_clocks_by_survivors"] = {int(k): {n: float(d[ns == k, i].mean()) for i, n in enumerate(names)}
                                     for k in np.unique(ns)}
