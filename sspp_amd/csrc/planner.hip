@@ -48,21 +48,25 @@ struct Dev {
 template <class T>
 struct Pinned {
     T* p = nullptr;
+    T* d = nullptr;  // its device address (mapped), looked up once per allocation
     size_t n = 0;
     ~Pinned() { if (p) (void)hipHostFree(p); }
     int reserve(size_t count) {
         if (count <= n) return SSPP_OK;
         if (p) (void)hipHostFree(p);
-        p = nullptr; n = 0;
+        p = nullptr; d = nullptr; n = 0;
         hipError_t e = hipHostMalloc((void**)&p, sizeof(T) * (count ? count : 1),
                                      hipHostMallocMapped | hipHostMallocCoherent);
         if (e != hipSuccess) return sspp::set_error(SSPP_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
         n = count;
         return SSPP_OK;
     }
-    T* dev() const {
-        void* d = nullptr;
-        return hipHostGetDevicePointer(&d, p, 0) == hipSuccess ? (T*)d : nullptr;
+    T* dev() {
+        if (!d && p) {
+            void* q = nullptr;
+            if (hipHostGetDevicePointer(&q, p, 0) == hipSuccess) d = (T*)q;
+        }
+        return d;
     }
 };
 

@@ -988,6 +988,17 @@ struct SsppC2F {
     int nt;        // launch shape (host side): threads per workgroup, dynamic LDS bytes
     int lds;
     int ctrl_feas; // ctrl_out rows only for candidates with no contact (written at the end)
+    // fused survivor queue (k_sspp_c2f<..., FQ = true>, one-wave workgroups): phase 1's survivors
+    // become items of the job's work-queue buffers, drained by every workgroup of the launch
+    int fq, fq_npg, fq_nchunk, fq_gs, fq_gcap;
+    unsigned fq_nps;
+    struct FqGroup* fq_grp;   // [steps][groups per step]
+    struct WqCtr* fq_ctr;
+    struct WqStep* fq_stp;
+    struct WqSurv* fq_surv;
+    double* fq_spert;
+    unsigned* fq_queue;
+    struct WqEnt* fq_list;
 };
 
 #ifdef SSPP_C2F_STATS
@@ -1120,7 +1131,15 @@ __device__ __forceinline__ bool cb_point_exact(const double* ctrl, const double*
 #ifndef SSPP_C2F_WAVES_PER_EU
 #define SSPP_C2F_WAVES_PER_EU 4  // measured: 3 -> 1280, 4 -> 1396, 5 -> 1237, 6 -> 697 M cand/s (robocrane)
 #endif
-template <int D, int NM, int P, bool ONEGEOM, int NT>
+template <int D, int NM, int P, bool ONEGEOM>
+__device__ void c2f_fused_tail(const SsppC2F& a, const SceneT& T, const double* __restrict__ otab,
+                               const int* __restrict__ ospan, const double* __restrict__ atab,
+                               const int* __restrict__ aspan, const double* __restrict__ init_ctrl,
+                               double* s_ctrl, double* s_box, const int* s_feas, int step, long long cand0,
+                               int nvalid, double* arc0, unsigned char* feas0, double* ctrl_out0,
+                               sspp_best* best0);
+
+template <int D, int NM, int P, bool ONEGEOM, int NT, bool FQ = false>
 __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     SsppC2F a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
     const double* __restrict__ atab, const int* __restrict__ aspan,
@@ -1144,6 +1163,10 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     int wg_ns = -1;
 #endif
     WG_PH(0);
+    double* const arc0 = arc;
+    unsigned char* const feas0 = feasible;
+    double* const ctrl_out0 = ctrl_out;
+    sspp_best* const best0 = best;
     if (step) {
         arc += step * a.B;
         feasible += step * a.B;
@@ -1297,6 +1320,11 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     }
     __syncthreads();
     WG_PH(3);
+    if (FQ) {  // survivors to the launch's queue; this workgroup then drains it (host-checked mode)
+        c2f_fused_tail<D, NM, P, ONEGEOM>(a, TT, otab, ospan, atab, aspan, init_ctrl, s_ctrl, s_box, s_feas, step,
+                                          cand0, nvalid, arc0, feas0, ctrl_out0, best0);
+        return;
+    }
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
     const int R = a.npts - a.n1;
     if (collide_on && R > 0 && !(a.ablate & 8)) {
@@ -1347,15 +1375,32 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         unsigned long long umask = 0ull;
         for (int i = 0; i < ns; ++i) umask |= s_mask[s_surv[i]];
         const int items = ns * R;
-        for (int base = 0; base < items; base += NT) {  // workgroup-uniform trip count
-            const int it = base + tid;
+        // Few items for many lanes (a single-step launch's 4-wave workgroup with one survivor):
+        // gp pair groups, each a 64-aligned copy of the item range on its own waves, group g
+        // scanning the pairs k = g (mod gp).  A contact in any group clears the survivor's flag,
+        // which stops the others; the result is the same OR over (waypoint, pair).
+        int gp = 1, stride = items;
+        if (np <= 64 && items > 0) {
+            const int s64 = (items + 63) & ~63;
+            while (gp < 8 && s64 * gp * 2 <= NT) gp *= 2;
+            if (gp > 1) stride = s64;
+        }
+        const unsigned long long gsel = gp == 2 ? 0x5555555555555555ull
+                                      : gp == 4 ? 0x1111111111111111ull
+                                      : gp == 8 ? 0x0101010101010101ull : ~0ull;
+        const int total = gp > 1 ? stride * gp : items;
+        for (int base = 0; base < total; base += NT) {  // workgroup-uniform trip count
+            const int lt = base + tid;
+            const int grp = gp > 1 ? lt / stride : 0;   // wave-uniform: stride is a multiple of 64
+            const int it = lt - grp * stride;
+            const unsigned long long gmask = gp > 1 ? gsel << grp : ~0ull;
             bool live = it < items;
             const int si = live ? it / R : 0;
             const int s = s_surv[si];
             const int j = a.n1 + (live ? it - si * R : 0);
             live = live && __hip_atomic_load(s_feas + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
             // lanes of this wave that work on the same survivor
-            const int wave_it0 = base + (tid & ~63);
+            const int wave_it0 = base + (tid & ~63) - grp * stride;
             int lo = si * R - wave_it0, hi = (si + 1) * R - wave_it0;
             lo = lo < 0 ? 0 : lo;
             hi = hi > 64 ? 64 : hi;
@@ -1364,7 +1409,8 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             double q[D];
             eval_pt<D, P>(s_ctrl + s * ndof, otab + j * P1, ospan[j], q);
             bool dfr = false;
-            const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s], umask, gb, s_feas + s, a.sc, TT, dfr);
+            const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s] & gmask, umask & gmask, gb, s_feas + s,
+                                                      a.sc, TT, dfr);
             if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -1751,6 +1797,253 @@ __device__ __forceinline__ void wq_step_finish(const SsppWQ& a, int step, sspp_b
             best[step].reserved = 0;
         }
     }
+}
+
+// ---------------------------------------------------------------- k_sspp_c2f, fused survivor queue
+// A many-step launch is bounded by its workgroups with phase-1 survivors: a feasible survivor's
+// remaining waypoints x every pair run on that workgroup's single wave (16k shader clocks per
+// survivor against ~50k for the rest of the workgroup).  With FQ the survivors are shared inside a
+// GROUP of fq_gs consecutive workgroups of one step (dispatched together):
+//   publish  a workgroup's survivors become entries of its group's queue (k_sspp_wq2's records
+//            and items: nchunk x npg items per survivor);
+//   drain    every member then claims the group's items (compare-and-swap, never past the
+//            published count) until none is left, and leaves.  A claim waits only for the entry of
+//            a survivor whose producer is running (it bumped the tail first); a member that finds
+//            the queue empty leaves, and a producer drains its own items if nobody else does.
+// A survivor's last item decides it (the pending/hit word): feasible -> arc length (canonical
+// order), outputs, one entry in its step's list.  Only the group's members touch its counters
+// (at most fq_gs contenders per word: a chip-wide queue measured ~1000x slower from contention).
+// gcnt = member exits + decisions - survivors published; a member publishes its -ns before its
+// items become claimable and adds its +1 after its drain, so gcnt reaches the group size exactly
+// at the last exit, after every decision: that member re-arms the group and counts it on its
+// step; the step's last group reduces the step's list into best[step] (findBestPath: lowest arc,
+// lowest id) and re-arms the step.  Hand-offs as in k_sspp_wq2: sc1 stores drained before the
+// atomic that signals them, sc1 loads after it.
+struct FqGroup {  // one 64-byte line per group; zero between launches
+    unsigned head, tail;
+    int gcnt;
+    unsigned pad[13];
+};
+__device__ __forceinline__ int fq_add(int* p, int v) {
+    return __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)p, v, WQ_RLX, WQ_AG);
+}
+__device__ __forceinline__ unsigned wq_ld(const unsigned* p) {
+    return __hip_atomic_load((gu32_t*)const_cast<unsigned*>(p), WQ_RLX, WQ_AG);
+}
+
+// whole wave: findBestPath over step `step`'s list into best0[step], then the step's re-arm
+__device__ __forceinline__ void fq_step_finish(const SsppC2F& a, int step, sspp_best* best0) {
+    const int lane = threadIdx.x & 63;
+    WqStep* S = a.fq_stp + step;
+    const unsigned ne = __builtin_amdgcn_readfirstlane(wq_add(&S->nent, 0u));
+    const unsigned cnt = __builtin_amdgcn_readfirstlane(wq_add(&S->count, 0u));
+    const WqEnt* L = a.fq_list + (long long)step * a.B;
+    double bc = INFINITY;
+    long long bi = -1;
+    for (unsigned i = lane; i < ne; i += 64) {
+        const double c = __longlong_as_double((long long)wq_ld64(&L[i].cost));
+        const long long id = (long long)wq_ld64(&L[i].idx);
+        if (better(c, id, bc, bi)) { bc = c; bi = id; }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double oc = __shfl_xor(bc, off, 64);
+        const long long oi = __shfl_xor(bi, off, 64);
+        if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
+    }
+    if (lane == 0) {
+        if (best0) {
+            best0[step].cost = bi < 0 ? INFINITY : bc;
+            best0[step].index = bi;
+            best0[step].count = cnt;
+            best0[step].reserved = 0;
+        }
+        wq_st(&S->nent, 0u);
+        wq_st(&S->count, 0u);
+        wq_st(&S->pad[0], 0u);
+    }
+}
+
+template <int D, int NM, int P, bool ONEGEOM>
+__device__ void c2f_fused_tail(const SsppC2F& a, const SceneT& T, const double* __restrict__ otab,
+                               const int* __restrict__ ospan, const double* __restrict__ atab,
+                               const int* __restrict__ aspan, const double* __restrict__ init_ctrl,
+                               double* s_ctrl, double* s_box, const int* s_feas, int step, long long cand0,
+                               int nvalid, double* arc0, unsigned char* feas0, double* ctrl_out0,
+                               sspp_best* best0) {
+    constexpr int P1 = P + 1;
+    constexpr int NB = 3 * NM;
+    const int lane = threadIdx.x & 63;
+    const int n = a.n, ndof = n * D, npert = (n - 2 * P) * D, np = a.sc.npairs;
+    const long long out0 = (long long)step * a.B + cand0;
+    const unsigned nps = a.fq_nps;
+    // this workgroup's group: fq_gs consecutive workgroups of its step
+    const int blk = (int)(cand0 / a.cpb);
+    const int gi = blk / a.fq_gs, gps = (a.nblk_step + a.fq_gs - 1) / a.fq_gs;
+    const int gsz = min(a.fq_gs, a.nblk_step - gi * a.fq_gs);
+    FqGroup* Gq = a.fq_grp + (long long)step * gps + gi;
+    unsigned* queue = a.fq_queue + ((long long)step * gps + gi) * a.fq_gcap;
+    const bool isc = lane < nvalid;
+    const bool surv = isc && s_feas[lane] != 0;
+    const unsigned long long sb = __ballot(surv);
+    const int ns = __popcll(sb);
+    if (isc && !surv) {  // phase 1 found a contact
+        feas0[out0 + lane] = 0;
+        arc0[out0 + lane] = INFINITY;
+    }
+    // ---- publish
+    if (ns > 0) {
+        unsigned base = 0;
+        if (lane == 0) {  // counted before any of its items can be claimed (hence decided)
+            fq_add(&Gq->gcnt, -ns);
+            wq_drain();
+            base = wq_add(&Gq->tail, (unsigned)ns);
+        }
+        base = __builtin_amdgcn_readfirstlane(base);
+        long long my_rec = -1;
+        int i = 0;
+        for (unsigned long long m = sb; m; m &= m - 1ull, ++i) {  // wave-uniform
+            const int g = __builtin_ctzll(m);
+            const double* c = s_ctrl + g * ndof;
+            unsigned long long hm = ~0ull;
+            if (a.hull != 0 && np <= 64) {  // the candidate-level broadphase (pair_may_touch)
+                if (lane < NB) {
+                    const int mm = lane / 3, d = lane - mm * 3, col = 7 * mm + d;
+                    double lo, hi;
+                    if (col < D) {
+                        lo = hi = c[col];
+                        for (int jj = 1; jj < n; ++jj) {
+                            const double v = c[jj * D + col];
+                            lo = v < lo ? v : lo;
+                            hi = v > hi ? v : hi;
+                        }
+                    } else {
+                        lo = hi = (double)((cmover_t)T.movers)[mm].qpos0[d];
+                    }
+                    s_box[lane] = lo;
+                    s_box[NB + lane] = hi;
+                }
+                __syncthreads();
+                bool t = false;
+                if (lane < np) {
+                    const DPair pr = load_pair((cpair_t)T.pairs + lane);
+                    const DGeom G = load_geom((cgeom_t)T.geoms + pr.gm);
+                    const int mm = (NM > 1 && G.mover == 1) ? 1 : 0;
+                    t = pair_may_touch(pr, G, s_box + 3 * mm, s_box + NB + 3 * mm);
+                }
+                hm = __ballot(t);
+                __syncthreads();
+            }
+            const long long rec = out0 + g;
+            for (int k = lane; k < npert; k += 64)
+                wq_st64((unsigned long long*)(a.fq_spert + rec * npert) + k,
+                        (unsigned long long)__double_as_longlong(c[P * D + k]));
+            if (lane == 0) {
+                WqSurv* R = a.fq_surv + rec;
+                wq_st64(&R->mask, hm);
+                wq_st64(&R->pend, (unsigned long long)nps);
+                wq_st64(&R->p1def, 0ull);
+            }
+            if (lane == i) my_rec = rec;
+        }
+        wq_drain();  // every record store of the wave is out before the entries that signal them
+        if (lane < ns) wq_st(&queue[base + (unsigned)lane], (unsigned)my_rec + 1u);  // base + ns <= gcap
+    }
+    // ---- drain the group's queue
+    for (;;) {
+        unsigned h = 0;
+        if (lane == 0) {
+            h = wq_ld(&Gq->head);
+            for (;;) {
+                const unsigned long long lim = (unsigned long long)wq_ld(&Gq->tail) * nps;
+                if ((unsigned long long)h >= lim) { h = ~0u; break; }
+                if (__hip_atomic_compare_exchange_strong((gu32_t*)&Gq->head, &h, h + 1u, WQ_RLX, WQ_RLX, WQ_AG))
+                    break;
+            }
+        }
+        h = __builtin_amdgcn_readfirstlane(h);
+        if (h == ~0u) break;
+        const unsigned e = h / nps, r = h - e * nps;
+        const unsigned chunk = r / (unsigned)a.fq_npg;
+        const int grp = (int)(r - chunk * (unsigned)a.fq_npg);
+        unsigned* qe = queue + e;
+        unsigned v = 0;
+        if (lane == 0) {  // its producer is running (it bumped the tail): a bounded wait
+            for (int it = 0; it < (1 << 22); ++it) {
+                v = wq_ld(qe);
+                if (v) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!v) wq_st(&a.fq_ctr->error[0], 2u);
+        }
+        v = __builtin_amdgcn_readfirstlane(v);
+        if (!v) continue;  // diagnostic only (sspp_debug_job_error)
+        const long long rec = (long long)v - 1;
+        WqSurv* R = a.fq_surv + rec;
+        const unsigned long long mask = wq_group_mask(wq_bcast64(wq_ld64(&R->mask)), grp, a.fq_npg);
+        const bool hit0 = (wq_bcast64(wq_ld64(&R->pend)) >> 32) != 0ull;  // a hint: may lag
+        __syncthreads();  // the previous item's reads of s_ctrl are done
+        for (int rr = lane; rr < ndof; rr += 64) {
+            double x = init_ctrl[rr];
+            const int k = rr - P * D;
+            if (k >= 0 && k < npert)
+                x = __longlong_as_double((long long)wq_ld64((const unsigned long long*)(a.fq_spert + rec * npert) + k));
+            s_ctrl[rr] = x;
+        }
+        __syncthreads();
+        const int j = a.n1 + (int)chunk * 64 + lane;
+        const bool scan = !hit0 && mask != 0ull;
+        const bool live = scan && j < a.npts;
+        const int row = live ? j : 0;
+        bool ghit = false, dfr = false;
+        if (scan) {
+            double q[D];
+            eval_pt<D, P>(s_ctrl, otab + row * P1, ospan[row], q);
+            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mask, mask, ~0ull, nullptr, a.sc, T, dfr);
+        }
+        const bool anyhit = __ballot(ghit) != 0ull;
+        unsigned long long prev = 0ull;
+        if (lane == 0) {
+            if (anyhit) wq_or64(&R->pend, 1ull << 32);
+            prev = wq_add64(&R->pend, ~0ull);  // pending - 1; returns the hit bit with the count
+        }
+        prev = wq_bcast64(prev);
+        if ((unsigned)prev != 1u) continue;
+        // ---- the survivor's last item: decide it
+        const bool bad = (prev >> 32) != 0ull;
+        double t = INFINITY;
+        if (!bad) t = wave_arc<D, P>(s_ctrl, a.W - 1, a.lpc, atab, aspan);
+        if (!bad && ctrl_out0 && a.ctrl_feas)
+            for (int k = lane; k < ndof; k += 64) ctrl_out0[rec * ndof + k] = s_ctrl[k];
+        if (lane == 0) {
+            feas0[rec] = bad ? 0 : 1;
+            arc0[rec] = t;
+            if (!bad) {
+                WqStep* S = a.fq_stp + step;
+                const unsigned slot = wq_add(&S->nent, 1u);
+                WqEnt* en = a.fq_list + (long long)step * a.B + slot;
+                wq_st64(&en->cost, (unsigned long long)__double_as_longlong(t));
+                wq_st64(&en->idx, (unsigned long long)(a.first_id + step * a.step_stride + (rec - (long long)step * a.B)));
+                wq_add(&S->count, 1u);
+            }
+            wq_st(qe, 0u);  // every claimer of this entry has read it (their items came first)
+            wq_drain();     // the list entry is out before the count that signals it
+            fq_add(&Gq->gcnt, 1);
+        }
+    }
+    // ---- leave: the group's last member re-arms it and counts it on its step
+    int done = 0;
+    if (lane == 0) {
+        done = fq_add(&Gq->gcnt, 1) + 1 == gsz;
+        if (done) {
+            wq_st(&Gq->head, 0u);
+            wq_st(&Gq->tail, 0u);
+            __hip_atomic_store((__attribute__((address_space(1))) int*)&Gq->gcnt, 0, WQ_RLX, WQ_AG);
+            done = wq_add(&a.fq_stp[step].pad[0], 1u) + 1u == (unsigned)gps ? 2 : 1;
+        }
+    }
+    done = __builtin_amdgcn_readfirstlane(done);
+    if (done == 2) fq_step_finish(a, step, best0);
 }
 
 #ifndef SSPP_WQ1_WAVES_PER_EU
@@ -2511,6 +2804,10 @@ struct sspp_job {
     int insample = 0;          // sample inside the scoring kernel (SSPP_INSAMPLE=1)
     // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
     int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16, nt2 = 256;
+    int fq = 0, fq_npg = 1, fq_gs = 16;  // k_sspp_c2f fused survivor queue (SSPP_FQ, SSPP_FQ_NPG, SSPP_FQ_GS)
+    FqGroup* d_fqgrp = nullptr;          // its group counters and queues (zero between launches)
+    unsigned* d_fqq = nullptr;
+    int64_t fq_ngrp = 0, fq_nq = 0;
     int shape_forced = 0;      // SSPP_NT / SSPP_G1 fix the c2f shape, else it is chosen per launch
     int64_t part_cap = 0;      // BlockBest records d_part holds
     int arc_all = 0;           // arc length for every candidate (else collision-free only)
@@ -2641,6 +2938,21 @@ hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o,
                                 hipStream_t st) {
     const double* atab = j->d_tab + (size_t)(j->W + 1) * (P + 1);
     const int* aspan = j->d_span + (j->W + 1);
+    if constexpr (NT == 64) {
+        if (k.fq) {  // fused survivor queue (host-checked: no cylinder-box pairs, so no k_sspp_cbfix)
+            if (NM == 1 && k.sc.onegeom)
+                hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true, 64, true>), dim3(nblk), dim3(64), k.lds, st, k,
+                                   scene_t_job(j, true), j->d_otab, j->d_ospan, atab, aspan, j->d_init,
+                                   j->d_limits, o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part,
+                                   j->d_sync, o.best);
+            else
+                hipLaunchKernelGGL((k_sspp_c2f<D, NM, P, false, 64, true>), dim3(nblk), dim3(64), k.lds, st, k,
+                                   scene_t_job(j, true), j->d_otab, j->d_ospan, atab, aspan, j->d_init,
+                                   j->d_limits, o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part,
+                                   j->d_sync, o.best);
+            return hipGetLastError();
+        }
+    }
     if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
         hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true, NT>), dim3(nblk), dim3(NT), k.lds, st, k,
                            scene_t_job(j, !o.ctrl_in), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,

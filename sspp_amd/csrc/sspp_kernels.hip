@@ -593,6 +593,11 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     }
     j->sampler = a->sampler ? 1 : 0;
     { const char* e = getenv("SSPP_SAMPLER"); if (e) j->sampler = atoi(e) ? 1 : 0; }
+    // fused survivor queue: opt-in (measured slower: the group queues' device-scope atomics cost
+    // more than the balance they buy)
+    { const char* e = getenv("SSPP_FQ"); j->fq = e ? atoi(e) : 0; }
+    { const char* e = getenv("SSPP_FQ_NPG"); j->fq_npg = e ? std::max(1, std::min(8, atoi(e))) : 1; }
+    { const char* e = getenv("SSPP_FQ_GS"); j->fq_gs = e ? std::max(1, std::min(256, atoi(e))) : 16; }
     // default: c2f draws inside the scoring kernel (SSPP_INSAMPLE=0: chip-wide k_sample_sspp; measured slower)
     { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : (j->c2f ? 1 : 0); }
     { const char* e = getenv("SSPP_HULL"); j->hull = e ? atoi(e) : 2; }
@@ -676,7 +681,8 @@ static int wq_reserve(sspp_job* j, int64_t cands) {
     if (hipMalloc((void**)&j->d_wsurv, sizeof(WqSurv) * cands) != hipSuccess ||
         hipMalloc((void**)&j->d_wspert, sizeof(double) * np * cands) != hipSuccess ||
         hipMalloc((void**)&j->d_wqueue, sizeof(unsigned) * kWqShards * cands) != hipSuccess ||
-        hipMalloc((void**)&j->d_wlist, sizeof(WqEnt) * cands) != hipSuccess)
+        hipMalloc((void**)&j->d_wlist, sizeof(WqEnt) * cands) != hipSuccess ||
+        hipMemset(j->d_wqueue, 0, sizeof(unsigned) * kWqShards * cands) != hipSuccess)  // fused queue: 0 = empty
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc work-queue buffers");
     j->wq_cap = cands;
     return SSPP_OK;
@@ -821,6 +827,40 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         c.hull = j->hull;
         c.dfr = j->d_dfr;
         c.ctrl_feas = j->ctrl_feas;
+        // fused survivor queue: the throughput shape (one-wave workgroups) on sampled candidates
+        // whose pair table needs no later fixup (no cylinder-box deferral, <= 64 pairs)
+        if (j->fq && !j->wq && nt == 64 && !d_ctrl && j->insample && !j->arc_all && c.npts > c.n1 &&
+            c.has_scene && c.sc.npairs > 0 && c.sc.npairs <= 64 && !c.sc.cylbox && !c.sc.static_block &&
+            c.ablate == 0) {
+            // sized once for the largest launch this job can make (up to 2M candidates), so no
+            // later launch re-allocates (and synchronises) inside a timed loop
+            int rc = wq_reserve(j, std::max<int64_t>((int64_t)steps * B,
+                                                     std::min<int64_t>((int64_t)kMaxSteps * j->max_batch, 1 << 21)));
+            if (rc) return rc;
+            const int gs = j->fq_gs, gps = (nblk + gs - 1) / gs, gcap = gs * cpb;
+            const int64_t ngrp = std::max<int64_t>((int64_t)steps * gps,
+                                                   (int64_t)kMaxSteps * (((j->max_batch + cpb - 1) / cpb + gs - 1) / gs));
+            if (ngrp > j->fq_ngrp || ngrp * gcap > j->fq_nq) {
+                (void)hipDeviceSynchronize();  // earlier launches may still use the old buffers
+                if (j->d_fqgrp) (void)hipFree(j->d_fqgrp);
+                if (j->d_fqq) (void)hipFree(j->d_fqq);
+                j->d_fqgrp = nullptr; j->d_fqq = nullptr; j->fq_ngrp = 0; j->fq_nq = 0;
+                if (hipMalloc((void**)&j->d_fqgrp, sizeof(FqGroup) * ngrp) != hipSuccess ||
+                    hipMalloc((void**)&j->d_fqq, sizeof(unsigned) * ngrp * gcap) != hipSuccess ||
+                    hipMemset(j->d_fqgrp, 0, sizeof(FqGroup) * ngrp) != hipSuccess ||
+                    hipMemset(j->d_fqq, 0, sizeof(unsigned) * ngrp * gcap) != hipSuccess)
+                    return sspp::set_error(SSPP_E_NOMEM, "hipMalloc fused-queue buffers");
+                j->fq_ngrp = ngrp; j->fq_nq = ngrp * gcap;
+            }
+            c.fq = 1;
+            c.fq_npg = std::min(j->fq_npg, c.sc.npairs);
+            c.fq_nchunk = (c.npts - c.n1 + 63) / 64;
+            c.fq_nps = (unsigned)(c.fq_nchunk * c.fq_npg);
+            c.fq_gs = gs; c.fq_gcap = gcap;
+            c.fq_grp = j->d_fqgrp; c.fq_queue = j->d_fqq;
+            c.fq_ctr = j->d_wctr; c.fq_stp = j->d_wstp; c.fq_surv = j->d_wsurv; c.fq_spert = j->d_wspert;
+            c.fq_list = j->d_wlist;
+        }
         const int nb = nblk * steps;
         e = hipErrorInvalidValue;
         switch (j->D) {
@@ -1084,7 +1124,7 @@ extern "C" void sspp_job_free(sspp_job* j) {
     if (j->d_wspert) (void)hipFree(j->d_wspert);
     if (j->d_wqueue) (void)hipFree(j->d_wqueue);
     if (j->d_wlist) (void)hipFree(j->d_wlist);
-    for (void* q : {(void*)j->d_pp_nd, (void*)j->d_pp_term, (void*)j->d_pp_arrive})
+    for (void* q : {(void*)j->d_pp_nd, (void*)j->d_pp_term, (void*)j->d_pp_arrive, (void*)j->d_fqgrp, (void*)j->d_fqq})
         if (q) (void)hipFree(q);
     if (j->upd_ev) {
         (void)hipEventSynchronize(j->upd_ev);

@@ -377,6 +377,45 @@ def test_step_executor_matches_eager(robocrane, spl):
         assert wq_error(j) == 0
 
 
+@pytest.mark.parametrize("fq,npg,gs", [("0", "1", "16"), ("1", "1", "16"), ("1", "2", "16"), ("1", "4", "4"),
+                                       ("1", "1", "1"), ("1", "2", "256")])
+@pytest.mark.parametrize("sigma,spl", [(0.08, 20), (0.08, 32), (0.02, 16), (0.3, 20)])
+def test_fused_queue_matches_oracle(robocrane, monkeypatch, fq, npg, gs, sigma, spl):
+    """k_sspp_c2f's fused survivor queue (the executor's one-wave launches of many steps): every
+    step's per-candidate feasibility and arc length equal the oracle's on the same Philox
+    candidates, and every step's argmin record the oracle's argmin — with the queue off (the
+    in-workgroup phase 2), on with groups of 1 to 256 workgroups, and with survivor items split
+    into 2 / 4 pair groups.  sigma 0.02
+    leaves most candidates surviving phase 1, sigma 0.3 almost none."""
+    import sspp_amd as S
+    import torch
+    monkeypatch.setenv("SSPP_FQ", fq)
+    monkeypatch.setenv("SSPP_FQ_NPG", npg)
+    monkeypatch.setenv("SSPP_FQ_GS", gs)
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    B, G, stride, first = 4096, spl, 4096, 7 * 4096
+    job = S.SsppJob(scene, knots, 3, ctrl0, sigma, np.ones(7), 128, max_batch=B)
+    arcs = [torch.empty(spl * B, dtype=torch.float64, device="cuda")]
+    feas = [torch.empty(spl * B, dtype=torch.uint8, device="cuda")]
+    ex = S.SsppSteps([job], [torch.cuda.current_stream()], B, arcs, feas, steps_per_launch=spl)
+    best = torch.zeros((G, 4), dtype=torch.int64, device="cuda")
+    for rep in range(2):  # the second launch reuses the re-armed queue and step counters
+        ex.enqueue(G, first + rep * G * stride, stride, best)
+        torch.cuda.synchronize()
+        arc, fe, got = arcs[0].cpu().numpy(), feas[0].cpu().numpy(), best.cpu()
+        for i in (0, 7, G - 1):
+            f0 = first + (rep * G + i) * stride
+            ctrl = O.sample_sspp(ctrl0, 3, sigma, np.ones(7), 0x5EED, f0, B)
+            arc_o, feas_o = O.sspp_score(oscene, knots, 3, ctrl, 128)
+            np.testing.assert_array_equal(fe[i * B:(i + 1) * B], feas_o)
+            assert arc_err(arc[i * B:(i + 1) * B], arc_o) <= COST_TOL
+            k, _ = O.argmin(arc_o, feas_o)
+            d = S.decode_best(got[i])
+            assert d[1] == (f0 + k if k >= 0 else -1) and d[2] == int(feas_o.sum()), (rep, i, d, k)
+    assert wq_error(job) == 0
+
+
 @pytest.mark.parametrize("kernel", ["2", "1"])
 def test_fp32_sampler_opt_in(robocrane, monkeypatch, kernel):
     """The opt-in FP32 Box-Muller quads (sampler = 1): candidates bit-identical to the oracle's
