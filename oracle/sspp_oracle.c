@@ -1235,6 +1235,30 @@ static or_cylbox cb_box_frame(const or_cylbox* c) {
     return b;
 }
 
+/* Vertical cylinder (ma[2] = ma[5] = 0) vs upright box (mb[2] = mb[5] = mb[6] = mb[7] = 0): both
+   are prisms along z, so the signed distance is that of the centre offset (box frame) to
+   (rectangle + disc R) x [-(ez + H), ez + H]; the device's sspd::cb_upright_sd, operation for
+   operation (the yaw-only TaskSpacePlanner mover keeps such pairs upright). */
+static int cb_upright(const double* ma, const double* mb) {
+    return ma[2] == 0.0 && ma[5] == 0.0 && mb[2] == 0.0 && mb[5] == 0.0 && mb[6] == 0.0 && mb[7] == 0.0;
+}
+static double cb_upright_sd(const double* pa, const double* sz, const double* pb, const double* mb,
+                            const double* eb) {
+    const double d0 = pa[0] - pb[0], d1 = pa[1] - pb[1], d2 = pa[2] - pb[2];
+    const double cx = fma(mb[3], d1, mb[0] * d0), cy = fma(mb[4], d1, mb[1] * d0), cz = mb[8] * d2;
+    const double ax = fabs(cx) - eb[0], ay = fabs(cy) - eb[1];
+    double dr;
+    if (ax > 0.0 || ay > 0.0) {
+        const double ox = ax > 0.0 ? ax : 0.0, oy = ay > 0.0 ? ay : 0.0;
+        dr = sqrt(fma(ox, ox, oy * oy));
+    } else {
+        dr = ax > ay ? ax : ay;
+    }
+    const double dxy = dr - sz[0], dz = fabs(cz) - (sz[1] + eb[2]);
+    if (dxy > 0.0 && dz > 0.0) return sqrt(fma(dxy, dxy, dz * dz));
+    return dxy > dz ? dxy : dz;
+}
+
 /* cylinder (A) vs box (B): signed distance < thr; SAT axes, then witnesses, then the
    remaining candidate directions */
 static int cyl_box_overlap(const double* pa, const double* ma, const double* sz, const double* pb,
@@ -1273,6 +1297,12 @@ static int collide(int t1, const double* p1, const double* m1, const double* s1,
         return -1;
     }
     if (t1 == OR_GEOM_CYLINDER && t2 == OR_GEOM_BOX) { /* exact; one contact (MuJoCo convex) */
+        if (cb_upright(m1, m2)) {
+            const double sd = cb_upright_sd(p1, s1, p2, m2, s2);
+            if (!(sd < margin)) return 0;
+            *ndeep = sd < DEEP;
+            return 1;
+        }
         int c = cyl_box_overlap(p1, m1, s1, p2, m2, s2, margin);
         if (!c) return 0;
         *ndeep = cyl_box_overlap(p1, m1, s1, p2, m2, s2, DEEP);

@@ -173,12 +173,13 @@ static int plan_enqueue(sspp_planner* p, const double* start, const double* end,
     if (!pinned_out)
         return sspp_job_sample_score(p->plan_job.j, first_id, B, p->d_arc.p, p->d_feas.p,
                                      all_ctrl ? p->d_ctrl.p : nullptr, p->d_best.p, p->stream);
+    // no device argmin here: findBestPath runs over the feasible rows in the host gather
+    // (sspp_planner_plan), which saves the kernel's cross-workgroup argmin hand-off
     double* ha = p->h_arc.dev();
     unsigned char* hf = p->h_feas.dev();
-    sspp_best* hb = p->h_best.dev();
     double* hc = p->h_ctrl.dev();
-    if (!ha || !hf || !hb || !hc) return sspp::set_error(SSPP_E_HIP, "hipHostGetDevicePointer failed");
-    return sspp_job_sample_score(p->plan_job.j, first_id, B, ha, hf, hc, hb, p->stream);
+    if (!ha || !hf || !hc) return sspp::set_error(SSPP_E_HIP, "hipHostGetDevicePointer failed");
+    return sspp_job_sample_score(p->plan_job.j, first_id, B, ha, hf, hc, nullptr, p->stream);
 }
 
 extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const double* end, double sigma,
@@ -195,18 +196,27 @@ extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const dou
         (rc = hipck(hipStreamSynchronize(p->stream), "plan")))
         return rc;
     // the feasible candidates in candidate order (findBestPath's input, include/sspp.h:215-216)
+    // and findBestPath itself (include/sspp.h:171-192): the lowest arc length, ties to the
+    // lowest id (the first in candidate order) — the device argmin's (cost, id) order
     const size_t nd = (size_t)init_points * p->D;
     const unsigned char* f = p->h_feas.p;
     long long cnt = 0;
+    double bc = INFINITY;
+    int64_t bi = -1;
     for (int64_t i = 0; i < sample_count; ++i) {
         if (f[i] != 1) continue;
+        const double a = p->h_arc.p[i];
+        if (bi < 0 || a < bc) { bc = a; bi = first_id + i; }
         if (feasible_ids) feasible_ids[cnt] = first_id + i;
-        if (feasible_arc) feasible_arc[cnt] = p->h_arc.p[i];
+        if (feasible_arc) feasible_arc[cnt] = a;
         if (feasible_ctrl) std::memcpy(feasible_ctrl + cnt * nd, p->h_ctrl.p + i * nd, sizeof(double) * nd);
         ++cnt;
     }
     *n_feasible = cnt;
-    *best_out = *p->h_best.p;
+    best_out->cost = bi < 0 ? INFINITY : bc;
+    best_out->index = bi;
+    best_out->count = cnt;
+    best_out->reserved = 0;
     return SSPP_OK;
 }
 

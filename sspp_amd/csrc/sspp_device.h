@@ -924,6 +924,32 @@ __host__ __device__ inline __attribute__((noinline)) bool cb_ext_overlap_call(
     return cb_ext_overlap(T0, T1, T2, a0, a1, a2, e0, e1, e2, R, H, thr);
 }
 
+// Cylinder (A) vs box (B) when the cylinder's axis is vertical (ma[2] = ma[5] = 0) and the box
+// is upright (mb[2] = mb[5] = mb[6] = mb[7] = 0): both are prisms along z, so their Minkowski
+// difference is (box rectangle + disc of radius R) x [-(ez + H), ez + H] and the signed distance
+// is that of the centre offset c (box frame) to it: d_xy = (signed distance of c_xy to the
+// rectangle) - R, d_z = |c_z| - (H + ez); sd = sqrt(d_xy^2 + d_z^2) when both are positive, else
+// max(d_xy, d_z).  Exact (the same decision as the candidate-direction search up to rounding);
+// the oracle runs the same operations (oracle/sspp_oracle.c::cb_upright_sd), so both decide
+// every pair identically.  A yaw-only TaskSpacePlanner mover keeps a vertical cylinder vertical.
+SSPP_HD bool cyl_vertical(const double* m) { return m[2] == 0.0 && m[5] == 0.0; }
+SSPP_HD double cb_upright_sd(const double* pa, const double* sz, const double* pb, const double* mb,
+                             const double* eb) {
+    const double d0 = pa[0] - pb[0], d1 = pa[1] - pb[1], d2 = pa[2] - pb[2];
+    const double cx = fma(mb[3], d1, mb[0] * d0), cy = fma(mb[4], d1, mb[1] * d0), cz = mb[8] * d2;
+    const double ax = fabs(cx) - eb[0], ay = fabs(cy) - eb[1];
+    double dr;
+    if (ax > 0.0 || ay > 0.0) {
+        const double ox = ax > 0.0 ? ax : 0.0, oy = ay > 0.0 ? ay : 0.0;
+        dr = sqrt(fma(ox, ox, oy * oy));
+    } else {
+        dr = ax > ay ? ax : ay;
+    }
+    const double dxy = dr - sz[0], dz = fabs(cz) - (sz[1] + eb[2]);
+    if (dxy > 0.0 && dz > 0.0) return sqrt(fma(dxy, dxy, dz * dz));
+    return dxy > dz ? dxy : dz;
+}
+
 // cylinder (A) vs box (B): signed distance < thr (thr = margin >= 0, or kDeep for a deep
 // contact).  The 7 SAT axes (world frame) separate most pairs; the rest runs in the box frame:
 // witnesses prove most overlaps, the candidate directions (OUTLINE: as a call) decide the rest.
@@ -960,7 +986,10 @@ SSPP_HD bool pair_supported(int t1, int t2) {
 // -1, undecided, without any narrowphase; the caller settles it later with the exact test
 // (k_sspp_c2f -> k_sspp_cbfix), so its pair loop carries none of that code.
 // UP (deep counts only): every box-box pair is upright (box_box_deep_count_up; host-checked).
-template <bool NEED_DEEP, bool CB = true, bool OUTLINE = false, bool DEFER = false, bool UP = false>
+// CB: 0 no cylinder-box pairs (code compiled out), 1 the exact test (vertical-cylinder /
+// upright-box pairs take cb_upright_sd), 2 every cylinder-box pair is vertical / upright
+// (host-checked): cb_upright_sd only, the candidate search compiled out.
+template <bool NEED_DEEP, int CB = 1, bool OUTLINE = false, bool DEFER = false, bool UP = false>
 SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1, int t2,
                     const double* p2, const double* m2, const double* s2, double margin, int* nd) {
     *nd = 0;
@@ -978,6 +1007,15 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
     }
     if (t1 == 5) {  // cylinder-box: exact signed distance test, one contact (MuJoCo's convex collider)
         if (!CB) return 0;
+        if (CB == 2 || (!DEFER && cyl_vertical(m1) && upright3(m2))) {
+            const double sd = cb_upright_sd(p1, s1, p2, m2, s2);
+            if (NEED_DEEP) {
+                const int d = (margin >= kDeep) ? (sd < kDeep) : (sd < margin && sd < kDeep);
+                *nd = d;
+                return d;
+            }
+            return sd < margin ? 1 : 0;
+        }
         if (DEFER && !NEED_DEEP) return -1;
         if (NEED_DEEP) {
             int d = (margin >= kDeep) ? (int)cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, kDeep)

@@ -70,6 +70,7 @@ struct KScene {
     double static_cost; // tsp: Collision.h cost of env-env contacts, added per waypoint
     int cylbox;         // some moving pair is cylinder-box (selects the kernels that carry that code)
     int upright;        // tsp: every box-box pair is upright for a yaw-only mover (k_tsp<..., UP>)
+    int cbup;           // tsp: every cylinder-box pair is vertical / upright (collide<..., CB = 2>)
 };
 
 // Scene tables are passed as separate __restrict__ kernel arguments: the pair loop is
@@ -585,7 +586,7 @@ __device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const doub
 // over several lanes can be summed afterwards in pair order, bit-identical to the sum.  REC 1:
 // rec_nd is unsigned char (LDS, k_tsp_pp); REC 2: rec_nd is unsigned and both are written with
 // write-through agent-scope stores (another workgroup reads them, k_tsp_pp2).
-template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, bool CB = true, int REC = 0, bool UP = false>
+template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, int CB = 1, int REC = 0, bool UP = false>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                              unsigned long long mask, double* cost, int* stop = nullptr,
                              void* rec_nd = nullptr, double* rec_term = nullptr) {
@@ -1233,10 +1234,15 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         const int nq = sample_items(a.sampler, npert);
         const int total = nvalid * nq;
         {
+            // item t = (sl, m) walked with add-with-carry (no integer division per item)
+            const int dsl = NT / nq, dm = NT - dsl * nq;
+            int sl = tid / nq, m = tid - sl * nq;
             for (int t = tid; t < total; t += NT) {
-                const int sl = t / nq, m = t - sl * nq;
                 sample_item(a.sampler, a.seed, (unsigned long long)(first_id + cand0 + sl), m, npert, D, a.sigma,
                             s_lim, s_ctrl + sl * ndof + P * D);
+                sl += dsl;
+                m += dm;
+                if (m >= nq) { m -= nq; ++sl; }
             }
         }
         __syncthreads();
@@ -2458,8 +2464,12 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
 
 // CB: the scene has cylinder-box pairs (without them the exact cylinder-box code is compiled
 // out: it costs registers even when it never runs)
-template <int NM, bool ONEGEOM, bool CB, bool UP = false>
-__global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WAVES_PER_EU) void k_tsp(
+#ifndef SSPP_TSP_WAVES_PER_EU_MG  // several moving geoms (their per-geom poses stay live)
+#define SSPP_TSP_WAVES_PER_EU_MG 2
+#endif
+template <int NM, bool ONEGEOM, int CB, bool UP = false>
+__global__ __launch_bounds__(kBlock, CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
+                                             : (ONEGEOM ? SSPP_TSP_WAVES_PER_EU : SSPP_TSP_WAVES_PER_EU_MG)) void k_tsp(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
     const double* __restrict__ sigma, const double* __restrict__ vias_in,
@@ -2563,7 +2573,7 @@ __global__ __launch_bounds__(kBlock, CB ? SSPP_TSP_WAVES_PER_EU_CB : SSPP_TSP_WA
 // of np.  Deep pairs are recorded per (waypoint, pair) in LDS; wave 0 then sums each waypoint's
 // terms in pair order and runs k_tsp's epilogue (same lanes, shuffles and reductions), so every
 // output is bit-identical to k_tsp's.  Needs cp <= 64 and np <= 64 (host check).
-template <int NM, bool ONEGEOM, bool CB, int G>
+template <int NM, bool ONEGEOM, int CB, int G>
 __global__ __launch_bounds__(64 * G, 2) void k_tsp_pp(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
@@ -2656,7 +2666,7 @@ __global__ __launch_bounds__(64 * G, 2) void k_tsp_pp(
 // every (waypoint, pair) of its groups — contact count (0 when not deep) and term — as
 // write-through agent-scope stores; its last arriving workgroup (agent-scope acquire) sums each
 // waypoint in pair order and runs the epilogue.  Same outputs as k_tsp, bit for bit.
-template <int NM, bool ONEGEOM, bool CB, int G>
+template <int NM, bool ONEGEOM, int CB, int G>
 __global__ __launch_bounds__(64 * G, 2) void k_tsp_pp2(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
@@ -2860,6 +2870,7 @@ inline KScene kscene(const sspp_scene* s, bool tsp) {
     k.static_block = (!tsp && s->count_static && s->static_contacts > 0) ? 1 : 0;
     k.static_cost = tsp ? s->static_cost : 0.0;
     k.upright = (tsp && !getenv("SSPP_TSP_GENERIC")) ? 1 : 0;  // SSPP_TSP_GENERIC: A/B and tests
+    k.cbup = k.upright;
     for (const DPair& p : s->pairs) {
         const DGeom& g = s->geoms[p.gm];
         const int tg = g.type;
@@ -2868,6 +2879,11 @@ inline KScene kscene(const sspp_scene* s, bool tsp) {
         // MODE 1, geom_rot_t, matmul3 for a moving partner) when the relative rotations have them
         if (tg == 6 && p.otype == 6)
             k.upright &= (!g.relrot || sspd::upright3(g.mat)) && sspd::upright3(p.omat);
+        // cylinder axis vertical (the mover's yaw keeps it so), box upright
+        if (tg == 5 && p.otype == 6)
+            k.cbup &= (!g.relrot || sspd::cyl_vertical(g.mat)) && sspd::upright3(p.omat);
+        if (tg == 6 && p.otype == 5)
+            k.cbup &= (!g.relrot || sspd::upright3(g.mat)) && sspd::cyl_vertical(p.omat);
     }
     return k;
 }
@@ -3072,10 +3088,13 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
                            j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
                            d_status, j->d_part, j->d_sync, d_best)
         const bool og = k.sc.onegeom && k.sc.npairs > 0;
-        if (og && k.sc.cylbox) SSPP_LAUNCH_TSPPP2(true, true);
-        else if (og) SSPP_LAUNCH_TSPPP2(true, false);
-        else if (k.sc.cylbox) SSPP_LAUNCH_TSPPP2(false, true);
-        else SSPP_LAUNCH_TSPPP2(false, false);
+        const int cbm = k.sc.cylbox ? (k.sc.cbup ? 2 : 1) : 0;
+        if (og && cbm == 1) SSPP_LAUNCH_TSPPP2(true, 1);
+        else if (og && cbm == 2) SSPP_LAUNCH_TSPPP2(true, 2);
+        else if (og) SSPP_LAUNCH_TSPPP2(true, 0);
+        else if (cbm == 1) SSPP_LAUNCH_TSPPP2(false, 1);
+        else if (cbm == 2) SSPP_LAUNCH_TSPPP2(false, 2);
+        else SSPP_LAUNCH_TSPPP2(false, 0);
 #undef SSPP_LAUNCH_TSPPP2
         return hipGetLastError();
     }
@@ -3086,10 +3105,13 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
                            j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
                            d_status, j->d_part, j->d_sync, d_best)
         const bool og = k.sc.onegeom && k.sc.npairs > 0;
-        if (og && k.sc.cylbox) SSPP_LAUNCH_TSPPP(true, true);
-        else if (og) SSPP_LAUNCH_TSPPP(true, false);
-        else if (k.sc.cylbox) SSPP_LAUNCH_TSPPP(false, true);
-        else SSPP_LAUNCH_TSPPP(false, false);
+        const int cbm = k.sc.cylbox ? (k.sc.cbup ? 2 : 1) : 0;
+        if (og && cbm == 1) SSPP_LAUNCH_TSPPP(true, 1);
+        else if (og && cbm == 2) SSPP_LAUNCH_TSPPP(true, 2);
+        else if (og) SSPP_LAUNCH_TSPPP(true, 0);
+        else if (cbm == 1) SSPP_LAUNCH_TSPPP(false, 1);
+        else if (cbm == 2) SSPP_LAUNCH_TSPPP(false, 2);
+        else SSPP_LAUNCH_TSPPP(false, 0);
 #undef SSPP_LAUNCH_TSPPP
         return hipGetLastError();
     }
@@ -3098,13 +3120,16 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
                        j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
                        d_status, j->d_part, j->d_sync, d_best)
     const bool og = k.sc.onegeom && k.sc.npairs > 0;
-    const bool up = k.sc.upright && !k.sc.cylbox;
-    if (og && k.sc.cylbox) SSPP_LAUNCH_TSP(true, true, false);
-    else if (og && up) SSPP_LAUNCH_TSP(true, false, true);
-    else if (og) SSPP_LAUNCH_TSP(true, false, false);
-    else if (k.sc.cylbox) SSPP_LAUNCH_TSP(false, true, false);
-    else if (up) SSPP_LAUNCH_TSP(false, false, true);
-    else SSPP_LAUNCH_TSP(false, false, false);
+    const int cbm = k.sc.cylbox ? (k.sc.cbup ? 2 : 1) : 0;
+    const bool up = k.sc.upright && cbm != 1;
+    if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false);
+    else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true); else SSPP_LAUNCH_TSP(true, 2, false); }
+    else if (og && up) SSPP_LAUNCH_TSP(true, 0, true);
+    else if (og) SSPP_LAUNCH_TSP(true, 0, false);
+    else if (cbm == 1) SSPP_LAUNCH_TSP(false, 1, false);
+    else if (cbm == 2) { if (up) SSPP_LAUNCH_TSP(false, 2, true); else SSPP_LAUNCH_TSP(false, 2, false); }
+    else if (up) SSPP_LAUNCH_TSP(false, 0, true);
+    else SSPP_LAUNCH_TSP(false, 0, false);
 #undef SSPP_LAUNCH_TSP
     return hipGetLastError();
 }

@@ -99,6 +99,40 @@ def test_cylinder_box_contact_matches_support_function_reference(margin):
     assert sat7_wrong > 0
 
 
+@pytest.mark.parametrize("margin", [0.0, 0.001, 0.01])
+def test_upright_cylinder_box_matches_support_function_reference(margin):
+    """Vertical cylinder vs upright box (both turned about z only, as a yaw-only TaskSpacePlanner
+    mover keeps them): the oracle takes the prism formula (cb_upright_sd, the device's
+    sspd::cb_upright_sd); its contact and deep decisions must agree with the same independent
+    support-function reference, stacked, side-by-side and corner configurations alike."""
+    rng = np.random.default_rng(70 + int(margin * 1000))
+    n, deep_checked = 0, 0
+    for it in range(450):
+        R, H = rng.uniform(0.02, 0.15), rng.uniform(0.02, 0.15)
+        e = rng.uniform(0.02, 0.2, 3)
+        yc, yb = rng.uniform(-math.pi, math.pi, 2)
+        qc = (math.cos(yc / 2), 0.0, 0.0, math.sin(yc / 2))
+        qb = (math.cos(yb / 2), 0.0, 0.0, math.sin(yb / 2))
+        if it % 3 == 0:  # on top of the box / below it
+            T = np.array([rng.uniform(-1, 1) * (e[0] + R), rng.uniform(-1, 1) * (e[1] + R),
+                          rng.choice([-1, 1]) * (e[2] + H) * rng.uniform(0.9, 1.05)])
+        else:
+            d = rng.normal(size=3)
+            d /= np.linalg.norm(d)
+            T = d * rng.uniform(0.3, 1.05) * (np.linalg.norm(e) + math.hypot(R, H))
+        Mc, Mb = _qmat(qc), _qmat(qb)
+        dist = ref_signed_distance(T, Mc[:, 2], H, R, Mb, e, rng)
+        cont, cost, nd = contacts([(CYL, (R, H, 0), (0, 0, 0), qc, margin)],
+                                  [(BOX, tuple(e), (0, 0, 0), (1, 0, 0, 0))], T, qb)
+        if abs(dist - margin) > 1e-6:
+            n += 1
+            assert (cont > 0) == (dist < margin), (R, H, e, qc, qb, T, dist)
+        if abs(dist - DEEP) > 1e-6:
+            deep_checked += 1
+            assert (nd > 0) == (dist < DEEP), (R, H, e, qc, qb, T, dist)
+    assert n > 400 and deep_checked > 400
+
+
 # ---------------------------------------------------------------- box-box manifold
 BIG = (BOX, (0.3, 0.3, 0.1), (0, 0, 0), (1, 0, 0, 0))
 
