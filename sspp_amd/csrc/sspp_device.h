@@ -309,6 +309,59 @@ SSPP_HD bool sat_box_box(const double* pa, const double* ma, const double* ea, c
 
 // The contact polygon of box_box_deep_count's face case (reference face fi: 0-2 faces of A,
 // 3-5 faces of B): the deep vertices of the incident face clipped to the reference rectangle.
+// The clipping of bb_clip_count in the reference face's (u, v) frame: the incident corners
+// (cu, cv, depth-defining cd), the rectangle |u| <= eu, |v| <= ev.
+SSPP_HD int bb_clip_2d(const double* cu, const double* cv, const double* cd, double eu, double ev) {
+    int nd = 0;
+    // each incident edge clipped to the rectangle |u| <= eu, |v| <= ev (Liang-Barsky with one
+    // reciprocal per direction): its entry point, and its exit point when it leaves early
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int e2 = (e + 1) & 3;
+        const double du = cu[e2] - cu[e], dv = cv[e2] - cv[e];
+        double t0 = 0.0, t1 = 1.0;
+        bool ok = true;
+        if (du == 0.0) {
+            ok = ok && !(cu[e] + eu < 0.0) && !(eu - cu[e] < 0.0);
+        } else {
+            const double r = 1.0 / du;
+            const double ta0 = -(cu[e] + eu) * r, ta1 = (eu - cu[e]) * r;  // u = -eu, u = eu
+            const double lo = du > 0.0 ? ta0 : ta1, hi = du > 0.0 ? ta1 : ta0;
+            if (lo > t0) t0 = lo;
+            if (hi < t1) t1 = hi;
+        }
+        if (dv == 0.0) {
+            ok = ok && !(cv[e] + ev < 0.0) && !(ev - cv[e] < 0.0);
+        } else {
+            const double r = 1.0 / dv;
+            const double tb0 = -(cv[e] + ev) * r, tb1 = (ev - cv[e]) * r;
+            const double lo = dv > 0.0 ? tb0 : tb1, hi = dv > 0.0 ? tb1 : tb0;
+            if (lo > t0) t0 = lo;
+            if (hi < t1) t1 = hi;
+        }
+        if (ok && t0 <= t1) {
+            const double dd = cd[e2] - cd[e];
+            if (-fma(t0, dd, cd[e]) < kDeep) ++nd;
+            if (t1 < 1.0 && -fma(t1, dd, cd[e]) < kDeep) ++nd;
+        }
+    }
+    // ... and the rectangle's corners strictly inside the incident parallelogram
+    const double au = cu[1] - cu[0], av = cv[1] - cv[0], bu = cu[3] - cu[0], bv = cv[3] - cv[0];
+    const double idet = 1.0 / (au * bv - av * bu);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const double qu = (q & 1) ? eu : -eu, qv = (q & 2) ? ev : -ev;
+        const double wu = qu - cu[0], wv = qv - cv[0];
+        const double al = (wu * bv - wv * bu) * idet, be = (au * wv - av * wu) * idet;
+        if (al > 0.0 && al < 1.0 && be > 0.0 && be < 1.0) {
+            const double d = fma(be, cd[3] - cd[0], fma(al, cd[1] - cd[0], cd[0]));
+            if (-d < kDeep) ++nd;
+        }
+    }
+    return nd > 0 ? nd : 1;
+}
+
+
 SSPP_HD int bb_clip_count(const double* pa, const double* ma, const double* ea, const double* pb,
                           const double* mb, const double* eb, int fi) {
     double A[3][3], Bc[3][3];
@@ -368,53 +421,82 @@ SSPP_HD int bb_clip_count(const double* pa, const double* ma, const double* ea, 
         cd[v] = off - dot3(P, n);
     }
     const double eu = pick3(ta, eR[0], eR[1], eR[2]), ev = pick3(tb, eR[0], eR[1], eR[2]);
-    int nd = 0;
-    // each incident edge clipped to the rectangle |u| <= eu, |v| <= ev (Liang-Barsky with one
-    // reciprocal per direction): its entry point, and its exit point when it leaves early
+    return bb_clip_2d(cu, cv, cd, eu, ev);
+}
+
+// bb_clip_count for two upright boxes (see box_box_deep_count_up): the same operations with the
+// products of the rotations' exact zeros dropped.  A z reference face (fi = 2, 5) has the other
+// box's z face as incident face; a side reference face has a side face of the other box as
+// incident face (its z face is exactly orthogonal to n, so never the most anti-parallel).
+SSPP_HD int bb_clip_count_up(const double* pa, const double* ma, const double* ea, const double* pb,
+                             const double* mb, const double* eb, int fi) {
+    // every operand is selected by value (a pointer select or a run-time index into these
+    // register-resident arrays would put them in scratch memory)
+    const bool refA = fi < 3;
+    const int f = refA ? fi : fi - 3;
+    const double R0 = refA ? ma[0] : mb[0], R1 = refA ? ma[1] : mb[1], R3 = refA ? ma[3] : mb[3],
+                 R4 = refA ? ma[4] : mb[4], R8 = refA ? ma[8] : mb[8];
+    const double I0 = refA ? mb[0] : ma[0], I1 = refA ? mb[1] : ma[1], I3 = refA ? mb[3] : ma[3],
+                 I4 = refA ? mb[4] : ma[4], I8 = refA ? mb[8] : ma[8];
+    const double pR0 = refA ? pa[0] : pb[0], pR1 = refA ? pa[1] : pb[1], pR2 = refA ? pa[2] : pb[2];
+    const double pI0 = refA ? pb[0] : pa[0], pI1 = refA ? pb[1] : pa[1], pI2 = refA ? pb[2] : pa[2];
+    const double eR0 = refA ? ea[0] : eb[0], eR1 = refA ? ea[1] : eb[1], eR2 = refA ? ea[2] : eb[2];
+    const double eI0 = refA ? eb[0] : ea[0], eI1 = refA ? eb[1] : ea[1], eI2 = refA ? eb[2] : ea[2];
+    const double dRI0 = pI0 - pR0, dRI1 = pI1 - pR1, dRI2 = pI2 - pR2;
+    double cu[4], cv[4], cd[4], eu, ev;
+    if (f == 2) {
+        double n2 = R8;
+        if (dRI2 * n2 < 0.0) n2 = -n2;
+        const double sg = I8 * n2 > 0.0 ? -eI2 : eI2;
+        const double off = pR2 * n2 + eR2;
+        const double P2 = fma(sg, I8, pI2);
+        const double cdz = off - P2 * n2;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int e2 = (e + 1) & 3;
-        const double du = cu[e2] - cu[e], dv = cv[e2] - cv[e];
-        double t0 = 0.0, t1 = 1.0;
-        bool ok = true;
-        if (du == 0.0) {
-            ok = ok && !(cu[e] + eu < 0.0) && !(eu - cu[e] < 0.0);
-        } else {
-            const double r = 1.0 / du;
-            const double ta0 = -(cu[e] + eu) * r, ta1 = (eu - cu[e]) * r;  // u = -eu, u = eu
-            const double lo = du > 0.0 ? ta0 : ta1, hi = du > 0.0 ? ta1 : ta0;
-            if (lo > t0) t0 = lo;
-            if (hi < t1) t1 = hi;
+        for (int v = 0; v < 4; ++v) {
+            const double c1 = (v == 0 || v == 3) ? eI0 : -eI0;
+            const double c2 = (v < 2) ? eI1 : -eI1;
+            const double P0 = fma(c2, I1, fma(c1, I0, pI0));
+            const double P1 = fma(c2, I4, fma(c1, I3, pI1));
+            const double dp0 = P0 - pR0, dp1 = P1 - pR1;
+            cu[v] = fma(dp1, R3, dp0 * R0);
+            cv[v] = fma(dp1, R4, dp0 * R1);
+            cd[v] = cdz;
         }
-        if (dv == 0.0) {
-            ok = ok && !(cv[e] + ev < 0.0) && !(ev - cv[e] < 0.0);
-        } else {
-            const double r = 1.0 / dv;
-            const double tb0 = -(cv[e] + ev) * r, tb1 = (ev - cv[e]) * r;
-            const double lo = dv > 0.0 ? tb0 : tb1, hi = dv > 0.0 ? tb1 : tb0;
-            if (lo > t0) t0 = lo;
-            if (hi < t1) t1 = hi;
-        }
-        if (ok && t0 <= t1) {
-            const double dd = cd[e2] - cd[e];
-            if (-fma(t0, dd, cd[e]) < kDeep) ++nd;
-            if (t1 < 1.0 && -fma(t1, dd, cd[e]) < kDeep) ++nd;
-        }
-    }
-    // ... and the rectangle's corners strictly inside the incident parallelogram
-    const double au = cu[1] - cu[0], av = cv[1] - cv[0], bu = cu[3] - cu[0], bv = cv[3] - cv[0];
-    const double idet = 1.0 / (au * bv - av * bu);
+        eu = eR0;
+        ev = eR1;
+    } else {
+        double n0 = f ? R1 : R0, n1 = f ? R4 : R3;
+        if (fma(dRI1, n1, dRI0 * n0) < 0.0) { n0 = -n0; n1 = -n1; }
+        const double d0 = fma(I3, n1, I0 * n0), d1 = fma(I4, n1, I1 * n0);
+        const bool k = fabs(d1) > fabs(d0);
+        // Ik: the incident horizontal axis k; Hh: the other horizontal axis (coefficient c1 for
+        // k = 0, c2 for k = 1); the vertical axis takes the other coefficient
+        const double Ik0 = k ? I1 : I0, Ik1 = k ? I4 : I3;
+        const double Hh0 = k ? I0 : I1, Hh1 = k ? I3 : I4;
+        const double eIk = k ? eI1 : eI0;
+        const double sg = (k ? d1 : d0) > 0.0 ? -eIk : eIk;
+        const double eK1 = k ? eI2 : eI1, eK2 = k ? eI0 : eI2;  // eI[k1], eI[k2]
+        const double off = fma(pR1, n1, pR0 * n0) + (f ? eR1 : eR0);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const double qu = (q & 1) ? eu : -eu, qv = (q & 2) ? ev : -ev;
-        const double wu = qu - cu[0], wv = qv - cv[0];
-        const double al = (wu * bv - wv * bu) * idet, be = (au * wv - av * wu) * idet;
-        if (al > 0.0 && al < 1.0 && be > 0.0 && be < 1.0) {
-            const double d = fma(be, cd[3] - cd[0], fma(al, cd[1] - cd[0], cd[0]));
-            if (-d < kDeep) ++nd;
+        for (int v = 0; v < 4; ++v) {
+            const double c1 = (v == 0 || v == 3) ? eK1 : -eK1;
+            const double c2 = (v < 2) ? eK2 : -eK2;
+            const double ch = k ? c2 : c1, cz = k ? c1 : c2;
+            const double P0 = fma(ch, Hh0, fma(sg, Ik0, pI0));
+            const double P1 = fma(ch, Hh1, fma(sg, Ik1, pI1));
+            const double P2 = fma(cz, I8, pI2);
+            const double dp0 = P0 - pR0, dp1 = P1 - pR1, dp2 = P2 - pR2;
+            const double hz = dp2 * R8;  // along the reference box's z axis
+            // f = 0: Ta = axis 1 (horizontal), Tb = z;  f = 1: Ta = z, Tb = axis 0 (horizontal)
+            const double hh = f == 0 ? fma(dp1, R4, dp0 * R1) : fma(dp1, R3, dp0 * R0);
+            cu[v] = f == 0 ? hh : hz;
+            cv[v] = f == 0 ? hz : hh;
+            cd[v] = off - fma(P1, n1, P0 * n0);
         }
+        eu = f == 0 ? eR1 : eR2;
+        ev = f == 0 ? eR2 : eR0;
     }
-    return nd > 0 ? nd : 1;
+    return bb_clip_2d(cu, cv, cd, eu, ev);
 }
 
 // Box-box deep contacts (TaskSpacePlanner cost: Collision.h:89-101 adds one term per contact
@@ -562,7 +644,7 @@ SSPP_HD int box_box_deep_count_up(const double* pa, const double* ma, const doub
 #ifdef SSPP_NO_MANIFOLD
     return 1;
 #endif
-    return bb_clip_count(pa, ma, ea, pb, mb, eb, fi);
+    return bb_clip_count_up(pa, ma, ea, pb, mb, eb, fi);
 }
 
 // Both rotations upright (see box_box_deep_count_up)?

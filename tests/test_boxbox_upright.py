@@ -1,7 +1,8 @@
-"""k_tsp's upright box-box specialisation (sspd::box_box_deep_count_up, used by k_tsp<..., UP>
-when every box-box pair of a TaskSpacePlanner job is upright for its yaw-only mover) returns the
-deep-contact count of the generic sspd::box_box_deep_count bit for bit: it only drops products
-with the exact zeros of upright rotations from the same fma chains.  Checked on the host build
+"""k_tsp's upright box-box specialisation (sspd::box_box_deep_count_up and its contact-polygon
+clip sspd::bb_clip_count_up, used by k_tsp<..., UP> when every box-box pair of a
+TaskSpacePlanner job is upright for its yaw-only mover) returns the deep-contact count of the
+generic sspd::box_box_deep_count bit for bit: it only drops products with the exact zeros of
+upright rotations from the same fma chains (z-face and side-face reference faces).  Checked on the host build
 of sspp_device.h over random upright pairs (stacked, side by side, anywhere within reach;
 identity, yawed and z-flipped boxes, both argument orders), whose counts span 0..8."""
 import os
