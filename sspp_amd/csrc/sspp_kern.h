@@ -991,6 +991,7 @@ struct SsppC2F {
     int ctrl_feas; // ctrl_out rows only for candidates with no contact (written at the end)
     // fused survivor queue (k_sspp_c2f<..., FQ = true>, one-wave workgroups): phase 1's survivors
     // become items of the job's work-queue buffers, drained by every workgroup of the launch
+    int p1cap;     // > 0: phase 1 runs at most p1cap wave pair iterations (SSPP_P1CAP)
     int fq, fq_npg, fq_nchunk, fq_gs, fq_gcap;
     unsigned fq_nps;
     struct FqGroup* fq_grp;   // [steps][groups per step]
@@ -1017,7 +1018,8 @@ struct SsppC2F {
 template <int D, int NM, bool ONEGEOM>
 __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned long long mymask,
                                            unsigned long long umask, unsigned long long gbits,
-                                           int* flag, const KScene& sc, const SceneT& T, bool& dfr) {
+                                           int* flag, const KScene& sc, const SceneT& T, bool& dfr,
+                                           int maxit = 1 << 30) {
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
     double mp[NM][3], mR[NM][9];
@@ -1084,6 +1086,7 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
         if (flag && live && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
             live = false;
         if (__ballot(live) == 0ull) break;
+        if (--maxit == 0) break;  // capped phase 1: the rest is phase 2's (k_sspp_c2f p1cap)
     }
     return ghit;
 }
@@ -1316,7 +1319,8 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             const bool live = valid && l < a.n1 && !a.sc.static_block && !(a.ablate & 16);
             double q[D];
             eval_pt_r<D, P>(s_ctrl + (valid ? g : 0) * ndof, N_p1, span_p1, q);
-            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mymask, umask, gbits, nullptr, a.sc, TT, dfr);
+            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mymask, umask, gbits, nullptr, a.sc, TT, dfr,
+                                              a.p1cap > 0 ? a.p1cap : (1 << 30));
         }
         const bool gdef = (__ballot(dfr) & gbits) != 0ull;
         if (l == 0) {
@@ -1332,7 +1336,10 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         return;
     }
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
-    const int R = a.npts - a.n1;
+    // p1cap: phase 1 stopped after p1cap pair iterations, so its undecided candidates are
+    // survivors whose every waypoint phase 2 checks (the OR over waypoints is unchanged)
+    const int j0 = a.p1cap > 0 ? 0 : a.n1;
+    const int R = a.npts - j0;
     if (collide_on && R > 0 && !(a.ablate & 8)) {
         if (tid < 64) {  // survivors compacted by one wave ballot (cpb <= 64), in candidate order
             const bool f = tid < nvalid && s_feas[tid] != 0;
@@ -1403,7 +1410,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             bool live = it < items;
             const int si = live ? it / R : 0;
             const int s = s_surv[si];
-            const int j = a.n1 + (live ? it - si * R : 0);
+            const int j = j0 + (live ? it - si * R : 0);
             live = live && __hip_atomic_load(s_feas + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
             // lanes of this wave that work on the same survivor
             const int wave_it0 = base + (tid & ~63) - grp * stride;
@@ -2815,6 +2822,7 @@ struct sspp_job {
     // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
     int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16, nt2 = 256;
     int fq = 0, fq_npg = 1, fq_gs = 16;  // k_sspp_c2f fused survivor queue (SSPP_FQ, SSPP_FQ_NPG, SSPP_FQ_GS)
+    int p1cap = 0;                       // k_sspp_c2f phase-1 iteration cap (SSPP_P1CAP)
     FqGroup* d_fqgrp = nullptr;          // its group counters and queues (zero between launches)
     unsigned* d_fqq = nullptr;
     int64_t fq_ngrp = 0, fq_nq = 0;

@@ -598,6 +598,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     { const char* e = getenv("SSPP_FQ"); j->fq = e ? atoi(e) : 0; }
     { const char* e = getenv("SSPP_FQ_NPG"); j->fq_npg = e ? std::max(1, std::min(8, atoi(e))) : 1; }
     { const char* e = getenv("SSPP_FQ_GS"); j->fq_gs = e ? std::max(1, std::min(256, atoi(e))) : 16; }
+    { const char* e = getenv("SSPP_P1CAP"); j->p1cap = e ? std::max(0, atoi(e)) : 0; }
     // default: c2f draws inside the scoring kernel (SSPP_INSAMPLE=0: chip-wide k_sample_sspp; measured slower)
     { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : (j->c2f ? 1 : 0); }
     { const char* e = getenv("SSPP_HULL"); j->hull = e ? atoi(e) : 2; }
@@ -827,6 +828,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         c.hull = j->hull;
         c.dfr = j->d_dfr;
         c.ctrl_feas = j->ctrl_feas;
+        c.p1cap = j->p1cap;
         // fused survivor queue: the throughput shape (one-wave workgroups) on sampled candidates
         // whose pair table needs no later fixup (no cylinder-box deferral, <= 64 pairs)
         if (j->fq && !j->wq && nt == 64 && !d_ctrl && j->insample && !j->arc_all && c.npts > c.n1 &&
@@ -853,6 +855,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
                 j->fq_ngrp = ngrp; j->fq_nq = ngrp * gcap;
             }
             c.fq = 1;
+            c.p1cap = 0;
             c.fq_npg = std::min(j->fq_npg, c.sc.npairs);
             c.fq_nchunk = (c.npts - c.n1 + 63) / 64;
             c.fq_nps = (unsigned)(c.fq_nchunk * c.fq_npg);

@@ -416,6 +416,28 @@ def test_fused_queue_matches_oracle(robocrane, monkeypatch, fq, npg, gs, sigma, 
     assert wq_error(job) == 0
 
 
+@pytest.mark.parametrize("cap", ["1", "2", "3"])
+@pytest.mark.parametrize("nt,g1", [("64", "4"), ("256", "64")])
+def test_phase1_cap_matches_oracle(robocrane, monkeypatch, cap, nt, g1):
+    """k_sspp_c2f with phase 1 capped at `cap` pair iterations (SSPP_P1CAP): the candidates it
+    leaves undecided go to phase 2 with every waypoint; feasibility, arcs and the argmin stay
+    the oracle's."""
+    import sspp_amd as S
+    monkeypatch.setenv("SSPP_P1CAP", cap)
+    monkeypatch.setenv("SSPP_NT", nt)
+    monkeypatch.setenv("SSPP_G1", g1)
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    B = 4096
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=B)
+    r = run_sspp(job, B, first=99 * B)
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 128)
+    np.testing.assert_array_equal(r["feasible"], feas_o)
+    assert arc_err(r["arc"], arc_o) <= COST_TOL
+    k, _ = O.argmin(arc_o, feas_o)
+    assert r["best"][1] == (99 * B + k if k >= 0 else -1)
+
+
 @pytest.mark.parametrize("kernel", ["2", "1"])
 def test_fp32_sampler_opt_in(robocrane, monkeypatch, kernel):
     """The opt-in FP32 Box-Muller quads (sampler = 1): candidates bit-identical to the oracle's
