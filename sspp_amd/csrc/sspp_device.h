@@ -1111,9 +1111,9 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
     // box-box: SAT (exact for boxes) decides contact; deep contacts: one pass, SAT + manifold
     if (NEED_DEEP) {
         SSPP_NP_STAT(13);
-        // UP: every box-box pair of the job is upright; otherwise the pairs that are (a yaw-only
-        // mover's upright geoms against upright boxes) still take the bit-identical upright form
-        if (UP || (upright3(m1) && upright3(m2)))
+        // UP: every box-box pair of the job is upright (a per-pair run-time dispatch for the
+        // generic kernels measured neutral on multi-goal: 31.4-31.5 vs 31.8 M cand/s)
+        if (UP)
             *nd = (margin >= kDeep || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
                       ? box_box_deep_count_up(p1, m1, s1, p2, m2, s2) : 0;
         else
