@@ -3,6 +3,8 @@
 // The kernels are in sspp_kern.h; their instantiations are compiled per dof in sspp_inst.hip.
 #include "sspp_kern.h"
 
+#include <random>
+
 using namespace sspk;
 
 #ifndef SSPP_SINGLE_TU
@@ -420,6 +422,98 @@ static std::vector<DPair> pairs_for_job(const sspp_scene* sc, const double* knot
     return sorted;
 }
 
+// Pair order by phase-1 hits (SSPP_PAIR_ORDER=2, the default at job creation): M host-sampled candidates (the
+// job's sigma / limits, a host normal generator — the order only steers the scan, never its
+// result), their first n1 coarse-to-fine waypoints, and per candidate the set of pairs in contact
+// at any of them; the pairs are then ordered greedily, each time the one that settles the most
+// candidates not yet settled (phase 1 stops a candidate at its first contact), the rest in
+// their previous order.
+static std::vector<DPair> order_by_hits(const sspp_scene* sc, const std::vector<DPair>& in, const double* knots,
+                                        int nknots, int p, const double* ctrl0, int D, double sigma,
+                                        const double* limits, const std::vector<int>& wps, int W) {
+    const int np = (int)in.size(), n = nknots - p - 1, nm = (int)sc->movers.size();
+    if (np < 2 || np > 64 || nm < 1 || nm > kMaxMovers) return in;
+    const int M = 256;
+    std::mt19937_64 rng(0x5EEDull);
+    std::normal_distribution<double> N01(0.0, 1.0);
+    std::vector<uint64_t> hit(M, 0ull);
+    std::vector<double> c((size_t)n * D);
+    for (int m = 0; m < M; ++m) {
+        for (size_t e = 0; e < c.size(); ++e) c[e] = ctrl0[e];
+        for (int jj = p; jj < n - p; ++jj)
+            for (int d = 0; d < D; ++d) c[(size_t)jj * D + d] += sigma * N01(rng) * limits[d];
+        for (int w : wps) {
+            const double u = (double)w / W;
+            const int sp = span_of(u, p, knots, nknots);
+            double N[kMaxP + 1];
+            basis_funcs(u, p, sp, knots, N);
+            double q[16] = {0};
+            for (int d = 0; d < D && d < 16; ++d) {
+                double acc = 0.0;
+                for (int r = 0; r <= p; ++r) {
+                    const int jj = sp - p + r;
+                    if (jj >= 0 && jj < n) acc += N[r] * c[(size_t)jj * D + d];
+                }
+                q[d] = acc;
+            }
+            double mp[kMaxMovers][3], mR[kMaxMovers][9];
+            for (int mv = 0; mv < nm; ++mv) {
+                double qp[7];
+                for (int k = 0; k < 7; ++k) qp[k] = (7 * mv + k < D) ? q[7 * mv + k] : sc->movers[mv].qpos0[k];
+                normalize4(qp + 3);
+                quat2mat(qp + 3, mR[mv]);
+                for (int k = 0; k < 3; ++k) mp[mv][k] = qp[k];
+            }
+            for (int k = 0; k < np; ++k) {
+                if ((hit[m] >> k) & 1ull) continue;
+                const DPair& pr = in[k];
+                const DGeom& G = sc->geoms[pr.gm];
+                const int mv = G.mover > 0 ? G.mover : 0;
+                double gp[3], gm[9], t3[3], op[3], om[9];
+                matvec3(mR[mv], G.pos, t3);
+                for (int d = 0; d < 3; ++d) gp[d] = mp[mv][d] + t3[d];
+                if (G.relrot) matmul3(mR[mv], G.mat, gm);
+                else for (int e = 0; e < 9; ++e) gm[e] = mR[mv][e];
+                if (pr.omover >= 0) {
+                    matvec3(mR[pr.omover], pr.opos, t3);
+                    for (int d = 0; d < 3; ++d) op[d] = mp[pr.omover][d] + t3[d];
+                    matmul3(mR[pr.omover], pr.omat, om);
+                } else {
+                    for (int d = 0; d < 3; ++d) op[d] = pr.opos[d];
+                    for (int e = 0; e < 9; ++e) om[e] = pr.omat[e];
+                }
+                if (G.rbound > 0.0 && pr.orbound > 0.0) {  // the bounding-sphere test
+                    const double dx = op[0] - gp[0], dy = op[1] - gp[1], dz = op[2] - gp[2];
+                    const double thr = G.rbound + pr.orbound + pr.margin;
+                    if (dx * dx + dy * dy + dz * dz > thr * thr) continue;
+                }
+                int nd = 0;
+                const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
+                const int nc = gfirst ? collide<false>(G.type, gp, gm, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd)
+                                      : collide<false>(pr.otype, op, om, pr.osize, G.type, gp, gm, G.size, pr.margin, &nd);
+                if (nc > 0) hit[m] |= 1ull << k;
+            }
+        }
+    }
+    std::vector<char> used(np, 0), settled(M, 0);
+    std::vector<DPair> out;
+    for (;;) {
+        int best = -1, bc = 0;
+        for (int k = 0; k < np; ++k) {
+            if (used[k]) continue;
+            int cnt = 0;
+            for (int m = 0; m < M; ++m) cnt += !settled[m] && ((hit[m] >> k) & 1ull);
+            if (cnt > bc) { bc = cnt; best = k; }
+        }
+        if (best < 0) break;
+        used[best] = 1;
+        out.push_back(in[best]);
+        for (int m = 0; m < M; ++m) if ((hit[m] >> best) & 1ull) settled[m] = 1;
+    }
+    for (int k = 0; k < np; ++k) if (!used[k]) out.push_back(in[k]);
+    return out;
+}
+
 // Pairs a SAMPLED candidate can reach (job-level broadphase, exact).  sampleWithNoise moves
 // control point (j, d), j in [p, n - p), by (sigma z) limits(d) with |z| <= 8.5722 (FP64
 // Box-Muller: u1 >= 2^-53) or 5.7683 (FP32 quads: u1 >= 2^-24); every other control point is the
@@ -513,8 +607,18 @@ static int upload_basis(const std::vector<double>& us, int p, const double* knot
 static int set_job_pairs(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, bool create,
                          void* stream, size_t pin_off) {
     const sspp_scene* sc = j->scene;
-    const char* po = getenv("SSPP_PAIR_ORDER");  // 0 = scene order (profiling)
-    j->h_pairs = (po && atoi(po) == 0) ? sc->pairs : pairs_for_job(sc, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D);
+    // SSPP_PAIR_ORDER: 0 = scene order (profiling), 1 = mean-path gap order, 2 = phase-1 hit order
+    // on top of it.  Default: 2 when the job is created (a few ms of host work, paid once), 1 on
+    // sspp_job_update (a re-plan at a new query stays on the microsecond host path).
+    const char* po = getenv("SSPP_PAIR_ORDER");
+    const int order = po ? atoi(po) : (create ? 2 : 1);
+    j->h_pairs = order == 0 ? sc->pairs : pairs_for_job(sc, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D);
+    if (order == 2 && j->kind == 0) {
+        std::vector<int> wps = c2f_order(j->W);
+        wps.resize(std::min<size_t>(wps.size(), (size_t)std::max(1, j->g1)));
+        j->h_pairs = order_by_hits(sc, j->h_pairs, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D, sigma,
+                                   limits, wps, j->W);
+    }
     const char* pr = getenv("SSPP_REACH");  // 0 = no job-level culling (profiling)
     j->h_pairs_s = (pr && atoi(pr) == 0) ? j->h_pairs
                                          : reachable_pairs(sc, j->h_pairs, init_ctrl, j->n, j->D, j->p, sigma, limits, j->sampler);
