@@ -1,8 +1,12 @@
 """Benchmark: candidate paths scored per second (BASELINE.json metric), MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config robocrane|stacking]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config robocrane|stacking|multigoal]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+--gpus N means N ranks, one per GPU: run without WORLD_SIZE and N > 1, bench.py starts itself
+under torch.distributed.run as a child process (before anything touches a GPU), forwards its
+output and exits with its status; under a launcher, WORLD_SIZE must equal N.
 
 A step is one pass of the hot path over one batch of synthetic candidates: on-device Philox
 sampling of the perturbed control points, B-spline evaluation, free-joint FK, collision against
@@ -36,7 +40,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6    # FP64 vector (VALU) spec
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None,
@@ -66,7 +70,7 @@ def parse():
     ap.add_argument("--steps-per-launch", type=int, default=32,
                     help="native mode: independent steps (each its own B candidates, outputs and "
                          "argmin) grouped into one kernel launch")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     if a.steps is None and a.mode == "tsp-anytime":
         a.steps = 10  # trials per budget and mode
     if a.steps is None:
@@ -124,9 +128,10 @@ def setup_robocrane(args, device):
     flops_per = (2 * W + 1) * 2 * (p + 1) * D + (W - 1) * (3 * D + 1) + \
         (W + 1) * (40 + 42 + 48 + 8 * 450 + 300)
     meta = dict(workload="robocrane SamplingPathPlanner7 (block_green free joint), sigma 0.08",
-                candidates_per_gpu=B, waypoints=W, init_points=n_, degree=p, dof=D,
-                sampler=args.sampler)
-    ctx = dict(kind="sspp", kernel_name="k_sspp_c2f" if os.environ.get("SSPP_KERNEL", "1") != "0" else "k_sspp",
+                candidates_per_gpu=B, waypoints=W, init_points=n_, degree=p, dof=D)
+    # the job's effective configuration (sampler, launch shape, scan orders, the creation's
+    # hit-order pre-pass), read back from the library after the timed region
+    ctx = dict(kind="sspp", kernel_name="k_sspp_c2f", effective=job.config,
                job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p,
                make_executor=make_executor,
                per_launch=B * (args.steps_per_launch if args.mode == "native" else 1))
@@ -614,14 +619,52 @@ def cpu_baseline_anytime(args, model, q0, qT):
                 **cpu_info())
 
 
-def main():
-    args = parse()
+def rank_launch_cmd(argv, n, port):
+    """The child command of `bench.py --gpus N` run without a launcher: this script under
+    torch.distributed.run with N ranks on one node (same arguments)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 without WORLD_SIZE: start the N ranks as a child process (subprocess, no
+    exec, nothing has touched the GPU yet) and return its exit status."""
+    import socket
+    import subprocess
+    import torch
+    visible = torch.cuda.device_count()  # counts devices without initialising them
+    if visible < args.gpus:
+        print("bench.py: --gpus %d needs %d visible GPUs, found %d" % (args.gpus, args.gpus, visible),
+              file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    sys.stdout.flush()
+    return subprocess.call(rank_launch_cmd(argv, args.gpus, port))
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if world_env is None and args.gpus > 1:
+        if args.mode in ("dropin", "tsp-anytime"):
+            print("bench.py: --mode %s is a single-GPU latency benchmark" % args.mode, file=sys.stderr)
+            return 2
+        return launch_ranks(args, argv)
+    if world_env is not None and int(world_env) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" % (world_env, args.gpus), file=sys.stderr)
+        return 2
     if args.mode == "dropin":
         run_dropin(args)
-        return
+        return 0
     if args.mode == "tsp-anytime":
         run_tsp_anytime(args)
-        return
+        return 0
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -630,6 +673,7 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        world = dist.get_world_size()  # the ranks that joined
     device = torch.device("cuda", local)
     import sspp_amd as S
 
@@ -712,6 +756,11 @@ def main():
                 rec.get("candidates_per_launch") == per_launch:
             traffic, traffic_src = rec["hbm_bytes_per_launch"], rec["source"]
 
+    if "effective" in ctx:
+        meta.update(ctx["effective"]())
+    lib_path = os.environ.get("SSPP_LIB_PATH")
+    if lib_path:  # a variant build (profiling only): say so on the line
+        meta["library"] = lib_path
     if rank == 0:
         total = args.steps * B * world
         if ctx["kind"] == "multigoal":
@@ -735,6 +784,7 @@ def main():
             "value": value,
             "unit": "candidate paths/s",
             "n_gpus": world,
+            "ranks_joined": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -775,7 +825,8 @@ def main():
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -199,9 +199,34 @@ int sspp_job_tsp_score_vias(sspp_job* job, const double* d_vias /* [B][K][4] */,
                             int64_t first_id, int64_t B, double* d_L, double* d_Cnf,
                             double* d_Cwf, uint8_t* d_status, double* d_cost, sspp_best* d_best,
                             void* stream);
+/* SamplingPathPlanner jobs: the last (or, before any launch, the throughput) k_sspp_c2f shape —
+ * lanes_per_candidate = phase-1 lanes G1; TaskSpacePlanner jobs: k_tsp's lanes per candidate */
 int sspp_job_info(const sspp_job* job, int* lanes_per_candidate, int* candidates_per_block,
                   int* block_threads, size_t* lds_bytes);
 void sspp_job_free(sspp_job* job);
+
+/* Explicit job options (tests and tuning; the library reads no environment variables).
+ * Nothing here changes a result: every option selects among bit-identical evaluation orders or
+ * kernel forms.  sspp_job_get_option also reads back the effective configuration.          */
+#define SSPP_OPT_SHAPE_NT 1     /* k_sspp_c2f threads per workgroup: 64 or 256; 0 = per launch  */
+#define SSPP_OPT_SHAPE_G1 2     /* phase-1 lanes per candidate 1..64; 0 = per launch            */
+#define SSPP_OPT_ORDER 3        /* scan order: 0 scene / bisection, 1 mean-path gap (pairs),
+                                   2 hit order (waypoints + pairs, host pre-pass; the default of
+                                   sampled jobs, sigma > 0); setting it rebuilds the tables
+                                   (synchronous)                                               */
+#define SSPP_OPT_TSP_FORM 4     /* TaskSpacePlanner: -1 by batch size, 0 k_tsp, 1 k_tsp_pp,
+                                   2 k_tsp_pp2 (where it applies); get: the last launch's form */
+#define SSPP_OPT_TSP_GENERIC 5  /* TaskSpacePlanner: 1 = generic box-box / cylinder-box code even
+                                   where every pair is upright                                 */
+#define SSPP_OPT_SAMPLER 6      /* get: the job's sampler (sspp_sspp_args::sampler)             */
+#define SSPP_OPT_LAST_NT 7      /* get: threads per workgroup of the last k_sspp_c2f launch     */
+#define SSPP_OPT_LAST_G1 8      /* get: phase-1 lanes per candidate of that launch              */
+#define SSPP_OPT_WP_ORDER 9     /* get: collision-waypoint order (0 bisection, 2 hit order)     */
+#define SSPP_OPT_PREPASS_US 10  /* get: host microseconds of the creation's hit-order pre-pass  */
+#define SSPP_OPT_NPAIRS 11      /* get: pairs in the sampled-candidate table                    */
+#define SSPP_OPT_CYLBOX 12      /* get: that table has cylinder-box pairs (k_sspp_c2f settles them) */
+int sspp_job_set_option(sspp_job* job, int key, int64_t value);
+int sspp_job_get_option(const sspp_job* job, int key, int64_t* value);
 
 /* ---- TaskSpacePlanner CES iteration on the device (tsp::Planner::plan) ----
  * An iteration's candidate list is [mean set, forwarded best (iterate && last_best), samples]
@@ -263,6 +288,10 @@ int sspp_ces_read(sspp_ces* ces, sspp_ces_state* state, double* L, double* C_nf,
                   double* last_best, int32_t* elites);     /* synchronous; outputs nullable */
 int sspp_ces_set_state(sspp_ces* ces, const double* mean, const double* sigma,
                        const double* last_best, int has_best /* -1 = keep */);
+/* SSPP_OPT_CES_FUSED: 1 (default) small slot lists rank their successes inside k_ces_update
+ * (3 launches per iteration), 0 the rank / scatter kernels (5 launches); bit-identical.     */
+#define SSPP_OPT_CES_FUSED 101
+int sspp_ces_set_option(sspp_ces* ces, int key, int64_t value);
 void sspp_ces_free(sspp_ces* ces);
 
 /* Re-target a SamplingPathPlanner job (same knots, dof, check_points) to new initial control
@@ -339,11 +368,6 @@ int sspp_score_ctrl_host(const sspp_scene* scene, const double* knots, int degre
 int sspp_sample_ctrl_host(const double* knots, int degree, const double* init_ctrl, int n, int D,
                           double sigma, const double* limits, uint64_t seed, int64_t first_id,
                           int64_t B, double* ctrl_out /* [B][n][D] */);
-
-/* ---- diagnostics ---- */
-/* spin-timeout word of a job's work-queue kernel: 0 = every wait of its in-launch hand-off was
- * satisfied (tests assert this); synchronous */
-int sspp_debug_job_error(const sspp_job* job);
 
 #ifdef __cplusplus
 }

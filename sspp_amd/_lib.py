@@ -150,8 +150,16 @@ SIGNATURES = {
     "sspp_ces_pack": (C.c_int, [_vp, _i, _vp, _vp]),
     "sspp_ces_unpack": (C.c_int, [_vp, _vp, _vp]),
     "sspp_ces_free": (None, [_vp]),
-    "sspp_debug_job_error": (C.c_int, [_vp]),
+    "sspp_job_set_option": (C.c_int, [_vp, _i, _i64]),
+    "sspp_job_get_option": (C.c_int, [_vp, _i, C.POINTER(_i64)]),
+    "sspp_ces_set_option": (C.c_int, [_vp, _i, _i64]),
 }
+
+# job options (include/sspp_hip.h SSPP_OPT_*)
+OPT_SHAPE_NT, OPT_SHAPE_G1, OPT_ORDER, OPT_TSP_FORM, OPT_TSP_GENERIC = 1, 2, 3, 4, 5
+OPT_SAMPLER, OPT_LAST_NT, OPT_LAST_G1, OPT_WP_ORDER, OPT_PREPASS_US, OPT_NPAIRS = 6, 7, 8, 9, 10, 11
+OPT_CYLBOX = 12
+OPT_CES_FUSED = 101
 
 
 def declared_symbols(header=HEADER_PATH):

@@ -491,6 +491,7 @@ struct sspp_ces {
     unsigned char* h_stage = nullptr;   // pinned: k_ces_stage's output
     size_t stage_bytes = 0;
     long long staged_iter = -1;         // iteration whose results k_ces_update already staged
+    int fused = 1;                      // SSPP_OPT_CES_FUSED (sspp_ces_set_option)
 };
 
 static CesK ces_k(const sspp_ces* p) {
@@ -505,6 +506,16 @@ static CesK ces_k(const sspp_ces* p) {
 }
 
 extern "C" {
+
+int sspp_ces_set_option(sspp_ces* p, int key, int64_t value) {
+    sspp::clear_error();
+    if (!p) return sspp::set_error(SSPP_E_INVAL, "null planner");
+    if (key == SSPP_OPT_CES_FUSED) {
+        p->fused = value ? 1 : 0;
+        return SSPP_OK;
+    }
+    return sspp::set_error(SSPP_E_INVAL, "unknown option");
+}
 
 void sspp_ces_free(sspp_ces* p) {
     if (!p) return;
@@ -664,7 +675,7 @@ int sspp_ces_update(sspp_ces* p, void* stream) {
     const int nt = (p->nslots + kRankTile - 1) / kRankTile;
     hipStream_t st = (hipStream_t)stream;
     p->last = st;
-    const int fused = p->nslots <= kCesThreads && !std::getenv("SSPP_CES_UNFUSED");
+    const int fused = p->nslots <= kCesThreads && p->fused;
     if (!fused) {
         hipLaunchKernelGGL(k_ces_rank, dim3(nt, nt), dim3(kRankTile), 0, st, p->nslots, p->d_cost,
                            p->d_status, p->d_rank, p->d_nsucc);

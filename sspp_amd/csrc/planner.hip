@@ -196,8 +196,9 @@ extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const dou
         (rc = hipck(hipStreamSynchronize(p->stream), "plan")))
         return rc;
     // the feasible candidates in candidate order (findBestPath's input, include/sspp.h:215-216)
-    // and findBestPath itself (include/sspp.h:171-192): the lowest arc length, ties to the
-    // lowest id (the first in candidate order) — the device argmin's (cost, id) order
+    // and findBestPath itself (include/sspp.h:171-192): a path is taken when its arc length is
+    // below the running minimum, which starts at +inf (an infinite or NaN arc is never taken);
+    // ties to the lowest id (the first in candidate order) — the device argmin's (cost, id) order
     const size_t nd = (size_t)init_points * p->D;
     const unsigned char* f = p->h_feas.p;
     long long cnt = 0;
@@ -206,7 +207,7 @@ extern "C" int sspp_planner_plan(sspp_planner* p, const double* start, const dou
     for (int64_t i = 0; i < sample_count; ++i) {
         if (f[i] != 1) continue;
         const double a = p->h_arc.p[i];
-        if (bi < 0 || a < bc) { bc = a; bi = first_id + i; }
+        if (a < bc) { bc = a; bi = first_id + i; }
         if (feasible_ids) feasible_ids[cnt] = first_id + i;
         if (feasible_arc) feasible_arc[cnt] = a;
         if (feasible_ctrl) std::memcpy(feasible_ctrl + cnt * nd, p->h_ctrl.p + i * nd, sizeof(double) * nd);

@@ -2,25 +2,22 @@
 //
 // Included by sspp_kernels.hip (host side: scenes, jobs, the C ABI) and by sspp_inst.hip,
 // which the Makefile compiles once per dof (-DSSPK_D=1,2,3,4,6,7,9) and once for the
-// TaskSpacePlanner kernel (-DSSPK_D=0), each explicitly instantiating its entry points, so the
-// ~200 kernel instantiations compile in parallel.  Variant builds (tools/build_variant.sh)
-// define SSPP_SINGLE_TU and instantiate everything in sspp_kernels.hip.
-//
+// TaskSpacePlanner kernels (-DSSPK_D=0), each explicitly instantiating its entry points, so the
+// kernel instantiations compile in parallel.  Variant builds (tools/build_variant.sh, profiling
+// and ablation only) define SSPP_SINGLE_TU and instantiate everything in sspp_kernels.hip.
 //
 // Hot path (reference include/sspp.h:194-225 and include/sspp/tsp_planner.h:95-138):
 //   candidate sampling -> B-spline evaluation -> free-joint FK -> collision -> cost -> argmin.
 //
-// Work decomposition:
-//   * a candidate owns LPC = 64*ceil(items/64) lanes (capped at 256), one waypoint per lane;
-//     a 256-thread workgroup holds CPB = 256/LPC candidates;
-//   * the workgroup prologue builds the shared basis tables (span + N_0..N_p for every
-//     waypoint parameter) and the candidates' control points in LDS (Philox + Box-Muller
-//     in-kernel, or a coalesced copy of caller-supplied control points);
-//   * each lane evaluates its waypoint(s): spline from LDS, FK of the moving body, pair
-//     loop over the scene table (wave-uniform -> scalar loads), broadphase + narrowphase;
+//   * k_sspp_c2f (SamplingPathPlanner): a workgroup holds CPB candidates; control points in
+//     LDS (Philox + Box-Muller in-kernel, or a coalesced copy of caller-supplied splines), a
+//     coarse-to-fine waypoint order with G1 lanes per candidate first, then the survivors'
+//     remaining waypoints over the whole workgroup;
+//   * k_tsp / k_tsp_pp / k_tsp_pp2 (TaskSpacePlanner): one waypoint per lane, the scene's pairs
+//     in a wave-uniform loop (scalar loads), deep-contact costs;
 //   * per-candidate sums use the canonical order (lane partials, xor butterfly per wave,
 //     waves in order) that oracle/sspp_oracle.c::or_canon_sum restates;
-//   * one BlockBest per workgroup, then a one-block argmin kernel (lowest id on ties).
+//   * one BlockBest per workgroup, reduced by the last workgroup to arrive (lowest id on ties).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -37,13 +34,6 @@ __device__ unsigned long long g_c2f_stats[16];
 #define SSPP_CB_STAT(i) atomicAdd(&g_c2f_stats[i], 1ull)
 #endif
 #ifdef SSPP_WG_TIMING  // profiling builds only: per-workgroup (start, end, CU, survivors) of k_sspp_c2f
-__device__ unsigned long long g_wq_t[8 << 16];  // k_sspp_wq1 tiles / k_sspp_wq2 items: 8 stamps each
-__device__ unsigned long long g_wq_i[8 << 16];
-#define WQ_T(arr, idx, k, v) do { if (threadIdx.x == 0 && (idx) < (1u << 16)) arr[8 * (idx) + (k)] = (v); } while (0)
-#else
-#define WQ_T(arr, idx, k, v) do { } while (0)
-#endif
-#ifdef SSPP_WG_TIMING
 __device__ unsigned long long g_wg_t[1 << 18];
 __device__ unsigned long long g_wg_ph[8 << 16];  // per workgroup: shader clock after each phase
 #define WG_PH(k) do { if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_wg_ph[8 * blockIdx.x + (k)] = clock64(); } while (0)
@@ -202,20 +192,6 @@ struct BlockBest {
     long long idx;
     long long count;
     long long pad;
-};
-
-struct SsppK {
-    KScene sc;
-    int has_scene;
-    int ablate;    // profiling only (SSPP_ABLATE env): 1 no sampling, 2 no collision, 4 no arc
-    int insample;  // draw the candidates inside the scoring kernel (else k_sample_sspp)
-    int sampler;   // 0 FP64 Box-Muller pairs (default), 1 FP32 quads (opt-in)
-    int p, n, W;
-    double sigma;
-    unsigned long long seed;
-    long long first_id, B;
-    int lpc, cpb, shared_endpoints;
-    int arc_all;
 };
 
 struct TspK {
@@ -393,26 +369,27 @@ __device__ __forceinline__ double uniform01(unsigned long long seed, unsigned lo
 
 // sampleWithNoise (include/sspp.h:114-130) in work items: item m of a candidate draws normals
 // 2m, 2m+1 (sampler 0: FP64 pair, Philox idx m) or 4m .. 4m+3 (sampler 1: FP32 quad) and adds
-// (sigma z) limits(d) to the perturbed control-point block c (column-major (j - p) * D + d).
+// (sigma z) limits(d) to the initial spline's perturbed control-point block `base` (row-major
+// (j - p) * D + d), writing the candidate's block c: c[k] = base[k] + (sigma z_k) limits[k % D].
 __device__ __forceinline__ int sample_items(int sampler, int npert) {
     return sampler ? (npert + 3) >> 2 : (npert + 1) >> 1;
 }
-__device__ __forceinline__ void sample_item(int sampler, unsigned long long seed, unsigned long long g,
-                                            int m, int npert, int D, double sigma,
-                                            const double* __restrict__ limits, double* c) {
+__device__ __forceinline__ void sample_item_to(int sampler, unsigned long long seed, unsigned long long g,
+                                               int m, int npert, int D, double sigma,
+                                               const double* limits, const double* base, double* c) {
     if (sampler == 0) {
         double z0, z1;
         normal_pair(seed, g, (unsigned)m, 0u, &z0, &z1);
         const int k = 2 * m;
-        c[k] = c[k] + (sigma * z0) * limits[k % D];
-        if (k + 1 < npert) c[k + 1] = c[k + 1] + (sigma * z1) * limits[(k + 1) % D];
+        c[k] = base[k] + (sigma * z0) * limits[k % D];
+        if (k + 1 < npert) c[k + 1] = base[k + 1] + (sigma * z1) * limits[(k + 1) % D];
     } else {
         double z[4];
         normal_quad(seed, g, (unsigned)m, 0u, z);
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
             const int k = 4 * m + h;
-            if (k < npert) c[k] = c[k] + (sigma * z[h]) * limits[k % D];
+            if (k < npert) c[k] = base[k] + (sigma * z[h]) * limits[k % D];
         }
     }
 }
@@ -796,186 +773,39 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
 }
 
 
-// ---------------------------------------------------------------- SamplingPathPlanner kernel
-// tab: host-precomputed basis rows, (W+1) collision rows u = i/W then W arc rows v = i/(W-1),
-// P+1 doubles each; span: matching knot spans.
-template <int D, int NM, int P, bool ONEGEOM>
-__global__ __launch_bounds__(kBlock, SSPP_SCORE_WAVES_PER_EU) void k_sspp(
-    SsppK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
-    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
-    const double* __restrict__ ctrl_in, const double* __restrict__ pert,
-    double* __restrict__ ctrl_out, double* __restrict__ arc, unsigned char* __restrict__ feasible,
-    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int P1 = P + 1;
-    const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, W = a.W;
-    const int ndof = n * D;
-    const int slot = tid / lpc, lane = tid - slot * lpc;
-    const long long cand0 = (long long)blockIdx.x * cpb;
-    double* s_ctrl = smem;                        // [cpb][n][D]
-    double* s_wsum = s_ctrl + cpb * ndof;         // [4]
-    double* s_arc = s_wsum + kBlock / 64;         // [4]
-    int* s_flag = (int*)(s_arc + 4);              // [cpb] + shared endpoints
-    const double* tcol = tab;
-    const double* tarc = tab + (W + 1) * P1;
-    const int* scol = span;
-    const int* sarc = span + (W + 1);
-
-    if (tid <= cpb) s_flag[tid] = 1;
-    const long long nvalid = min((long long)cpb, a.B - cand0);
-    // prefetch this lane's basis rows (global, L2-resident) while the control points stage
-    double Ncol[P1];
-    int sc0 = P;
-    {
-        const int i = lane + 1 < W ? lane + 1 : W - 1;
-#pragma unroll
-        for (int r = 0; r < P1; ++r) Ncol[r] = tcol[i * P1 + r];
-        sc0 = scol[i];
-    }
-    if (ctrl_in) {
-        const double* src = ctrl_in + cand0 * ndof;
-        for (int e = tid; e < nvalid * ndof; e += kBlock) s_ctrl[e] = src[e];
-    } else {
-        // init control points + perturbed columns j in [p, n-p): from the sampler kernel, or
-        // (insample) drawn here by the workgroup itself
-        const int npert = (n - 2 * P) * D;
-        const bool from_pert = !a.insample && !(a.ablate & 1);
-        for (int e = tid; e < cpb * ndof; e += kBlock) {
-            const int sl = e / ndof, r = e - sl * ndof;
-            const int k = r - P * D;
-            s_ctrl[e] = (from_pert && k >= 0 && k < npert && sl < nvalid)
-                            ? pert[(cand0 + sl) * npert + k]
-                            : init_ctrl[r];
-        }
-        if (a.insample) {
-            __syncthreads();
-            const int nq = sample_items(a.sampler, npert);
-            for (int e = tid; e < cpb * nq; e += kBlock) {
-                const int sl = e / nq, m = e - sl * nq;
-                if (sl >= nvalid) continue;
-                sample_item(a.sampler, a.seed, (unsigned long long)(a.first_id + cand0 + sl), m, npert, D,
-                            a.sigma, limits, s_ctrl + sl * ndof + P * D);
-            }
-        }
-    }
-    __syncthreads();
-    if (ctrl_out) {
-        double* dst = ctrl_out + cand0 * ndof;
-        for (int e = tid; e < nvalid * ndof; e += kBlock) dst[e] = s_ctrl[e];
-    }
-
-    const bool valid = slot < nvalid;
-    const double* myc = s_ctrl + slot * ndof;
-    double q[D], q2[D];
-    const unsigned long long mask =
-        a.has_scene ? hull_mask<D, NM, 0>(myc, n, a.sc.npairs, (cpair_t)T.pairs, (cgeom_t)T.geoms,
-                                          (cmover_t)T.movers)
-                    : 0ull;
-
-    // checkCollision: interior points i = 1..W-1 one per lane; endpoints i = 0, W on a spare lane
-    // Flags are plain LDS stores (every writer stores 0; read after the barrier below):
-    // no volatile/atomic access, so the scene tables stay on the scalar-load path.
-    if (a.has_scene && valid && !(a.ablate & 2)) {
-        int* vflag = s_flag;
-        if (a.sc.static_block) vflag[slot] = 0;
-        for (int j = lane; j < W - 1; j += lpc) {
-            const int i = j + 1;
-            if (j == lane) eval_pt<D, P>(myc, Ncol, sc0, q);
-            else eval_pt<D, P>(myc, tcol + i * P1, scol[i], q);
-            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr, vflag + slot)) {
-                __hip_atomic_store(vflag + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                break;
-            }
-        }
-        const int spare = (W - 1) % lpc == 0 ? 0 : lpc - 1;
-        bool duty0 = false, dutyW = false;
-        int fidx = slot;
-        if (a.shared_endpoints) {
-            fidx = cpb;
-            if (lane == spare) {
-                if (nvalid == 1) { duty0 = dutyW = slot == 0; }
-                else { duty0 = slot == 0; dutyW = slot == 1; }
-            }
-        } else if (lane == spare) {
-            duty0 = dutyW = true;
-        }
-        if (duty0) {
-            eval_pt<D, P>(myc, tcol, scol[0], q);
-            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr)) vflag[fidx] = 0;
-        }
-        if (dutyW) {
-            eval_pt<D, P>(myc, tcol + W * P1, scol[W], q);
-            if (point_collide<D, NM, 0, false, ONEGEOM>(q, a.sc, T, mask, nullptr)) vflag[fidx] = 0;
-        }
-    }
-
-    // computeArcLength: chords between v_{i-1} and v_i, i = 1..W-1
-    double acc = 0.0;
-    if (valid && !(a.ablate & 4)) {
-        for (int j = lane; j < W - 1; j += lpc) {
-            const int i = j + 1;
-            eval_pt<D, P>(myc, tarc + (i - 1) * P1, sarc[i - 1], q);
-            eval_pt<D, P>(myc, tarc + i * P1, sarc[i], q2);
-            acc = acc + dist_nd<D>(q, q2);
-        }
-    }
-    acc = wave_sum(acc);
-    if ((tid & 63) == 0) s_wsum[tid >> 6] = acc;
-    __syncthreads();
-    if (lane == 0 && valid) {
-        const int w0 = (slot * lpc) >> 6, nw = lpc >> 6;
-        double t = s_wsum[w0];
-        for (int w = 1; w < nw; ++w) t = t + s_wsum[w0 + w];
-        const long long c = cand0 + slot;
-        const int f = s_flag[slot] & s_flag[cpb];
-        arc[c] = (f || a.arc_all) ? t : INFINITY;
-        feasible[c] = (unsigned char)f;
-        s_arc[slot] = f ? t : INFINITY;
-    }
-    __syncthreads();
-    BlockBest bb;
-    if (tid == 0) {
-        bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
-        for (int s = 0; s < nvalid; ++s) {
-            if (!(s_flag[s] & s_flag[cpb])) continue;
-            bb.count++;
-            if (s_arc[s] < bb.cost) { bb.cost = s_arc[s]; bb.idx = a.first_id + cand0 + s; }
-        }
-    }
-    finish_batch(bb, part, sync, best);
-}
-
 // ================================================================ coarse-to-fine feasibility
-// k_sspp_c2f: SamplingPathPlanner scoring, workgroup = CPB candidates (CPB = 256 / G1).
+// k_sspp_c2f: SamplingPathPlanner scoring (include/sspp.h:194-225), workgroup = NT threads in
+// waves of CPW = 64 / G1 candidates (G1 phase-1 lanes per candidate; lanes past CPW * G1 idle).
 //
 // checkCollision (include/sspp.h:132-150) stops at the first waypoint in contact, so the result
 // is an OR over waypoints and pairs; the order in which they are examined cannot change it.
 // An infeasible candidate is typically in contact over a long stretch of its path (robocrane,
-// config 2: ~55 of 129 waypoints), so a handful of well-spread waypoints finds almost all of
-// them.  The host orders the W+1 collision waypoints breadth-first by interval bisection
-// (ord table); then per workgroup:
-//   phase 1  G1 lanes per candidate test the first G1 waypoints of that order; a candidate's
-//            lanes leave the pair loop together at the first pair any of them touches
-//            (ballot over the candidate's lane group);
+// config 2: ~55 of 129 waypoints), so a handful of well-chosen waypoints finds almost all of
+// them.  The host orders the W+1 collision waypoints (ord table: the job's hit order, then
+// breadth-first interval bisection); then per workgroup:
+//   prologue the initial spline once per workgroup in LDS (the control points sampleWithNoise
+//            leaves alone, include/sspp.h:118-129: rows outside [p, n-p)), each candidate's
+//            perturbed rows [p, n-p) drawn in-kernel (Philox4x32-10 + Box-Muller);
+//   phase 1  G1 lanes per candidate test the first n1 <= G1 waypoints of that order; a
+//            candidate's lanes leave the pair loop together at the first pair any of them
+//            touches (ballot over the candidate's lane group);
 //   phase 2  the survivors (few: the feasible ones plus the rare misses) are compacted in LDS
-//            and their remaining waypoints spread over all 256 lanes; a lane group that finds
+//            and their remaining waypoints spread over all NT lanes; a lane group that finds
 //            a contact clears the candidate's LDS flag, which stops its other lanes;
-//   phase 3  arc length for every candidate, in passes of 256/LPC candidates that keep the
-//            canonical reduction order of oracle/sspp_oracle.c::or_canon_sum;
+//   settle   cylinder-box pairs the scans left undecided (collide<..., DEFER>) get the exact
+//            test, out of line, for the (rare) candidates that have no other contact;
+//   phase 3  arc length of the collision-free candidates, in the canonical reduction order of
+//            oracle/sspp_oracle.c::or_canon_sum;
 //   phase 4  block argmin + the fused batch argmin (finish_batch).
-// Sampling (sampleWithNoise, include/sspp.h:114-130) runs in the prologue: one Box-Muller pair
-// per thread.
 struct SsppC2F {
     KScene sc;
     int has_scene;
-    int ablate;
-    int insample;
-    int sampler;
+    int sampler;   // 0 FP64 Box-Muller pairs (default), 1 FP32 quads (opt-in)
     int p, n, W;
     double sigma;
     unsigned long long seed;
     long long first_id, B;
-    int g1, cpb;   // phase-1 lanes per candidate (divides 64), candidates per workgroup
+    int g1, cpw, cpb;  // phase-1 lanes per candidate, candidates per wave (64 / g1) and workgroup
     int npts, n1;  // collision waypoints per candidate (W+1), phase-1 waypoints (<= g1)
     int lpc;       // canonical lanes of the arc-length sum (or_lanes_for(W-1))
     // several independent steps (batches) per launch: workgroup b belongs to step b / nblk_step;
@@ -984,23 +814,12 @@ struct SsppC2F {
     int nblk_step;
     long long step_stride;
     int arc_all;   // 0: arc length only for collision-free candidates (+inf otherwise)
-    int hull;      // candidate hull broadphase: 0 off, 1 all candidates, 2 phase-1 survivors
-    unsigned* dfr; // [0]: candidates of this launch left undecided (cylinder-box), [1]: k_sspp_cbfix arrivals
+    // control-point rows kept per candidate: [r0, r1) — sampled candidates [p, n-p) (the others
+    // are the initial spline's, one shared copy per workgroup), caller splines [0, n)
+    int r0, r1;
     int nt;        // launch shape (host side): threads per workgroup, dynamic LDS bytes
     int lds;
-    int ctrl_feas; // ctrl_out rows only for candidates with no contact (written at the end)
-    // fused survivor queue (k_sspp_c2f<..., FQ = true>, one-wave workgroups): phase 1's survivors
-    // become items of the job's work-queue buffers, drained by every workgroup of the launch
-    int p1cap;     // > 0: phase 1 runs at most p1cap wave pair iterations (SSPP_P1CAP)
-    int fq, fq_npg, fq_nchunk, fq_gs, fq_gcap;
-    unsigned fq_nps;
-    struct FqGroup* fq_grp;   // [steps][groups per step]
-    struct WqCtr* fq_ctr;
-    struct WqStep* fq_stp;
-    struct WqSurv* fq_surv;
-    double* fq_spert;
-    unsigned* fq_queue;
-    struct WqEnt* fq_list;
+    int ctrl_feas; // ctrl_out rows only for candidates with no contact
 };
 
 #ifdef SSPP_C2F_STATS
@@ -1009,17 +828,46 @@ struct SsppC2F {
 #define C2F_STAT(i, v) do { } while (0)
 #endif
 
+// LDS offset (in doubles) of control-point row j of a candidate whose own rows [r0, r1) start at
+// `mine`; the other rows are the workgroup's shared copy of the initial spline at `fix`.
+__device__ __forceinline__ int crow(int mine, int fix, int r0, int r1, int j, int D) {
+    return (j >= r0 && j < r1) ? mine + (j - r0) * D : fix + j * D;
+}
+// eval_pt on split rows: the same products and fma order, so bit-identical to eval_pt on the
+// candidate's full control-point array
+template <int D, int P>
+__device__ __forceinline__ void eval_split(const double* sm, int mine, int fix, int r0, int r1,
+                                           const double (&Nr)[P + 1], int span, double* q) {
+    int o[P + 1];
+#pragma unroll
+    for (int r = 0; r <= P; ++r) o[r] = crow(mine, fix, r0, r1, span - P + r, D);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        double acc = Nr[0] * sm[o[0] + d];
+#pragma unroll
+        for (int r = 1; r <= P; ++r) acc = fma(Nr[r], sm[o[r] + d], acc);
+        q[d] = acc;
+    }
+}
+template <int D, int P>
+__device__ __forceinline__ void eval_split_g(const double* sm, int mine, int fix, int r0, int r1,
+                                             const double* __restrict__ row, int span, double* q) {
+    double Nr[P + 1];
+#pragma unroll
+    for (int r = 0; r <= P; ++r) Nr[r] = row[r];
+    eval_split<D, P>(sm, mine, fix, r0, r1, Nr, span, q);
+}
+
 // Pair loop of one waypoint per lane.  All 64 lanes run the (wave-uniform) loop; `live` lanes
 // test the pairs of their own mask.  gbits = the lanes of this lane's candidate within the
 // wave: when any of them touches, all of them stop (returns true for the group).  flag: the
 // candidate's LDS feasibility flag (phase 2), polled so lanes in other waves stop too.
 // A cylinder-box pair that passes the bounding-sphere test sets dfr (undecided) and counts as
-// no contact here (collide<..., DEFER>); k_sspp_cbfix settles it with the exact test.
+// no contact here (collide<..., DEFER>); the settle step decides it with the exact test.
 template <int D, int NM, bool ONEGEOM>
 __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned long long mymask,
                                            unsigned long long umask, unsigned long long gbits,
-                                           int* flag, const KScene& sc, const SceneT& T, bool& dfr,
-                                           int maxit = 1 << 30) {
+                                           int* flag, const KScene& sc, const SceneT& T, bool& dfr) {
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
     double mp[NM][3], mR[NM][9];
@@ -1086,18 +934,22 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
         if (flag && live && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
             live = false;
         if (__ballot(live) == 0ull) break;
-        if (--maxit == 0) break;  // capped phase 1: the rest is phase 2's (k_sspp_c2f p1cap)
     }
     return ghit;
 }
 
+#ifndef SSPP_CB_INLINE
+#define SSPP_CB_INLINE __attribute__((noinline))
+#endif
 // The exact cylinder-box test (witnesses + candidate search, sspd::cyl_box_overlap) of one
-// waypoint over the pairs of `mask` (k_sspp_cbfix).
-template <int D, int NM, int P, bool ONEGEOM>
-__device__ __forceinline__ bool cb_point_exact(const double* ctrl, const double* row, int span,
-                                               unsigned long long mask, int np, SceneT T) {
+// waypoint of one candidate over its cylinder-box pairs.  Out of line: it runs only for the
+// candidates the scans left undecided, and its registers stay out of the kernel's pair loops.
+template <int D, int NM, int P>
+__device__ SSPP_CB_INLINE bool c2f_cb_exact(const double* sm, int mine, int fix, int r0, int r1,
+                                                       const double* __restrict__ row, int span,
+                                                       unsigned long long mask, int np, SceneT T) {
     double q[D];
-    eval_pt<D, P>(ctrl, row, span, q);
+    eval_split_g<D, P>(sm, mine, fix, r0, r1, row, span, q);
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
     double mp[NM][3], mR[NM][9];
@@ -1132,59 +984,58 @@ __device__ __forceinline__ bool cb_point_exact(const double* ctrl, const double*
     return false;
 }
 
+// Occupancy per shape: one-wave workgroups of a single-geom mover at 5 waves per SIMD (96 VGPRs,
+// no spill: 20 workgroups per CU, so a 20-step launch of 4096-candidate steps is one resident
+// round); 4-wave workgroups and multi-geom movers at 4 (128 VGPRs; at 5 they spill).
 #ifndef SSPP_C2F_WAVES_PER_EU
-#define SSPP_C2F_WAVES_PER_EU 4  // measured: 3 -> 1280, 4 -> 1396, 5 -> 1237, 6 -> 697 M cand/s (robocrane)
+#define SSPP_C2F_WAVES_PER_EU 5
 #endif
-template <int D, int NM, int P, bool ONEGEOM>
-__device__ void c2f_fused_tail(const SsppC2F& a, const SceneT& T, const double* __restrict__ otab,
-                               const int* __restrict__ ospan, const double* __restrict__ atab,
-                               const int* __restrict__ aspan, const double* __restrict__ init_ctrl,
-                               double* s_ctrl, double* s_box, const int* s_feas, int step, long long cand0,
-                               int nvalid, double* arc0, unsigned char* feas0, double* ctrl_out0,
-                               sspp_best* best0);
-
-template <int D, int NM, int P, bool ONEGEOM, int NT, bool FQ = false>
-__global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
+#ifndef SSPP_C2F_WAVES_PER_EU_WIDE
+#define SSPP_C2F_WAVES_PER_EU_WIDE 4
+#endif
+// profiling builds only (tools/build_variant.sh -DSSPP_ABLATE=mask): 1 no sampling, 2 no
+// collision, 4 no arc, 8 no phase 2, 16 no phase 1, 64 return at entry (launch cost only)
+#ifndef SSPP_ABLATE
+#define SSPP_ABLATE 0
+#endif
+// CBX: the pair table has cylinder-box pairs, so the kernel carries the settle step (its
+// out-of-line exact test costs the whole kernel registers: 96 -> 128 VGPRs and scratch)
+template <int D, int NM, int P, bool ONEGEOM, int NT, bool CBX>
+__global__ __launch_bounds__(NT, (NT == 64 && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU : SSPP_C2F_WAVES_PER_EU_WIDE) void k_sspp_c2f(
     SsppC2F a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
     const double* __restrict__ atab, const int* __restrict__ aspan,
     const double* __restrict__ init_ctrl, const double* __restrict__ limits,
-    const double* __restrict__ ctrl_in, const double* __restrict__ pert,
-    double* __restrict__ ctrl_out, double* __restrict__ arc, unsigned char* __restrict__ feasible,
-    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    const double* __restrict__ ctrl_in, double* __restrict__ ctrl_out, double* __restrict__ arc,
+    unsigned char* __restrict__ feasible, BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int P1 = P + 1;
     constexpr int NB = 3 * NM;  // AABB extents per candidate (x, y, z per mover)
+    constexpr int ABL = SSPP_ABLATE;
     const int tid = threadIdx.x, cpb = a.cpb, n = a.n, W = a.W, g1 = a.g1;
-    const int lg1 = __builtin_ctz(g1);
     const int ndof = n * D, nch = W - 1;
+    const int r0 = a.r0, r1 = a.r1, nrd = (r1 - r0) * D;  // doubles kept per candidate
     const int step = blockIdx.x / a.nblk_step, blk = blockIdx.x - step * a.nblk_step;
     const long long cand0 = (long long)blk * cpb;
     const int nvalid = (int)min((long long)cpb, a.B - cand0);
     const long long first_id = a.first_id + step * a.step_stride;
-    if (a.ablate & 64) return;  // profiling: launch + dispatch cost only
+    if (ABL & 64) return;
 #ifdef SSPP_WG_TIMING
     const unsigned long long wg_t0 = wall_clock64();
     int wg_ns = -1;
 #endif
     WG_PH(0);
-    double* const arc0 = arc;
-    unsigned char* const feas0 = feasible;
-    double* const ctrl_out0 = ctrl_out;
-    sspp_best* const best0 = best;
     if (step) {
         arc += step * a.B;
         feasible += step * a.B;
-        if (pert) pert += step * a.B * ((n - 2 * P) * D);
         if (ctrl_out) ctrl_out += step * a.B * ndof;
         part += step * a.nblk_step;
         sync += step;
         if (best) best += step;
     }
-    double* s_ctrl = smem;                                    // [cpb][n][D]
-    double* s_lim = s_ctrl + cpb * ndof;                      // [D] sampleWithNoise limits
-    // s_box is dead once phase 2's hull masks are built (a barrier follows), so phase 3's
-    // s_vsum / s_arc reuse its space: 384 B less per 16-candidate workgroup, which lets LDS
-    // hold 16 workgroups per CU instead of 14
+    // LDS (doubles): the shared initial spline [n][D], the candidates' own rows [cpb][r1-r0][D],
+    // the limits [D], then the hull boxes (phase 2) — reused by phase 3's sums — and the flags
+    const int o_fix = 0, o_own = ndof;
+    double* s_lim = smem + o_own + cpb * nrd;                 // [D] sampleWithNoise limits
     const int nvw3 = a.lpc >> 6, rbox = 2 * NB > nvw3 + 1 ? 2 * NB : nvw3 + 1;
     double* s_box = s_lim + D;                                // [cpb][2][NB] (hull)
     double* s_vsum = s_box;                                   // [cpb][lpc/64] (phase 3)
@@ -1194,153 +1045,88 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
     int* s_surv = s_feas + cpb;                               // [cpb + 1] (last = count)
     int* s_defer = s_surv + cpb + 1;                          // [cpb] undecided cylinder-box pair
 
-    // ---- prologue: control points (+ sampleWithNoise) in LDS.  Every independent global read
-    // of the prologue and phase 1 (the initial spline, the limits, this lane's phase-1 basis row)
-    // is issued here, so their L2 round trips overlap instead of following one another.
-    const int l_p1 = tid & (g1 - 1);
-    const int row_p1 = l_p1 < a.npts ? l_p1 : 0;
+    // ---- per-lane layout: wave w holds candidates [w cpw, (w + 1) cpw), g1 lanes each
+    const int wv = tid >> 6, ln = tid & 63;
+    const int lg = ln / g1, l = ln - lg * g1;
+    const bool in_grp = lg < a.cpw;
+    const int g = wv * a.cpw + (in_grp ? lg : 0);
+    const unsigned long long gbits = g1 >= 64 ? ~0ull : (((1ull << g1) - 1ull) << (lg * g1));
+
+    // ---- prologue.  Every independent global read of the prologue and phase 1 (the initial
+    // spline, the limits, this lane's phase-1 basis row) is issued here, so their L2 round trips
+    // overlap instead of following one another.
+    const int row_p1 = l < a.npts ? l : 0;
     double N_p1[P1];
 #pragma unroll
     for (int r = 0; r < P1; ++r) N_p1[r] = otab[row_p1 * P1 + r];
     const int span_p1 = ospan[row_p1];
+    for (int rr = tid; rr < ndof; rr += NT) smem[o_fix + rr] = init_ctrl[rr];
     if (tid < D) s_lim[tid] = limits[tid];
-    {
-        if (ctrl_in) {  // element e = sl * ndof + r walked with add-with-carry
-            const int dsl = NT / ndof, dr = NT - dsl * ndof;
-            int sl = tid / ndof, r = tid - sl * ndof;
-            const double* src = ctrl_in + cand0 * ndof;
-            for (; sl < nvalid; sl += dsl) {
-                s_ctrl[sl * ndof + r] = src[sl * ndof + r];
-                r += dr;
-                if (r >= ndof) { r -= ndof; ++sl; }
-            }
-        } else {
-            // lane-owned columns: the initial spline's value is loaded once per column and
-            // stored for every candidate (LDS stores only, no load latency per element)
-            const int npert = (n - 2 * P) * D;
-            const bool from_pert = !a.insample && !(a.ablate & 1);
-            for (int rr = tid; rr < ndof; rr += NT) {
-                const double v0 = init_ctrl[rr];
-                const int k = rr - P * D;
-                const bool pr = from_pert && k >= 0 && k < npert;
-                for (int s2 = 0; s2 < cpb; ++s2)
-                    s_ctrl[s2 * ndof + rr] = (pr && s2 < nvalid) ? pert[(cand0 + s2) * npert + k] : v0;
-            }
+    if (ctrl_in) {  // element e = sl * ndof + r walked with add-with-carry
+        const int dsl = NT / ndof, dr = NT - dsl * ndof;
+        int sl = tid / ndof, r = tid - sl * ndof;
+        const double* src = ctrl_in + cand0 * ndof;
+        for (; sl < nvalid; sl += dsl) {
+            smem[o_own + sl * ndof + r] = src[sl * ndof + r];
+            r += dr;
+            if (r >= ndof) { r -= ndof; ++sl; }
         }
     }
-    if (tid < cpb) s_mask[tid] = 0ull;
     __syncthreads();
     WG_PH(1);
-    if (!ctrl_in && a.insample && !(a.ablate & 1)) {
-        // sampleWithNoise: item t = (candidate sl, sampler item m), spread over the workgroup
-        const int npert = (n - 2 * P) * D;
-        const int nq = sample_items(a.sampler, npert);
-        const int total = nvalid * nq;
-        {
-            // item t = (sl, m) walked with add-with-carry (no integer division per item)
-            const int dsl = NT / nq, dm = NT - dsl * nq;
-            int sl = tid / nq, m = tid - sl * nq;
-            for (int t = tid; t < total; t += NT) {
-                sample_item(a.sampler, a.seed, (unsigned long long)(first_id + cand0 + sl), m, npert, D, a.sigma,
-                            s_lim, s_ctrl + sl * ndof + P * D);
-                sl += dsl;
-                m += dm;
-                if (m >= nq) { m -= nq; ++sl; }
+    if (!ctrl_in && nrd > 0) {
+        // sampleWithNoise: item t = (candidate sl, sampler item m), spread over the workgroup,
+        // walked with add-with-carry (no integer division per item); each item writes
+        // init + (sigma z) limits into the candidate's own rows (unsampled slots: the init rows)
+        const int nq = sample_items(a.sampler, nrd);
+        const double* base = smem + o_fix + r0 * D;
+        const int dsl = NT / nq, dm = NT - dsl * nq;
+        int sl = tid / nq, m = tid - sl * nq;
+        for (int t = tid; t < nvalid * nq; t += NT) {
+            double* dst = smem + o_own + sl * nrd;
+            if (!(ABL & 1)) {
+                sample_item_to(a.sampler, a.seed, (unsigned long long)(first_id + cand0 + sl), m, nrd, D, a.sigma,
+                               s_lim, base, dst);
+            } else {
+                const int per = a.sampler ? 4 : 2;
+                for (int h = 0; h < per; ++h) {
+                    const int k = per * m + h;
+                    if (k < nrd) dst[k] = base[k];
+                }
             }
+            sl += dsl;
+            m += dm;
+            if (m >= nq) { m -= nq; ++sl; }
         }
         __syncthreads();
-    }
-    if (ctrl_out && !a.ctrl_feas) {
-        double* dst = ctrl_out + cand0 * ndof;
-        for (int e = tid; e < nvalid * ndof; e += NT) dst[e] = s_ctrl[e];
     }
     WG_PH(2);
 
     const SceneT TT = T;
-    const bool collide_on = a.has_scene && !(a.ablate & 2);
+    const bool collide_on = a.has_scene && !(ABL & 2);
     const int np = a.sc.npairs;
-    // ---- candidate-level broadphase (convex hull of the control points, see pair_may_touch):
-    // AABB per (candidate, mover, axis), then one (candidate, pair) test per thread; the mask
-    // bits are OR-ed into LDS.
-    // hull = 1: every candidate before phase 1; hull = 2 (default): only phase 1's survivors,
-    // before phase 2 — phase 1 stops at the first touching pair anyway, and on robocrane the
-    // all-candidate hull cost more than it saved (measured: 1.11 vs 1.22 G cand/s without it)
-    const int hull = (a.ablate & 32) ? 0 : a.hull;
-    if (collide_on && hull == 1) {
-        for (int e = tid; e < cpb * NB; e += NT) {
-            const int sl = e / NB, md = e - sl * NB, m = md / 3, d = md - m * 3;
-            const int col = 7 * m + d;
-            double lo, hi;
-            if (col < D) {
-                const double* c = s_ctrl + sl * ndof + col;
-                lo = hi = c[0];
-                for (int j = 1; j < n; ++j) {
-                    const double v = c[j * D];
-                    lo = v < lo ? v : lo;
-                    hi = v > hi ? v : hi;
-                }
-            } else {
-                lo = hi = (double)((cmover_t)TT.movers)[m].qpos0[d];
-            }
-            s_box[sl * 2 * NB + md] = lo;
-            s_box[sl * 2 * NB + NB + md] = hi;
-        }
-        __syncthreads();
-        if (np > 64) {
-            if (tid < cpb) s_mask[tid] = ~0ull;
-        } else {
-            for (int e = tid; e < cpb * np; e += NT) {
-                const int sl = e / np, k = e - sl * np;
-                const DPair pr = load_pair((cpair_t)TT.pairs + k);
-                const DGeom G = load_geom((cgeom_t)TT.geoms + pr.gm);
-                const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
-                const double* bx = s_box + sl * 2 * NB;
-                if (pair_may_touch(pr, G, bx + 3 * m, bx + NB + 3 * m))
-                    atomicOr(s_mask + sl, 1ull << k);
-            }
-        }
-        __syncthreads();
-    } else if (collide_on) {
-        if (tid < cpb) s_mask[tid] = ~0ull;
-        __syncthreads();
-    }
     // ---- phase 1: G1 lanes per candidate, first n1 waypoints of the coarse-to-fine order
     {
-        const int g = tid >> lg1, l = tid & (g1 - 1), wg = (tid & 63) >> lg1;
-        const unsigned long long low = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
-        const unsigned long long gbits = low << (wg * g1);
-        const bool valid = g < nvalid;
+        const bool valid = in_grp && g < nvalid;
         bool ghit = false, dfr = false;
         if (collide_on) {
-            const unsigned long long mymask = s_mask[g];
-            unsigned long long umask = 0ull;  // union over the wave's groups (wave-uniform)
-            const int g0 = (tid & ~63) >> lg1;
-            for (int w = 0; w < (64 >> lg1); ++w) umask |= s_mask[g0 + w];
-            const bool live = valid && l < a.n1 && !a.sc.static_block && !(a.ablate & 16);
+            const bool live = valid && l < a.n1 && !a.sc.static_block && !(ABL & 16);
             double q[D];
-            eval_pt_r<D, P>(s_ctrl + (valid ? g : 0) * ndof, N_p1, span_p1, q);
-            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mymask, umask, gbits, nullptr, a.sc, TT, dfr,
-                                              a.p1cap > 0 ? a.p1cap : (1 << 30));
+            eval_split<D, P>(smem, o_own + (valid ? g : 0) * nrd, o_fix, r0, r1, N_p1, span_p1, q);
+            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, ~0ull, ~0ull, gbits, nullptr, a.sc, TT, dfr);
         }
         const bool gdef = (__ballot(dfr) & gbits) != 0ull;
-        if (l == 0) {
+        if (in_grp && l == 0 && g < cpb) {
             s_feas[g] = valid && !ghit && !(collide_on && a.sc.static_block);
             s_defer[g] = gdef;
         }
     }
     __syncthreads();
     WG_PH(3);
-    if (FQ) {  // survivors to the launch's queue; this workgroup then drains it (host-checked mode)
-        c2f_fused_tail<D, NM, P, ONEGEOM>(a, TT, otab, ospan, atab, aspan, init_ctrl, s_ctrl, s_box, s_feas, step,
-                                          cand0, nvalid, arc0, feas0, ctrl_out0, best0);
-        return;
-    }
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
-    // p1cap: phase 1 stopped after p1cap pair iterations, so its undecided candidates are
-    // survivors whose every waypoint phase 2 checks (the OR over waypoints is unchanged)
-    const int j0 = a.p1cap > 0 ? 0 : a.n1;
+    const int j0 = a.n1;
     const int R = a.npts - j0;
-    if (collide_on && R > 0 && !(a.ablate & 8)) {
+    if (collide_on && R > 0 && !(ABL & 8)) {
         if (tid < 64) {  // survivors compacted by one wave ballot (cpb <= 64), in candidate order
             const bool f = tid < nvalid && s_feas[tid] != 0;
             const unsigned long long m = __ballot(f);
@@ -1353,16 +1139,20 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
 #ifdef SSPP_WG_TIMING
         wg_ns = ns;
 #endif
-        if (hull == 2 && ns > 0 && np <= 64) {  // the survivors' hull masks (see above)
+        // the survivors' hull masks: AABB of the control points per (survivor, mover, axis),
+        // then one (survivor, pair) test per thread (pair_may_touch; exact, see above).  Only
+        // survivors: phase 1 stops at the first touching pair anyway, and computing the masks
+        // for every candidate cost more than it saved (robocrane: 1.11 vs 1.22 G cand/s)
+        if (ns > 0 && np <= 64) {
             for (int e = tid; e < ns * NB; e += NT) {
                 const int si = e / NB, md = e - si * NB, m = md / 3, d = md - m * 3;
                 const int sl = s_surv[si], col = 7 * m + d;
                 double lo, hi;
                 if (col < D) {
-                    const double* c = s_ctrl + sl * ndof + col;
-                    lo = hi = c[0];
+                    const int own = o_own + sl * nrd;
+                    lo = hi = smem[crow(own, o_fix, r0, r1, 0, D) + col];
                     for (int j = 1; j < n; ++j) {
-                        const double v = c[j * D];
+                        const double v = smem[crow(own, o_fix, r0, r1, j, D) + col];
                         lo = v < lo ? v : lo;
                         hi = v > hi ? v : hi;
                     }
@@ -1383,6 +1173,9 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
                 if (pair_may_touch(pr, G, bx + 3 * m, bx + NB + 3 * m))
                     atomicOr(s_mask + sl, 1ull << k);
             }
+            __syncthreads();
+        } else if (ns > 0) {
+            if (tid < ns) s_mask[s_surv[tid]] = ~0ull;
             __syncthreads();
         }
         unsigned long long umask = 0ull;
@@ -1420,7 +1213,7 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
             unsigned long long gb = 0ull;
             if (it < items && hi > lo) gb = (hi - lo >= 64) ? ~0ull : (((1ull << (hi - lo)) - 1ull) << lo);
             double q[D];
-            eval_pt<D, P>(s_ctrl + s * ndof, otab + j * P1, ospan[j], q);
+            eval_split_g<D, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], q);
             bool dfr = false;
             const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s] & gmask, umask & gmask, gb, s_feas + s,
                                                       a.sc, TT, dfr);
@@ -1429,14 +1222,35 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         }
     }
     WG_PH(4);
+    // ---- settle: candidates with no contact but an undecided cylinder-box pair get the exact
+    // test at every collision waypoint (the OR over waypoints and pairs is unchanged)
+    if (CBX && collide_on) {
+        __syncthreads();
+        if (tid < 64) {
+            const bool u = tid < nvalid && s_feas[tid] != 0 && s_defer[tid] != 0;
+            const unsigned long long m = __ballot(u);
+            if (u) s_surv[__popcll(m & ((1ull << tid) - 1ull))] = tid;
+            if (tid == 0) s_surv[cpb] = __popcll(m);
+        }
+        __syncthreads();
+        const int nu = s_surv[cpb];
+        for (int i = 0; i < nu; ++i) {  // workgroup-uniform
+            const int s = s_surv[i];
+            for (int j = tid; j < a.npts; j += NT) {
+                if (__hip_atomic_load(s_feas + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
+                if (c2f_cb_exact<D, NM, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], ~0ull, np, TT))
+                    __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    }
     // ---- phase 3: arc length (computeArcLength, include/sspp.h:152-169) of the listed
     // candidates: the collision-free ones (findBestPath scores only successful paths), or all
-    // of them with arc_all.  Chords v_j -> v_{j+1} (v_i = s(i/(W-1))) go to LDS, then each
-    // candidate's chords are summed in the canonical order of oracle/sspp_oracle.c::or_canon_sum:
-    // lpc lane partials (chords vl, vl+lpc, ...), an xor butterfly per 64 lanes, 64-lane groups
-    // in order.
+    // of them with arc_all.  Each candidate's chords are summed in the canonical order of
+    // oracle/sspp_oracle.c::or_canon_sum: lpc lane partials (chords vl, vl+lpc, ...), an xor
+    // butterfly per 64 lanes, 64-lane groups in order.
+    __syncthreads();
     if (tid < cpb) s_arc[tid] = INFINITY;
-    if (!(a.ablate & 4)) {
+    if (!(ABL & 4)) {
         __syncthreads();
         int* s_list = s_surv;  // phase 2 is done with it
         if (tid < 64) {  // one wave ballot, candidate order
@@ -1451,19 +1265,19 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         // accumulates chords j = 64 v + l, + lpc, ... (the lane partials of or_canon_sum), then
         // the xor butterfly gives the group's sum.  A chord's first point is the previous lane's
         // second point (same candidate, same pass), taken by shuffle: bit-identical to
-        // evaluating it again.  No chord array: the workgroup's LDS holds only control points.
+        // evaluating it again.
         const int lpc = a.lpc, nvw = lpc >> 6, lane = tid & 63;
         for (int vw = tid >> 6; vw < nl * nvw; vw += NT / 64) {  // wave-uniform
             const int si = vw / nvw, v = vw - si * nvw;
-            const double* myc = s_ctrl + s_list[si] * ndof;
+            const int own = o_own + s_list[si] * nrd;
             double acc = 0.0;
             for (int base = v * 64; base < nch; base += lpc) {  // wave-uniform trip count
                 const int j = base + lane, jj = j < nch ? j : nch - 1;
                 double qa[D], qb[D];
-                eval_pt<D, P>(myc, atab + (jj + 1) * P1, aspan[jj + 1], qb);
+                eval_split_g<D, P>(smem, own, o_fix, r0, r1, atab + (jj + 1) * P1, aspan[jj + 1], qb);
 #pragma unroll
                 for (int d = 0; d < D; ++d) qa[d] = __shfl_up(qb[d], 1, 64);
-                if (lane == 0) eval_pt<D, P>(myc, atab + jj * P1, aspan[jj], qa);
+                if (lane == 0) eval_split_g<D, P>(smem, own, o_fix, r0, r1, atab + jj * P1, aspan[jj], qa);
                 if (j < nch) acc = acc + dist_nd<D>(qa, qb);
             }
             acc = wave_sum(acc);
@@ -1483,26 +1297,26 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         const long long c = cand0 + tid;
         if (s_feas[tid]) C2F_STAT(8, 0);
         arc[c] = s_arc[tid];
-        // 2: no contact except cylinder-box pairs left undecided; k_sspp_cbfix writes 0 or 1
-        feasible[c] = (unsigned char)(s_feas[tid] == 0 ? 0 : (s_defer[tid] ? 2 : 1));
+        feasible[c] = (unsigned char)(s_feas[tid] != 0);
     }
-    if (ctrl_out && a.ctrl_feas) {  // the rows a plan() returns: feasible (or undecided) only
+    if (ctrl_out) {  // [B][n][D] rows: every candidate, or (ctrl_feas, plan()) the feasible ones
         double* dst = ctrl_out + cand0 * ndof;
-        for (int e = tid; e < nvalid * ndof; e += NT)
-            if (s_feas[e / ndof]) dst[e] = s_ctrl[e];
+        for (int e = tid; e < nvalid * ndof; e += NT) {
+            const int sl = e / ndof, r = e - sl * ndof, j = r / D;
+            if (!a.ctrl_feas || s_feas[sl]) dst[e] = smem[crow(o_own + sl * nrd, o_fix, r0, r1, j, D) + (r - j * D)];
+        }
     }
     // block argmin over the workgroup's feasible candidates: one wave, lexicographic (cost, id)
     // xor butterfly (exact, order independent: the lowest id wins ties like the serial scan).
-    // Undecided candidates stay out; k_sspp_cbfix merges the ones it clears.
+    // findBestPath (include/sspp.h:171-192) takes a path only when its cost < the running
+    // minimum from +inf, so a feasible candidate with an infinite or NaN arc is never the best
+    // (it still counts as feasible).
     BlockBest bb;
     if (tid < 64) {
-        const bool und = tid < nvalid && s_feas[tid] != 0 && s_defer[tid] != 0;
-        const unsigned long long um = __ballot(und);
-        if (tid == 0 && um != 0ull)
-            __hip_atomic_fetch_add(a.dfr, (unsigned)__popcll(um), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool f = tid < nvalid && s_feas[tid] != 0 && !und;
-        double bc = f ? s_arc[tid] : INFINITY;
-        long long bi = f ? first_id + cand0 + tid : -1;
+        const bool f = tid < nvalid && s_feas[tid] != 0;
+        const bool fa = f && s_arc[tid] < INFINITY;
+        double bc = fa ? s_arc[tid] : INFINITY;
+        long long bi = fa ? first_id + cand0 + tid : -1;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             const double oc = __shfl_xor(bc, off, 64);
@@ -1521,833 +1335,6 @@ __global__ __launch_bounds__(NT, SSPP_C2F_WAVES_PER_EU) void k_sspp_c2f(
         g_wg_t[4 * blockIdx.x + 3] = (unsigned long long)(long long)wg_ns;
     }
 #endif
-}
-
-// ---------------------------------------------------------------- undecided cylinder-box pairs
-// k_sspp_c2f leaves a cylinder-box pair that passes the bounding-sphere test undecided (the
-// exact test's registers would spill its whole pair loop).  A candidate with no other contact is
-// written as feasible = 2, kept out of the argmin and counted in dfr[0].  This kernel, queued
-// right after it on the same stream, gives each such candidate the exact test at every
-// collision waypoint: a contact makes it infeasible (arc +inf unless arc_all), otherwise it is
-// feasible and is merged into its step's records (block record and fused result, lexicographic
-// (cost, id) under the step's lock, count + 1), so the outputs equal a kernel that ran the exact
-// test inline.  With dfr[0] == 0 (every scene without such pairs near a path) each workgroup
-// returns after one scalar load.  The last workgroup to finish re-arms dfr.
-constexpr int kFixThreads = 256;
-constexpr int kFixBlocks = 64;
-template <int D, int NM, int P, bool ONEGEOM>
-__global__ __launch_bounds__(kFixThreads) void k_sspp_cbfix(
-    SsppC2F a, SceneT T, int steps, const double* __restrict__ otab, const int* __restrict__ ospan,
-    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
-    const double* __restrict__ ctrl_in, const double* __restrict__ pert, double* __restrict__ arc,
-    unsigned char* __restrict__ feasible, BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
-    if (__hip_atomic_load(a.dfr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int P1 = P + 1;
-    __shared__ int s_list[kFixThreads + 1];
-    __shared__ int s_hit;
-    const int tid = threadIdx.x, n = a.n, ndof = n * D;
-    double* s_ctrl = smem;  // [n][D]
-    const long long total = (long long)steps * a.B;
-    for (long long base = (long long)blockIdx.x * kFixThreads; base < total; base += (long long)gridDim.x * kFixThreads) {
-        const long long c0 = base + tid;
-        if (tid == 0) s_list[kFixThreads] = 0;
-        __syncthreads();
-        if (c0 < total && feasible[c0] == 2) s_list[atomicAdd(&s_list[kFixThreads], 1)] = tid;
-        __syncthreads();
-        const int nl = s_list[kFixThreads];
-        for (int i = 0; i < nl; ++i) {  // workgroup-uniform
-            const long long c = base + s_list[i];
-            const int step = (int)(c / a.B);
-            const long long cand = c - (long long)step * a.B;
-            const long long first_id = a.first_id + step * a.step_stride;
-            // the candidate's control points, exactly as k_sspp_c2f's prologue made them
-            const int npert = (n - 2 * P) * D;
-            for (int r = tid; r < ndof; r += kFixThreads) {
-                const int k = r - P * D;
-                double v = init_ctrl[r];
-                if (ctrl_in) v = ctrl_in[cand * ndof + r];
-                else if (pert && !a.insample && !(a.ablate & 1) && k >= 0 && k < npert)
-                    v = pert[((long long)step * a.B + cand) * npert + k];
-                s_ctrl[r] = v;
-            }
-            if (tid == 0) s_hit = 0;
-            __syncthreads();
-            if (!ctrl_in && a.insample && !(a.ablate & 1)) {
-                const int nq = sample_items(a.sampler, npert);
-                for (int m = tid; m < nq; m += kFixThreads)
-                    sample_item(a.sampler, a.seed, (unsigned long long)(first_id + cand), m, npert, D, a.sigma,
-                                limits, s_ctrl + P * D);
-                __syncthreads();
-            }
-            for (int j = tid; j < a.npts; j += kFixThreads) {
-                if (__hip_atomic_load(&s_hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-                if (cb_point_exact<D, NM, P, ONEGEOM>(s_ctrl, otab + j * P1, ospan[j], ~0ull, a.sc.npairs, T))
-                    __hip_atomic_store(&s_hit, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            __syncthreads();
-            if (tid == 0) {
-                if (s_hit) {
-                    feasible[c] = 0;
-                    if (!a.arc_all) arc[c] = INFINITY;
-                } else {
-                    feasible[c] = 1;
-                    const double cost = arc[c];
-                    const long long id = first_id + cand;
-                    unsigned* lock = &sync[step].top[1];
-                    while (atomicCAS(lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(2);
-                    __threadfence();
-                    BlockBest* pb = part + (long long)step * a.nblk_step + cand / a.cpb;
-                    BlockBest r = ld_rec(pb);
-                    if (better(cost, id, r.cost, r.idx)) { r.cost = cost; r.idx = id; }
-                    r.count += 1;
-                    st_rec(pb, r);
-                    if (best) {
-                        volatile sspp_best* o = best + step;
-                        if (better(cost, id, o->cost, o->index)) { o->cost = cost; o->index = id; }
-                        o->count = o->count + 1;
-                    }
-                    __threadfence();
-                    atomicExch(lock, 0u);
-                }
-            }
-            __syncthreads();
-        }
-    }
-    // the last workgroup re-arms the counters for the next launch on this job
-    if (tid == 0) {
-        __threadfence();
-        const unsigned prev = __hip_atomic_fetch_add(a.dfr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == gridDim.x - 1) {
-            __hip_atomic_store(a.dfr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.dfr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// ================================================================ two-kernel scoring (k_sspp_wq1/2)
-// SamplingPathPlanner scoring (include/sspp.h:194-225) shaped so that one plan() batch of 4096
-// candidates fills the chip and its slowest candidate — a feasible one, whose check must visit
-// every waypoint and every pair — runs on several waves at once.
-//   k_sspp_wq1: one TILE of cpw candidates of one step per one-wave workgroup (grid = tiles):
-//     sampleWithNoise (Philox + FP64 Box-Muller into LDS), then phase 1 — g1 = 64 / cpw lanes per
-//     candidate test the first n1 waypoints of the coarse-to-fine order (k_sspp_c2f's phase 1).  A
-//     candidate with a contact is decided (infeasible).  Every other one is a SURVIVOR: its
-//     perturbed control points and hull mask go to its record (indexed by candidate) and it joins
-//     queue shard (tile % 8).  Candidates decided feasible here (no scene, or no waypoint left)
-//     go straight to their step's feasible list.  No wave waits for another.
-//   k_sspp_wq2 (queued behind it on the stream): a survivor is nchunk x npg ITEMS — its waypoints
-//     [n1 + 64 c, n1 + 64 (c + 1)) (one per lane) against pair group g of its hull-masked pairs
-//     (the live pairs dealt round robin over npg groups).  Workgroup b drains shard b % 8 with one
-//     returning atomic add per claim (8 shards: 8 words share the claims).  A contact sets the
-//     record's hit bit; the item that finishes last (the pending count in the same 64-bit word,
-//     so its decrement returns the hit bit too) decides the candidate: cylinder-box pairs left
-//     undecided by the scan (collide<..., DEFER>) get the exact test here, out of line
-//     (wq_cb_exact, CB variant only), and a feasible candidate gets its arc length
-//     (computeArcLength, canonical order) and one entry in its step's feasible list.  A step is
-//     decided when its survivors are; the wave deciding the last one reduces the list
-//     (findBestPath: lowest arc, lowest id) into best[step].  Steps without survivors are
-//     reduced by workgroup `step` on entry.
-// Hand-offs: k_sspp_wq1 -> k_sspp_wq2 through the kernel boundary (plain stores / loads); inside
-// k_sspp_wq2 list entries and hit bits travel as 8-byte sc1 stores drained before the counter
-// add that signals them, read with sc1 loads after that add's return (cdna_hip_programming.md
-// Guideline 16, R1).  The last k_sspp_wq2 workgroup out (sharded arrival counters) re-arms the
-// queue counters; a step's reducer re-arms the step's.
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef __attribute__((address_space(1))) unsigned gu32_t;
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-#else
-typedef unsigned gu32_t;
-typedef unsigned long long gu64_t;
-#endif
-constexpr int kWqShards = 8;
-struct WqCtr {  // per job, zeroed at creation; every counter on its own 64-byte line
-    unsigned tail[kWqShards][16];   // survivors queued per shard (k_sspp_wq1)
-    unsigned head[kWqShards][16];   // items claimed per shard (k_sspp_wq2)
-    unsigned exitc[kWqShards][16];  // k_sspp_wq2 arrivals per shard (block % 8)
-    unsigned top[16];
-    unsigned error[16];             // diagnostics: a queue entry past the capacity
-};
-struct WqStep {  // per step of a launch
-    unsigned nsurv;    // survivors (k_sspp_wq1)
-    unsigned decided;  // survivors decided (k_sspp_wq2)
-    unsigned nent;     // entries in the step's feasible list
-    unsigned count;    // feasible candidates
-    unsigned pad[12];
-};
-struct WqSurv {  // survivor record, at the candidate's index (step * B + candidate)
-    unsigned long long mask;   // hull-masked pairs (bit k: pair k may touch)
-    unsigned long long pend;   // pending items (low 32 bits) | hit (bit 32)
-    unsigned long long p1def;  // undecided cylinder-box pairs at phase-1 waypoints
-    unsigned long long pad;
-};
-struct WqEnt {  // feasible-list entry
-    unsigned long long cost, idx;
-};
-struct SsppWQ {
-    KScene sc;
-    int has_scene, ablate, sampler;
-    int p, n, W, npert;
-    double sigma;
-    unsigned long long seed;
-    long long first_id, B, step_stride;
-    int steps;
-    int cpw, g1, n1, npts, lpc, nchunk, npg, arc_all, hull;
-    unsigned tps, ntiles, nps;  // tiles per step, tiles, items per survivor (nchunk * npg)
-    long long cap;              // candidates the record / queue buffers hold
-    WqCtr* ctr;
-    WqStep* stp;
-    WqSurv* surv;               // [cap]
-    double* spert;              // survivors' perturbed control points [cap][npert]
-    unsigned* queue;            // [kWqShards][cap] record indices
-    WqEnt* list;                // feasible lists [step][B]
-};
-#define WQ_RLX __ATOMIC_RELAXED
-#define WQ_AG __HIP_MEMORY_SCOPE_AGENT
-__device__ __forceinline__ unsigned wq_add(unsigned* p, unsigned v) {
-    return __hip_atomic_fetch_add((gu32_t*)p, v, WQ_RLX, WQ_AG);
-}
-__device__ __forceinline__ void wq_st(unsigned* p, unsigned v) { __hip_atomic_store((gu32_t*)p, v, WQ_RLX, WQ_AG); }
-__device__ __forceinline__ unsigned long long wq_ld64(const unsigned long long* p) {
-    return __hip_atomic_load((gu64_t*)const_cast<unsigned long long*>(p), WQ_RLX, WQ_AG);
-}
-__device__ __forceinline__ void wq_st64(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store((gu64_t*)p, v, WQ_RLX, WQ_AG);
-}
-__device__ __forceinline__ unsigned long long wq_add64(unsigned long long* p, unsigned long long v) {
-    return __hip_atomic_fetch_add((gu64_t*)p, v, WQ_RLX, WQ_AG);
-}
-__device__ __forceinline__ unsigned long long wq_or64(unsigned long long* p, unsigned long long v) {
-    return __hip_atomic_fetch_or((gu64_t*)p, v, WQ_RLX, WQ_AG);
-}
-__device__ __forceinline__ void wq_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ unsigned long long wq_bcast64(unsigned long long v) {
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return ((unsigned long long)hi << 32) | lo;
-}
-
-// computeArcLength (include/sspp.h:152-169) of one candidate by one wave, in the canonical
-// order of oracle/sspp_oracle.c::or_canon_sum (lpc lane partials, xor butterfly per 64 lanes,
-// 64-lane groups in order); a chord's first point is the previous lane's second (shuffle).
-template <int D, int P>
-__device__ __forceinline__ double wave_arc(const double* myc, int nch, int lpc, const double* __restrict__ atab,
-                                           const int* __restrict__ aspan) {
-    constexpr int P1 = P + 1;
-    const int lane = threadIdx.x & 63, nvw = lpc >> 6;
-    double tot = 0.0;
-    for (int v = 0; v < nvw; ++v) {  // wave-uniform
-        double acc = 0.0;
-        for (int base = v * 64; base < nch; base += lpc) {
-            const int j = base + lane, jj = j < nch ? j : nch - 1;
-            double qa[D], qb[D];
-            eval_pt<D, P>(myc, atab + (jj + 1) * P1, aspan[jj + 1], qb);
-#pragma unroll
-            for (int d = 0; d < D; ++d) qa[d] = __shfl_up(qb[d], 1, 64);
-            if (lane == 0) eval_pt<D, P>(myc, atab + jj * P1, aspan[jj], qa);
-            if (j < nch) acc = acc + dist_nd<D>(qa, qb);
-        }
-        acc = wave_sum(acc);
-        tot = v == 0 ? acc : tot + acc;
-    }
-    return tot;
-}
-
-// the exact cylinder-box test (sspd::cyl_box_overlap) of one waypoint, out of line: reached only
-// for pairs the scan left undecided, and its registers stay out of the scan loop
-template <int D, int NM, int P>
-__device__ __attribute__((noinline)) bool wq_cb_exact(const double* ctrl, const double* row, int span,
-                                                      int np, SceneT T) {
-    return cb_point_exact<D, NM, P, false>(ctrl, row, span, ~0ull, np, T);
-}
-
-// the pairs of `mask` whose rank among its set bits is g mod npg (item pair groups)
-__device__ __forceinline__ unsigned long long wq_group_mask(unsigned long long mask, int g, int npg) {
-    if (npg <= 1) return mask;
-    unsigned long long out = 0ull;
-    int r = 0;
-    for (unsigned long long m = mask; m; m &= m - 1ull, ++r)
-        if (r % npg == g) out |= m & (0ull - m);
-    return out;
-}
-
-// lane 0: one feasible-list entry (cost, id) standing for nfeas feasible candidates
-__device__ __forceinline__ void wq_append(const SsppWQ& a, int step, double cost, long long idx, unsigned nfeas) {
-    WqStep* S = a.stp + step;
-    const unsigned slot = wq_add(&S->nent, 1u);
-    WqEnt* e = a.list + (long long)step * a.B + slot;
-    wq_st64(&e->cost, (unsigned long long)__double_as_longlong(cost));
-    wq_st64(&e->idx, (unsigned long long)idx);
-    wq_add(&S->count, nfeas);
-}
-
-// whole wave: reduce step `step`'s feasible list into best[step] (the step's counters are re-armed
-// by the last k_sspp_wq2 workgroup: a step's survivor count must stay readable all launch long)
-__device__ __forceinline__ void wq_step_finish(const SsppWQ& a, int step, sspp_best* best) {
-    const int lane = threadIdx.x & 63;
-    WqStep* S = a.stp + step;
-    const unsigned ne = __builtin_amdgcn_readfirstlane(wq_add(&S->nent, 0u));
-    const unsigned cnt = __builtin_amdgcn_readfirstlane(wq_add(&S->count, 0u));
-    const WqEnt* L = a.list + (long long)step * a.B;
-    double bc = INFINITY;
-    long long bi = -1;
-    for (unsigned i = lane; i < ne; i += 64) {
-        const double c = __longlong_as_double((long long)wq_ld64(&L[i].cost));
-        const long long id = (long long)wq_ld64(&L[i].idx);
-        if (better(c, id, bc, bi)) { bc = c; bi = id; }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double oc = __shfl_xor(bc, off, 64);
-        const long long oi = __shfl_xor(bi, off, 64);
-        if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
-    }
-    if (lane == 0) {
-        if (best) {
-            best[step].cost = bi < 0 ? INFINITY : bc;
-            best[step].index = bi;
-            best[step].count = cnt;
-            best[step].reserved = 0;
-        }
-    }
-}
-
-// ---------------------------------------------------------------- k_sspp_c2f, fused survivor queue
-// A many-step launch is bounded by its workgroups with phase-1 survivors: a feasible survivor's
-// remaining waypoints x every pair run on that workgroup's single wave (16k shader clocks per
-// survivor against ~50k for the rest of the workgroup).  With FQ the survivors are shared inside a
-// GROUP of fq_gs consecutive workgroups of one step (dispatched together):
-//   publish  a workgroup's survivors become entries of its group's queue (k_sspp_wq2's records
-//            and items: nchunk x npg items per survivor);
-//   drain    every member then claims the group's items (compare-and-swap, never past the
-//            published count) until none is left, and leaves.  A claim waits only for the entry of
-//            a survivor whose producer is running (it bumped the tail first); a member that finds
-//            the queue empty leaves, and a producer drains its own items if nobody else does.
-// A survivor's last item decides it (the pending/hit word): feasible -> arc length (canonical
-// order), outputs, one entry in its step's list.  Only the group's members touch its counters
-// (at most fq_gs contenders per word: a chip-wide queue measured ~1000x slower from contention).
-// gcnt = member exits + decisions - survivors published; a member publishes its -ns before its
-// items become claimable and adds its +1 after its drain, so gcnt reaches the group size exactly
-// at the last exit, after every decision: that member re-arms the group and counts it on its
-// step; the step's last group reduces the step's list into best[step] (findBestPath: lowest arc,
-// lowest id) and re-arms the step.  Hand-offs as in k_sspp_wq2: sc1 stores drained before the
-// atomic that signals them, sc1 loads after it.
-struct FqGroup {  // one 64-byte line per group; zero between launches
-    unsigned head, tail;
-    int gcnt;
-    unsigned pad[13];
-};
-__device__ __forceinline__ int fq_add(int* p, int v) {
-    return __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)p, v, WQ_RLX, WQ_AG);
-}
-__device__ __forceinline__ unsigned wq_ld(const unsigned* p) {
-    return __hip_atomic_load((gu32_t*)const_cast<unsigned*>(p), WQ_RLX, WQ_AG);
-}
-
-// whole wave: findBestPath over step `step`'s list into best0[step], then the step's re-arm
-__device__ __forceinline__ void fq_step_finish(const SsppC2F& a, int step, sspp_best* best0) {
-    const int lane = threadIdx.x & 63;
-    WqStep* S = a.fq_stp + step;
-    const unsigned ne = __builtin_amdgcn_readfirstlane(wq_add(&S->nent, 0u));
-    const unsigned cnt = __builtin_amdgcn_readfirstlane(wq_add(&S->count, 0u));
-    const WqEnt* L = a.fq_list + (long long)step * a.B;
-    double bc = INFINITY;
-    long long bi = -1;
-    for (unsigned i = lane; i < ne; i += 64) {
-        const double c = __longlong_as_double((long long)wq_ld64(&L[i].cost));
-        const long long id = (long long)wq_ld64(&L[i].idx);
-        if (better(c, id, bc, bi)) { bc = c; bi = id; }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double oc = __shfl_xor(bc, off, 64);
-        const long long oi = __shfl_xor(bi, off, 64);
-        if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
-    }
-    if (lane == 0) {
-        if (best0) {
-            best0[step].cost = bi < 0 ? INFINITY : bc;
-            best0[step].index = bi;
-            best0[step].count = cnt;
-            best0[step].reserved = 0;
-        }
-        wq_st(&S->nent, 0u);
-        wq_st(&S->count, 0u);
-        wq_st(&S->pad[0], 0u);
-    }
-}
-
-template <int D, int NM, int P, bool ONEGEOM>
-__device__ void c2f_fused_tail(const SsppC2F& a, const SceneT& T, const double* __restrict__ otab,
-                               const int* __restrict__ ospan, const double* __restrict__ atab,
-                               const int* __restrict__ aspan, const double* __restrict__ init_ctrl,
-                               double* s_ctrl, double* s_box, const int* s_feas, int step, long long cand0,
-                               int nvalid, double* arc0, unsigned char* feas0, double* ctrl_out0,
-                               sspp_best* best0) {
-    constexpr int P1 = P + 1;
-    constexpr int NB = 3 * NM;
-    const int lane = threadIdx.x & 63;
-    const int n = a.n, ndof = n * D, npert = (n - 2 * P) * D, np = a.sc.npairs;
-    const long long out0 = (long long)step * a.B + cand0;
-    const unsigned nps = a.fq_nps;
-    // this workgroup's group: fq_gs consecutive workgroups of its step
-    const int blk = (int)(cand0 / a.cpb);
-    const int gi = blk / a.fq_gs, gps = (a.nblk_step + a.fq_gs - 1) / a.fq_gs;
-    const int gsz = min(a.fq_gs, a.nblk_step - gi * a.fq_gs);
-    FqGroup* Gq = a.fq_grp + (long long)step * gps + gi;
-    unsigned* queue = a.fq_queue + ((long long)step * gps + gi) * a.fq_gcap;
-    const bool isc = lane < nvalid;
-    const bool surv = isc && s_feas[lane] != 0;
-    const unsigned long long sb = __ballot(surv);
-    const int ns = __popcll(sb);
-    if (isc && !surv) {  // phase 1 found a contact
-        feas0[out0 + lane] = 0;
-        arc0[out0 + lane] = INFINITY;
-    }
-    // ---- publish
-    if (ns > 0) {
-        unsigned base = 0;
-        if (lane == 0) {  // counted before any of its items can be claimed (hence decided)
-            fq_add(&Gq->gcnt, -ns);
-            wq_drain();
-            base = wq_add(&Gq->tail, (unsigned)ns);
-        }
-        base = __builtin_amdgcn_readfirstlane(base);
-        long long my_rec = -1;
-        int i = 0;
-        for (unsigned long long m = sb; m; m &= m - 1ull, ++i) {  // wave-uniform
-            const int g = __builtin_ctzll(m);
-            const double* c = s_ctrl + g * ndof;
-            unsigned long long hm = ~0ull;
-            if (a.hull != 0 && np <= 64) {  // the candidate-level broadphase (pair_may_touch)
-                if (lane < NB) {
-                    const int mm = lane / 3, d = lane - mm * 3, col = 7 * mm + d;
-                    double lo, hi;
-                    if (col < D) {
-                        lo = hi = c[col];
-                        for (int jj = 1; jj < n; ++jj) {
-                            const double v = c[jj * D + col];
-                            lo = v < lo ? v : lo;
-                            hi = v > hi ? v : hi;
-                        }
-                    } else {
-                        lo = hi = (double)((cmover_t)T.movers)[mm].qpos0[d];
-                    }
-                    s_box[lane] = lo;
-                    s_box[NB + lane] = hi;
-                }
-                __syncthreads();
-                bool t = false;
-                if (lane < np) {
-                    const DPair pr = load_pair((cpair_t)T.pairs + lane);
-                    const DGeom G = load_geom((cgeom_t)T.geoms + pr.gm);
-                    const int mm = (NM > 1 && G.mover == 1) ? 1 : 0;
-                    t = pair_may_touch(pr, G, s_box + 3 * mm, s_box + NB + 3 * mm);
-                }
-                hm = __ballot(t);
-                __syncthreads();
-            }
-            const long long rec = out0 + g;
-            for (int k = lane; k < npert; k += 64)
-                wq_st64((unsigned long long*)(a.fq_spert + rec * npert) + k,
-                        (unsigned long long)__double_as_longlong(c[P * D + k]));
-            if (lane == 0) {
-                WqSurv* R = a.fq_surv + rec;
-                wq_st64(&R->mask, hm);
-                wq_st64(&R->pend, (unsigned long long)nps);
-                wq_st64(&R->p1def, 0ull);
-            }
-            if (lane == i) my_rec = rec;
-        }
-        wq_drain();  // every record store of the wave is out before the entries that signal them
-        if (lane < ns) wq_st(&queue[base + (unsigned)lane], (unsigned)my_rec + 1u);  // base + ns <= gcap
-    }
-    // ---- drain the group's queue
-    for (;;) {
-        unsigned h = 0;
-        if (lane == 0) {
-            h = wq_ld(&Gq->head);
-            for (;;) {
-                const unsigned long long lim = (unsigned long long)wq_ld(&Gq->tail) * nps;
-                if ((unsigned long long)h >= lim) { h = ~0u; break; }
-                if (__hip_atomic_compare_exchange_strong((gu32_t*)&Gq->head, &h, h + 1u, WQ_RLX, WQ_RLX, WQ_AG))
-                    break;
-            }
-        }
-        h = __builtin_amdgcn_readfirstlane(h);
-        if (h == ~0u) break;
-        const unsigned e = h / nps, r = h - e * nps;
-        const unsigned chunk = r / (unsigned)a.fq_npg;
-        const int grp = (int)(r - chunk * (unsigned)a.fq_npg);
-        unsigned* qe = queue + e;
-        unsigned v = 0;
-        if (lane == 0) {  // its producer is running (it bumped the tail): a bounded wait
-            for (int it = 0; it < (1 << 22); ++it) {
-                v = wq_ld(qe);
-                if (v) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (!v) wq_st(&a.fq_ctr->error[0], 2u);
-        }
-        v = __builtin_amdgcn_readfirstlane(v);
-        if (!v) continue;  // diagnostic only (sspp_debug_job_error)
-        const long long rec = (long long)v - 1;
-        WqSurv* R = a.fq_surv + rec;
-        const unsigned long long mask = wq_group_mask(wq_bcast64(wq_ld64(&R->mask)), grp, a.fq_npg);
-        const bool hit0 = (wq_bcast64(wq_ld64(&R->pend)) >> 32) != 0ull;  // a hint: may lag
-        __syncthreads();  // the previous item's reads of s_ctrl are done
-        for (int rr = lane; rr < ndof; rr += 64) {
-            double x = init_ctrl[rr];
-            const int k = rr - P * D;
-            if (k >= 0 && k < npert)
-                x = __longlong_as_double((long long)wq_ld64((const unsigned long long*)(a.fq_spert + rec * npert) + k));
-            s_ctrl[rr] = x;
-        }
-        __syncthreads();
-        const int j = a.n1 + (int)chunk * 64 + lane;
-        const bool scan = !hit0 && mask != 0ull;
-        const bool live = scan && j < a.npts;
-        const int row = live ? j : 0;
-        bool ghit = false, dfr = false;
-        if (scan) {
-            double q[D];
-            eval_pt<D, P>(s_ctrl, otab + row * P1, ospan[row], q);
-            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mask, mask, ~0ull, nullptr, a.sc, T, dfr);
-        }
-        const bool anyhit = __ballot(ghit) != 0ull;
-        unsigned long long prev = 0ull;
-        if (lane == 0) {
-            if (anyhit) wq_or64(&R->pend, 1ull << 32);
-            prev = wq_add64(&R->pend, ~0ull);  // pending - 1; returns the hit bit with the count
-        }
-        prev = wq_bcast64(prev);
-        if ((unsigned)prev != 1u) continue;
-        // ---- the survivor's last item: decide it
-        const bool bad = (prev >> 32) != 0ull;
-        double t = INFINITY;
-        if (!bad) t = wave_arc<D, P>(s_ctrl, a.W - 1, a.lpc, atab, aspan);
-        if (!bad && ctrl_out0 && a.ctrl_feas)
-            for (int k = lane; k < ndof; k += 64) ctrl_out0[rec * ndof + k] = s_ctrl[k];
-        if (lane == 0) {
-            feas0[rec] = bad ? 0 : 1;
-            arc0[rec] = t;
-            if (!bad) {
-                WqStep* S = a.fq_stp + step;
-                const unsigned slot = wq_add(&S->nent, 1u);
-                WqEnt* en = a.fq_list + (long long)step * a.B + slot;
-                wq_st64(&en->cost, (unsigned long long)__double_as_longlong(t));
-                wq_st64(&en->idx, (unsigned long long)(a.first_id + step * a.step_stride + (rec - (long long)step * a.B)));
-                wq_add(&S->count, 1u);
-            }
-            wq_st(qe, 0u);  // every claimer of this entry has read it (their items came first)
-            wq_drain();     // the list entry is out before the count that signals it
-            fq_add(&Gq->gcnt, 1);
-        }
-    }
-    // ---- leave: the group's last member re-arms it and counts it on its step
-    int done = 0;
-    if (lane == 0) {
-        done = fq_add(&Gq->gcnt, 1) + 1 == gsz;
-        if (done) {
-            wq_st(&Gq->head, 0u);
-            wq_st(&Gq->tail, 0u);
-            __hip_atomic_store((__attribute__((address_space(1))) int*)&Gq->gcnt, 0, WQ_RLX, WQ_AG);
-            done = wq_add(&a.fq_stp[step].pad[0], 1u) + 1u == (unsigned)gps ? 2 : 1;
-        }
-    }
-    done = __builtin_amdgcn_readfirstlane(done);
-    if (done == 2) fq_step_finish(a, step, best0);
-}
-
-#ifndef SSPP_WQ1_WAVES_PER_EU
-#define SSPP_WQ1_WAVES_PER_EU 4
-#endif
-#ifndef SSPP_WQ2_WAVES_PER_EU
-#define SSPP_WQ2_WAVES_PER_EU 4
-#endif
-template <int D, int NM, int P, bool ONEGEOM>
-__global__ __launch_bounds__(64, SSPP_WQ1_WAVES_PER_EU) void k_sspp_wq1(
-    SsppWQ a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
-    const double* __restrict__ atab, const int* __restrict__ aspan,
-    const double* __restrict__ init_ctrl, const double* __restrict__ limits,
-    const double* __restrict__ ctrl_in, double* __restrict__ ctrl_out, double* __restrict__ arc,
-    unsigned char* __restrict__ feasible) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int P1 = P + 1;
-    constexpr int NB = 3 * NM;
-    if (a.ablate & 64) return;  // profiling: launch + dispatch cost only
-    const int lane = threadIdx.x;
-    const int n = a.n, ndof = n * D, cpw = a.cpw, g1 = a.g1, lg1 = __builtin_ctz(g1);
-    const int np = a.sc.npairs, npert = a.npert;
-    double* s_ctrl = smem;                // [cpw][ndof]
-    double* s_box = s_ctrl + cpw * ndof;  // [2][NB] a survivor's control-point AABB
-    const bool collide_on = a.has_scene && !(a.ablate & 2);
-    const unsigned long long glow = g1 == 64 ? ~0ull : ((1ull << g1) - 1ull);
-    const unsigned id = blockIdx.x;
-    const int step = (int)(id / a.tps);
-    const long long cand0 = (long long)(id - (unsigned)step * a.tps) * cpw;
-    const int nvalid = (int)min((long long)cpw, a.B - cand0);
-    const long long gid0 = a.first_id + step * a.step_stride + cand0;
-    const long long out0 = (long long)step * a.B + cand0;
-    WQ_T(g_wq_t, id, 0, wall_clock64());
-    WQ_T(g_wq_t, id, 1, clock64());
-    // ---- control points: the initial spline + sampleWithNoise (or the caller's splines)
-    if (ctrl_in) {
-        for (int e = lane; e < nvalid * ndof; e += 64) s_ctrl[e] = ctrl_in[cand0 * ndof + e];
-    } else {
-        for (int rr = lane; rr < ndof; rr += 64) {
-            const double v0 = init_ctrl[rr];
-            for (int s2 = 0; s2 < cpw; ++s2) s_ctrl[s2 * ndof + rr] = v0;
-        }
-        __syncthreads();
-        if (!(a.ablate & 1)) {
-            const int nq = sample_items(a.sampler, npert), total = nvalid * nq;
-            for (int t = lane; t < total; t += 64) {
-                const int sl = t / nq, m = t - sl * nq;
-                sample_item(a.sampler, a.seed, (unsigned long long)(gid0 + sl), m, npert, D, a.sigma, limits,
-                            s_ctrl + sl * ndof + P * D);
-            }
-        }
-    }
-    __syncthreads();
-    if (ctrl_out) {
-        double* dst = ctrl_out + out0 * ndof;
-        for (int e = lane; e < nvalid * ndof; e += 64) dst[e] = s_ctrl[e];
-    }
-    WQ_T(g_wq_t, id, 2, clock64());
-    // ---- phase 1: g1 lanes per candidate, the first n1 coarse-to-fine waypoints, every pair
-    bool ghit = false, dfr = false;
-    const bool scan = collide_on && !a.sc.static_block;
-    {
-        const int g = lane >> lg1, l = lane & (g1 - 1);
-        if (scan) {
-            const bool live = g < nvalid && l < a.n1 && !(a.ablate & 16);
-            const int row = l < a.npts ? l : 0;
-            double q[D];
-            eval_pt<D, P>(s_ctrl + (g < nvalid ? g : 0) * ndof, otab + row * P1, ospan[row], q);
-            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, ~0ull, ~0ull, glow << (lane & ~(g1 - 1)), nullptr, a.sc, T, dfr);
-        }
-    }
-    WQ_T(g_wq_t, id, 3, clock64());
-    // ---- decide what phase 1 decided; queue the survivors
-    const unsigned long long hb = __ballot(ghit), db = __ballot(dfr);
-    const bool isc = lane < nvalid;
-    const int sh = isc ? lane * g1 : 0;
-    const bool chit = isc && collide_on && (a.sc.static_block || ((hb >> sh) & 1ull));
-    const bool cdef = isc && collide_on && !chit && (((db >> sh) & glow) != 0ull);
-    const bool csurv = isc && collide_on && !chit && (a.npts > a.n1 || cdef);
-    const bool cfeas = isc && !chit && !csurv;
-    const unsigned long long need = __ballot(a.arc_all ? isc : cfeas);
-    double my_arc = INFINITY;
-    for (unsigned long long m = need; m; m &= m - 1ull) {  // wave-uniform
-        const int g = __builtin_ctzll(m);
-        const double t = wave_arc<D, P>(s_ctrl + g * ndof, a.W - 1, a.lpc, atab, aspan);
-        if (lane == g) my_arc = t;
-    }
-    if (isc) {
-        if (!csurv) feasible[out0 + lane] = cfeas ? 1 : 0;
-        if (!csurv || a.arc_all) arc[out0 + lane] = (a.arc_all || cfeas) ? my_arc : INFINITY;
-    }
-    const unsigned long long fb = __ballot(cfeas);
-    if (fb) {  // the tile's decided-feasible candidates: one list entry (lowest arc, lowest id)
-        double bc = cfeas ? my_arc : INFINITY;
-        long long bi = cfeas ? gid0 + lane : -1;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double oc = __shfl_xor(bc, off, 64);
-            const long long oi = __shfl_xor(bi, off, 64);
-            if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
-        }
-        if (lane == 0) wq_append(a, step, bc, bi, (unsigned)__popcll(fb));
-    }
-    const unsigned long long sb = __ballot(csurv);
-    const int nsv = __popcll(sb);
-    WQ_T(g_wq_t, id, 4, clock64());
-    WQ_T(g_wq_t, id, 5, wall_clock64());
-    WQ_T(g_wq_t, id, 6, (unsigned long long)nsv);
-    WQ_T(g_wq_t, id, 7, (unsigned long long)__smid());
-    if (!nsv) return;
-    const int shard = (int)(id & (kWqShards - 1));
-    unsigned base = 0;
-    if (lane == 0) {
-        base = wq_add(&a.ctr->tail[shard][0], (unsigned)nsv);
-        wq_add(&a.stp[step].nsurv, (unsigned)nsv);
-    }
-    base = __builtin_amdgcn_readfirstlane(base);
-    int i = 0;
-    for (unsigned long long m = sb; m; m &= m - 1ull, ++i) {  // wave-uniform
-        const int g = __builtin_ctzll(m);
-        const double* c = s_ctrl + g * ndof;
-        unsigned long long hm = ~0ull;
-        if (a.hull != 0 && np <= 64 && !(a.ablate & 32)) {
-            // candidate-level broadphase (pair_may_touch): the control points' AABB per mover axis
-            if (lane < NB) {
-                const int mm = lane / 3, d = lane - mm * 3, col = 7 * mm + d;
-                double lo, hi;
-                if (col < D) {
-                    lo = hi = c[col];
-                    for (int jj = 1; jj < n; ++jj) {
-                        const double v = c[jj * D + col];
-                        lo = v < lo ? v : lo;
-                        hi = v > hi ? v : hi;
-                    }
-                } else {
-                    lo = hi = (double)((cmover_t)T.movers)[mm].qpos0[d];
-                }
-                s_box[lane] = lo;
-                s_box[NB + lane] = hi;
-            }
-            __syncthreads();
-            bool t = false;
-            if (lane < np) {
-                const DPair pr = load_pair((cpair_t)T.pairs + lane);
-                const DGeom G = load_geom((cgeom_t)T.geoms + pr.gm);
-                const int mm = (NM > 1 && G.mover == 1) ? 1 : 0;
-                t = pair_may_touch(pr, G, s_box + 3 * mm, s_box + NB + 3 * mm);
-            }
-            hm = __ballot(t);
-            __syncthreads();
-        }
-        const long long rec = out0 + g;
-        if (!ctrl_in)
-            for (int k = lane; k < npert; k += 64) a.spert[rec * npert + k] = c[P * D + k];
-        const int def_g = __shfl((int)cdef, g, 64);
-        if (lane == 0) {
-            WqSurv* R = a.surv + rec;
-            R->mask = hm;
-            R->pend = (unsigned long long)a.nps;  // pending = nps, hit = 0
-            R->p1def = (unsigned long long)(unsigned)def_g;
-            const unsigned slot = base + (unsigned)i;
-            if (slot < (unsigned)a.cap) a.queue[(long long)shard * a.cap + slot] = (unsigned)rec;
-            else wq_st(&a.ctr->error[0], 1u);
-        }
-    }
-}
-
-template <int D, int NM, int P, bool ONEGEOM, bool CB>
-__global__ __launch_bounds__(64, SSPP_WQ2_WAVES_PER_EU) void k_sspp_wq2(
-    SsppWQ a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
-    const double* __restrict__ atab, const int* __restrict__ aspan,
-    const double* __restrict__ init_ctrl, const double* __restrict__ ctrl_in, double* __restrict__ arc,
-    unsigned char* __restrict__ feasible, sspp_best* best) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int P1 = P + 1;
-    if (a.ablate & 64) return;
-    const int lane = threadIdx.x;
-    const int ndof = a.n * D, np = a.sc.npairs, npert = a.npert;
-    double* s_ctrl = smem;  // [ndof] the item's candidate
-    WqCtr* C = a.ctr;
-    const int shard = (int)(blockIdx.x & (kWqShards - 1));
-    // steps with no survivor: their candidates were all decided by k_sspp_wq1
-    if ((int)blockIdx.x < a.steps && a.stp[blockIdx.x].nsurv == 0u) wq_step_finish(a, (int)blockIdx.x, best);
-    const unsigned nps = a.nps;
-    const unsigned long long lim = (unsigned long long)C->tail[shard][0] * nps;
-    for (;;) {
-        unsigned id = 0;
-        if (lane == 0) id = wq_add(&C->head[shard][0], 1u);
-        id = __builtin_amdgcn_readfirstlane(id);
-        if ((unsigned long long)id >= lim) break;
-#ifdef SSPP_WG_TIMING
-        const unsigned tix = (unsigned)shard * 8192u + (id < 8192u ? id : 8191u);
-#endif
-        WQ_T(g_wq_i, tix, 0, wall_clock64());
-        WQ_T(g_wq_i, tix, 1, clock64());
-        const unsigned e = id / nps, r = id - e * nps;
-        const unsigned chunk = r / (unsigned)a.npg;
-        const int grp = (int)(r - chunk * (unsigned)a.npg);
-        const long long rec = (long long)a.queue[(long long)shard * a.cap + e];
-        const int step = (int)(rec / a.B);
-        const long long cand = rec - (long long)step * a.B;
-        WqSurv* R = a.surv + rec;
-        const unsigned long long mask = wq_group_mask(wq_bcast64(R->mask), grp, a.npg);
-        const bool p1def = R->p1def != 0ull;
-        const bool hit0 = (wq_bcast64(wq_ld64(&R->pend)) >> 32) != 0ull;  // a hint: may lag
-        if (!hit0) {
-            for (int rr = lane; rr < ndof; rr += 64) {
-                double v;
-                if (ctrl_in) {
-                    v = ctrl_in[cand * ndof + rr];
-                } else {
-                    v = init_ctrl[rr];
-                    const int k = rr - P * D;
-                    if (k >= 0 && k < npert) v = a.spert[rec * npert + k];
-                }
-                s_ctrl[rr] = v;
-            }
-        }
-        __syncthreads();
-        WQ_T(g_wq_i, tix, 2, clock64());
-        const int j = a.n1 + (int)chunk * 64 + lane;
-        const bool scan = !hit0 && mask != 0ull && !(a.ablate & 8);
-        const bool live = scan && j < a.npts;
-        const int row = live ? j : 0;
-        bool ghit = false, dfr = false;
-        if (scan) {
-            double q[D];
-            eval_pt<D, P>(s_ctrl, otab + row * P1, ospan[row], q);
-            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, mask, mask, ~0ull, nullptr, a.sc, T, dfr);
-        }
-        WQ_T(g_wq_i, tix, 3, clock64());
-        WQ_T(g_wq_i, tix, 6, (unsigned long long)__popcll(mask) | ((unsigned long long)hit0 << 32));
-        bool anyhit = __ballot(ghit) != 0ull;
-        if (CB && scan && !anyhit && __ballot(dfr) != 0ull) {
-            bool h = false;
-            if (dfr) h = wq_cb_exact<D, NM, P>(s_ctrl, otab + row * P1, ospan[row], np, T);
-            anyhit = __ballot(h) != 0ull;
-        }
-        unsigned long long prev = 0ull;
-        if (lane == 0) {
-            if (anyhit) wq_or64(&R->pend, 1ull << 32);
-            prev = wq_add64(&R->pend, ~0ull);  // pending - 1; returns the hit bit with the count
-        }
-        prev = wq_bcast64(prev);
-        if ((unsigned)prev == 1u) {  // the survivor's last item: decide it
-            bool bad = (prev >> 32) != 0ull;
-            if (CB && !bad && p1def) {  // phase 1's undecided cylinder-box pairs, exactly
-                bool h = false;
-                if (lane < a.n1) h = wq_cb_exact<D, NM, P>(s_ctrl, otab + lane * P1, ospan[lane], np, T);
-                bad = __ballot(h) != 0ull;
-            }
-            double t = INFINITY;
-            if (!bad) t = wave_arc<D, P>(s_ctrl, a.W - 1, a.lpc, atab, aspan);
-            unsigned prev_d = 0;
-            if (lane == 0) {
-                feasible[rec] = bad ? 0 : 1;
-                if (!a.arc_all) arc[rec] = t;
-                if (!bad) wq_append(a, step, t, a.first_id + step * a.step_stride + cand, 1u);
-                wq_drain();  // the list entry is out before the decision count that signals it
-                prev_d = wq_add(&a.stp[step].decided, 1u);
-            }
-            prev_d = __builtin_amdgcn_readfirstlane(prev_d);
-            if (prev_d + 1u == a.stp[step].nsurv) wq_step_finish(a, step, best);
-        }
-        WQ_T(g_wq_i, tix, 4, clock64());
-        WQ_T(g_wq_i, tix, 5, wall_clock64());
-        WQ_T(g_wq_i, tix, 7, (unsigned long long)__smid() | ((unsigned long long)((unsigned)prev == 1u) << 32) |
-                                 ((unsigned long long)anyhit << 33));
-        __syncthreads();  // LDS is free for the next item
-    }
-    // ---- leave: the last workgroup out re-arms the queue counters for the next launch
-    if (lane == 0) {
-        const unsigned nsh = (gridDim.x - (unsigned)shard + kWqShards - 1) / kWqShards;
-        if (wq_add(&C->exitc[shard][0], 1u) == nsh - 1u) {
-            const unsigned nshards = gridDim.x < (unsigned)kWqShards ? gridDim.x : (unsigned)kWqShards;
-            if (wq_add(&C->top[0], 1u) == nshards - 1u) {
-                for (int k = 0; k < kWqShards; ++k) {
-                    wq_st(&C->tail[k][0], 0u);
-                    wq_st(&C->head[k][0], 0u);
-                    wq_st(&C->exitc[k][0], 0u);
-                }
-                for (int st = 0; st < a.steps; ++st) {
-                    wq_st(&a.stp[st].nsurv, 0u);
-                    wq_st(&a.stp[st].decided, 0u);
-                    wq_st(&a.stp[st].nent, 0u);
-                    wq_st(&a.stp[st].count, 0u);
-                }
-                wq_st(&C->top[0], 0u);
-            }
-        }
-    }
 }
 
 // ---------------------------------------------------------------- TaskSpacePlanner kernel
@@ -2801,7 +1788,7 @@ struct sspp_job {
     int kind = 0;  // 0 sspp, 1 tsp
     const sspp_scene* scene = nullptr;
     int D = 0, p = 0, n = 0, W = 0, nknots = 0, K = 0, cp = 0;
-    int lpc = 0, cpb = 0, nm = 1, shared_endpoints = 0;
+    int lpc = 0, cpb = 0, nm = 1;
     size_t lds = 0;
     int64_t max_batch = 0;
     double sigma = 0.0;
@@ -2815,45 +1802,31 @@ struct sspp_job {
     double* d_mean = nullptr;
     double* d_sigma = nullptr;
     BlockBest* d_part = nullptr;
-    double* d_pert = nullptr;  // sampler output: perturbed columns [pert_steps][max_batch][(n-2p)*D]
-    int npert = 0;
-    int pert_steps = 1;        // steps per launch the sampler buffer holds
-    int insample = 0;          // sample inside the scoring kernel (SSPP_INSAMPLE=1)
-    // coarse-to-fine kernel (k_sspp_c2f; SSPP_KERNEL=0 selects the one-waypoint-per-lane k_sspp)
-    int c2f = 1, g1 = 16, cpb2 = 16, n1 = 16, nt2 = 256;
-    int fq = 0, fq_npg = 1, fq_gs = 16;  // k_sspp_c2f fused survivor queue (SSPP_FQ, SSPP_FQ_NPG, SSPP_FQ_GS)
-    int p1cap = 0;                       // k_sspp_c2f phase-1 iteration cap (SSPP_P1CAP)
-    FqGroup* d_fqgrp = nullptr;          // its group counters and queues (zero between launches)
-    unsigned* d_fqq = nullptr;
-    int64_t fq_ngrp = 0, fq_nq = 0;
-    int shape_forced = 0;      // SSPP_NT / SSPP_G1 fix the c2f shape, else it is chosen per launch
     int64_t part_cap = 0;      // BlockBest records d_part holds
+    int sampler = 0;           // 0 FP64 Box-Muller pairs (default), 1 FP32 quads (opt-in)
     int arc_all = 0;           // arc length for every candidate (else collision-free only)
-    int hull = 2;              // c2f hull broadphase (SSPP_HULL: 0 off, 1 all, 2 survivors)
-    size_t lds2 = 0;
-    double* d_otab = nullptr;  // collision rows in coarse-to-fine order
+    // k_sspp_c2f launch shape: chosen per launch from the candidates it holds unless forced by
+    // sspp_job_set_option (SSPP_OPT_SHAPE_NT / _G1, tests and tuning); the effective values of
+    // the last launch are readable (sspp_job_get_option)
+    int opt_nt = 0, opt_g1 = 0;
+    int last_nt = 0, last_g1 = 0;
+    int pair_order = 0;        // effective pair order of the tables (SSPP_ORDER_*)
+    int wp_order = 0;          // effective collision-waypoint order (SSPP_ORDER_*)
+    double prepass_ms = 0.0;   // host time of the hit-order pre-pass at creation
+    double* d_otab = nullptr;  // collision rows in the job's waypoint order
     int* d_ospan = nullptr;
-    DPair* d_pairs = nullptr;  // this job's pair table (closest-to-the-mean-path first)
+    std::vector<int> h_wps;    // that order
+    DPair* d_pairs = nullptr;  // this job's pair table (ordered)
     DPair* d_pairs_s = nullptr;  // the same without the pairs no sampled candidate can reach
     int np_full = 0, np_samp = 0, cb_full = 0, cb_samp = 0, og_full = 1, og_samp = 1;
     ArgminSync* d_sync = nullptr;  // sharded arrival counters of the fused argmin [kMaxSteps]
-    unsigned* d_dfr = nullptr;     // k_sspp_c2f -> k_sspp_cbfix counters (SsppC2F::dfr)
-    int has_cb = 0;                // the pair table has cylinder-box pairs (k_sspp_cbfix runs)
-    int sampler = 0;               // 0 FP64 Box-Muller pairs (default), 1 FP32 quads (opt-in)
-    // two-kernel work queue (k_sspp_wq1/2, SSPP_KERNEL=2; measured, not the default)
-    int wq = 0;
-    WqCtr* d_wctr = nullptr;       // launch counters
-    WqStep* d_wstp = nullptr;      // per-step decision counters [kMaxSteps]
-    WqSurv* d_wsurv = nullptr;     // survivor records [wq_cap]
-    double* d_wspert = nullptr;    // survivors' perturbed control points [wq_cap][npert]
-    unsigned* d_wqueue = nullptr;  // survivor queue shards [kWqShards][wq_cap]
-    WqEnt* d_wlist = nullptr;      // feasible lists [wq_cap]
-    int64_t wq_cap = 0;            // candidates per launch the buffers hold
-    int wq_occ = 0, wq_occ_lds = -1;  // resident k_sspp_wq2 workgroups (all CUs) at that LDS size
     std::vector<double> h_knots;   // host copies: the knot vector, and the values the device
     std::vector<double> h_stage;   // holds (init | limits; sspp_job_update_sspp skips equal updates)
     std::vector<DPair> h_pairs, h_pairs_s;
     int ctrl_feas = 0;               // k_sspp_c2f writes ctrl_out rows of feasible candidates only
+    // TaskSpacePlanner options (sspp_job_set_option): evaluation form (-1 automatic, 0 k_tsp,
+    // 1 k_tsp_pp, 2 k_tsp_pp2) and the generic (non-upright) narrowphase
+    int tsp_form = -1, tsp_generic = 0, last_form = -1;
     unsigned* d_pp_nd = nullptr;     // k_tsp_pp2 records / arrival counters (allocated on first use)
     double* d_pp_term = nullptr;
     unsigned* d_pp_arrive = nullptr;
@@ -2869,7 +1842,8 @@ struct sspp_job {
 
 namespace sspk {
 
-inline KScene kscene(const sspp_scene* s, bool tsp) {
+// generic: the TaskSpacePlanner generic box-box narrowphase even where every pair is upright
+inline KScene kscene(const sspp_scene* s, bool tsp, bool generic = false) {
     KScene k{};
     if (!s) return k;
     k.npairs = (int)s->pairs.size();
@@ -2877,7 +1851,7 @@ inline KScene kscene(const sspp_scene* s, bool tsp) {
     for (const DPair& p : s->pairs) k.onegeom &= (p.gm == s->pairs[0].gm);
     k.static_block = (!tsp && s->count_static && s->static_contacts > 0) ? 1 : 0;
     k.static_cost = tsp ? s->static_cost : 0.0;
-    k.upright = (tsp && !getenv("SSPP_TSP_GENERIC")) ? 1 : 0;  // SSPP_TSP_GENERIC: A/B and tests
+    k.upright = (tsp && !generic) ? 1 : 0;
     k.cbup = k.upright;
     for (const DPair& p : s->pairs) {
         const DGeom& g = s->geoms[p.gm];
@@ -2905,7 +1879,6 @@ inline SceneT scene_t(const sspp_scene* s) {
     return t;
 }
 
-
 struct SsppPtrs {
     const double* ctrl_in;
     double* ctrl_out;
@@ -2913,21 +1886,6 @@ struct SsppPtrs {
     unsigned char* feasible;
     sspp_best* best;
 };
-
-template <int D, int NM, int P>
-hipError_t launch_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs& o, int nblk,
-                              hipStream_t st) {
-    if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
-        hipLaunchKernelGGL((k_sspp<D, 1, P, true>), dim3(nblk), dim3(kBlock), j->lds, st, k,
-                           scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
-                           j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL((k_sspp<D, NM, P, false>), dim3(nblk), dim3(kBlock), j->lds, st, k,
-                       scene_t(j->scene), j->d_tab, j->d_span, j->d_init, j->d_limits, o.ctrl_in,
-                       j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
-    return hipGetLastError();
-}
 
 // the job's pair table: sampled candidates use the reachable subset, caller splines the full one
 inline SceneT scene_t_job(const sspp_job* j, bool sampled) {
@@ -2945,144 +1903,49 @@ inline KScene kscene_job(const sspp_job* j, bool sampled) {
     return k;
 }
 
-// k_sspp_cbfix after the scoring launch, only when the job's pairs include cylinder-box ones
-template <int D, int NM, int P, bool OG>
-hipError_t launch_cbfix(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
-                               hipStream_t st) {
-    if (!k.sc.cylbox || !k.has_scene) return hipSuccess;
-    hipLaunchKernelGGL((k_sspp_cbfix<D, NM, P, OG>), dim3(kFixBlocks), dim3(kFixThreads),
-                       sizeof(double) * j->n * D, st, k, scene_t_job(j, !o.ctrl_in), nblk / k.nblk_step, j->d_otab,
-                       j->d_ospan, j->d_init, j->d_limits, o.ctrl_in, j->d_pert, o.arc, o.feasible,
-                       j->d_part, j->d_sync, o.best);
-    return hipGetLastError();
-}
-
 template <int D, int NM, int P, int NT>
-hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
-                                hipStream_t st) {
-    const double* atab = j->d_tab + (size_t)(j->W + 1) * (P + 1);
-    const int* aspan = j->d_span + (j->W + 1);
-    if constexpr (NT == 64) {
-        if (k.fq) {  // fused survivor queue (host-checked: no cylinder-box pairs, so no k_sspp_cbfix)
-            if (NM == 1 && k.sc.onegeom)
-                hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true, 64, true>), dim3(nblk), dim3(64), k.lds, st, k,
-                                   scene_t_job(j, true), j->d_otab, j->d_ospan, atab, aspan, j->d_init,
-                                   j->d_limits, o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part,
-                                   j->d_sync, o.best);
-            else
-                hipLaunchKernelGGL((k_sspp_c2f<D, NM, P, false, 64, true>), dim3(nblk), dim3(64), k.lds, st, k,
-                                   scene_t_job(j, true), j->d_otab, j->d_ospan, atab, aspan, j->d_init,
-                                   j->d_limits, o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part,
-                                   j->d_sync, o.best);
-            return hipGetLastError();
-        }
-    }
-    if (NM == 1 && k.sc.onegeom && k.sc.npairs > 0) {
-        hipLaunchKernelGGL((k_sspp_c2f<D, 1, P, true, NT>), dim3(nblk), dim3(NT), k.lds, st, k,
-                           scene_t_job(j, !o.ctrl_in), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
-                           o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
-        const hipError_t e = hipGetLastError();
-        return e != hipSuccess ? e : launch_cbfix<D, 1, P, true>(k, j, o, nblk, st);
-    }
-    hipLaunchKernelGGL((k_sspp_c2f<D, NM, P, false, NT>), dim3(nblk), dim3(NT), k.lds, st, k,
-                       scene_t_job(j, !o.ctrl_in), j->d_otab, j->d_ospan, atab, aspan, j->d_init, j->d_limits,
-                       o.ctrl_in, j->d_pert, o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best);
-    const hipError_t e = hipGetLastError();
-    return e != hipSuccess ? e : launch_cbfix<D, NM, P, false>(k, j, o, nblk, st);
-}
-
-template <int D, int NM, int P>
-hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk,
-                             hipStream_t st) {
-    if (k.nt == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
-#ifdef SSPP_DEV_ONLY  // variant builds for experiments: robocrane shapes only (fast compile)
-    return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
-#else
-    if (k.nt == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st);
-    return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
-#endif
-}
-
-template <int D, int NM, int P, bool OG, bool CB>
-hipError_t launch_wq_t(const SsppWQ& k, sspp_job* j, const SsppPtrs& o, size_t lds, hipStream_t st) {
+hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
     const double* atab = j->d_tab + (size_t)(j->W + 1) * (P + 1);
     const int* aspan = j->d_span + (j->W + 1);
     const SceneT T = scene_t_job(j, !o.ctrl_in);
-    hipLaunchKernelGGL((k_sspp_wq1<D, NM, P, OG>), dim3(k.ntiles), dim3(64), lds, st, k, T, j->d_otab, j->d_ospan,
-                       atab, aspan, j->d_init, j->d_limits, o.ctrl_in, o.ctrl_out, o.arc, o.feasible);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const size_t lds2 = sizeof(double) * (size_t)j->n * D;
-    if (j->wq_occ_lds != (int)lds2) {  // resident k_sspp_wq2 waves: blocks per CU (occupancy API) x CUs
-        int nb = 0, dev = 0, cus = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sspp_wq2<D, NM, P, OG, CB>, 64, lds2);
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        j->wq_occ = std::max(1, nb) * std::max(1, cus);
-        j->wq_occ_lds = (int)lds2;
-    }
-    // k_sspp_wq2 workgroups: one per 16 candidates of the launch (survivors are a few %), at least
-    // one per step (steps without survivors are reduced by workgroup `step`) and per shard, at most
-    // the resident waves (SSPP_WQ_G2 overrides)
-    static const int env_g2 = [] { const char* v = getenv("SSPP_WQ_G2"); return v ? atoi(v) : 0; }();
-    long long g2 = env_g2 > 0 ? env_g2 : std::min<long long>((long long)k.steps * k.B / 16, j->wq_occ);
-    g2 = std::max<long long>(g2, std::max(k.steps, kWqShards));
-    hipLaunchKernelGGL((k_sspp_wq2<D, NM, P, OG, CB>), dim3((unsigned)g2), dim3(64), lds2, st, k, T, j->d_otab,
-                       j->d_ospan, atab, aspan, j->d_init, o.ctrl_in, o.arc, o.feasible, o.best);
+#define SSPP_LAUNCH_C2F(NMV, OGV, CBV)                                                                    \
+    hipLaunchKernelGGL((k_sspp_c2f<D, NMV, P, OGV, NT, CBV>), dim3(nblk), dim3(NT), k.lds, st, k, T, j->d_otab, \
+                       j->d_ospan, atab, aspan, j->d_init, j->d_limits, o.ctrl_in, o.ctrl_out, o.arc,      \
+                       o.feasible, j->d_part, j->d_sync, o.best)
+    const bool og = NM == 1 && k.sc.onegeom && k.sc.npairs > 0;
+    if (og && k.sc.cylbox) SSPP_LAUNCH_C2F(1, true, true);
+    else if (og) SSPP_LAUNCH_C2F(1, true, false);
+    else if (k.sc.cylbox) SSPP_LAUNCH_C2F(NM, false, true);
+    else SSPP_LAUNCH_C2F(NM, false, false);
+#undef SSPP_LAUNCH_C2F
     return hipGetLastError();
 }
 
+// two workgroup sizes: one-wave workgroups (throughput shapes) and 4-wave workgroups (a single
+// plan() batch, latency shape); DESIGN.md §5
 template <int D, int NM, int P>
-hipError_t launch_wq(const SsppWQ& k, sspp_job* j, const SsppPtrs& o, size_t lds, hipStream_t st) {
-    const bool og = NM == 1 && k.sc.onegeom && k.sc.npairs > 0;
-    if (k.sc.cylbox) return og ? launch_wq_t<D, 1, P, true, true>(k, j, o, lds, st)
-                               : launch_wq_t<D, NM, P, false, true>(k, j, o, lds, st);
-    return og ? launch_wq_t<D, 1, P, true, false>(k, j, o, lds, st) : launch_wq_t<D, NM, P, false, false>(k, j, o, lds, st);
+hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
+    if (k.nt == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
+    return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
 }
-
 
 // ---- per-dof entry points, instantiated one dof per translation unit (sspp_inst.hip, built
 // with -DSSPK_D=1..9) so the kernels compile in parallel; the host code (sspp_kernels.hip)
 // switches on the job's dof
-template <int D>
-hipError_t entry_wq(const SsppWQ& k, sspp_job* j, const SsppPtrs& o, size_t lds, hipStream_t st) {
-    if (j->nm == 2) {
-        if constexpr (D == 9) return j->p == 3 ? launch_wq<9, 2, 3>(k, j, o, lds, st) : launch_wq<9, 2, 2>(k, j, o, lds, st);
-        return hipErrorInvalidValue;
-    }
-#ifdef SSPP_DEV_ONLY
-    if (j->p != 3) return hipErrorInvalidValue;
-    return launch_wq<D, 1, 3>(k, j, o, lds, st);
-#else
-    return j->p == 3 ? launch_wq<D, 1, 3>(k, j, o, lds, st) : launch_wq<D, 1, 2>(k, j, o, lds, st);
-#endif
-}
 template <int D>
 hipError_t entry_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
     if (j->nm == 2) {
         if constexpr (D == 9) return j->p == 3 ? launch_c2f<9, 2, 3>(k, j, o, nblk, st) : launch_c2f<9, 2, 2>(k, j, o, nblk, st);
         return hipErrorInvalidValue;
     }
-#ifdef SSPP_DEV_ONLY
+#ifdef SSPP_DEV_ONLY  // variant builds for experiments: degree 3 only (fast compile)
     if (j->p != 3) return hipErrorInvalidValue;
     return launch_c2f<D, 1, 3>(k, j, o, nblk, st);
 #else
     return j->p == 3 ? launch_c2f<D, 1, 3>(k, j, o, nblk, st) : launch_c2f<D, 1, 2>(k, j, o, nblk, st);
 #endif
 }
-template <int D>
-hipError_t entry_sspp(const SsppK& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
-#ifdef SSPP_DEV_ONLY
-    (void)k; (void)j; (void)o; (void)nblk; (void)st;
-    return hipErrorInvalidValue;
-#else
-    if (j->nm == 2) {
-        if constexpr (D == 9) return j->p == 3 ? launch_sspp<9, 2, 3>(k, j, o, nblk, st) : launch_sspp<9, 2, 2>(k, j, o, nblk, st);
-        return hipErrorInvalidValue;
-    }
-    return j->p == 3 ? launch_sspp<D, 1, 3>(k, j, o, nblk, st) : launch_sspp<D, 1, 2>(k, j, o, nblk, st);
-#endif
-}
+
 // TaskSpacePlanner evaluation (k_tsp), its own translation unit (SSPK_D = 0)
 template <int Unused>
 hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* mean, const double* sigma,
@@ -3143,9 +2006,7 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
 }
 
 #define SSPK_ENTRY_DECL(X, D)                                                                             \
-    X template hipError_t entry_wq<D>(const SsppWQ&, sspp_job*, const SsppPtrs&, size_t, hipStream_t);    \
-    X template hipError_t entry_c2f<D>(const SsppC2F&, const sspp_job*, const SsppPtrs&, int, hipStream_t); \
-    X template hipError_t entry_sspp<D>(const SsppK&, const sspp_job*, const SsppPtrs&, int, hipStream_t);
+    X template hipError_t entry_c2f<D>(const SsppC2F&, const sspp_job*, const SsppPtrs&, int, hipStream_t);
 #define SSPK_TSP_DECL(X)                                                                                  \
     X template hipError_t entry_tsp<0>(const TspK&, const sspp_job*, int, const double*, const double*,    \
                                        const double*, double*, double*, double*, double*, double*, uint8_t*, \

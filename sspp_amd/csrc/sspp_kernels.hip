@@ -3,6 +3,7 @@
 // The kernels are in sspp_kern.h; their instantiations are compiled per dof in sspp_inst.hip.
 #include "sspp_kern.h"
 
+#include <chrono>
 #include <random>
 
 using namespace sspk;
@@ -21,33 +22,6 @@ SSPK_TSP_DECL(extern)
 #endif
 
 namespace sspk {
-// ---------------------------------------------------------------- candidate sampler
-// sampleWithNoise (include/sspp.h:114-130) for `steps` batches of B candidates, step s covering
-// ids first_id + s * step_stride + [0, B): one thread per (step, candidate, Box-Muller pair) over
-// the whole chip; writes the perturbed control-point columns j in [p, n-p) as
-// pert[steps][B][npert] with npert = (n-2p)*D, value = init + (sigma * z) * limits[d].
-// A separate launch at full occupancy (26 VGPRs, 8 waves/SIMD): the FP64 log/sqrt/sincospi
-// chains are latency-bound, and in the scoring kernel (3 waves/SIMD) they were 40% of its time.
-__global__ __launch_bounds__(kBlock) void k_sample_sspp(
-    unsigned long long seed, long long first_id, long long step_stride, long long B, int steps,
-    int D, int p, int npert, double sigma, const double* __restrict__ init_ctrl,
-    const double* __restrict__ limits, double* __restrict__ pert, int sampler) {
-    const int nq = sample_items(sampler, npert), per = sampler ? 4 : 2;
-    const long long t = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= (long long)steps * B * nq) return;
-    const long long sb = t / nq;
-    const int m = (int)(t - sb * nq);
-    const long long s = sb / B, b = sb - s * B;
-    const double* base = init_ctrl + p * D;
-    double* out = pert + sb * npert;
-    for (int h = 0; h < per; ++h) {
-        const int k = per * m + h;
-        if (k < npert) out[k] = base[k];
-    }
-    sample_item(sampler, seed, (unsigned long long)(first_id + s * step_stride + b), m, npert, D, sigma,
-                limits, out);
-}
-
 constexpr int kArgminThreads = 1024;
 __global__ __launch_bounds__(kArgminThreads) void k_argmin(const BlockBest* __restrict__ part,
                                                            int nparts, sspp_best* out) {
@@ -422,28 +396,52 @@ static std::vector<DPair> pairs_for_job(const sspp_scene* sc, const double* knot
     return sorted;
 }
 
-// Pair order by phase-1 hits (SSPP_PAIR_ORDER=2, the default at job creation): M host-sampled candidates (the
-// job's sigma / limits, a host normal generator — the order only steers the scan, never its
-// result), their first n1 coarse-to-fine waypoints, and per candidate the set of pairs in contact
-// at any of them; the pairs are then ordered greedily, each time the one that settles the most
-// candidates not yet settled (phase 1 stops a candidate at its first contact), the rest in
-// their previous order.
-static std::vector<DPair> order_by_hits(const sspp_scene* sc, const std::vector<DPair>& in, const double* knots,
-                                        int nknots, int p, const double* ctrl0, int D, double sigma,
-                                        const double* limits, const std::vector<int>& wps, int W) {
-    const int np = (int)in.size(), n = nknots - p - 1, nm = (int)sc->movers.size();
-    if (np < 2 || np > 64 || nm < 1 || nm > kMaxMovers) return in;
-    const int M = 256;
+// Coarse-to-fine order of the collision waypoints 0..W: breadth-first interval bisection, so
+// every prefix is spread evenly over the path.
+static std::vector<int> c2f_order(int W) {
+    std::vector<int> ord;
+    std::vector<std::pair<int, int>> cur{{0, W}}, next;
+    while (!cur.empty()) {
+        next.clear();
+        for (auto [lo, hi] : cur) {
+            if (lo > hi) continue;
+            const int mid = lo + (hi - lo) / 2;
+            ord.push_back(mid);
+            next.push_back({lo, mid - 1});
+            next.push_back({mid + 1, hi});
+        }
+        cur.swap(next);
+    }
+    return ord;
+}
+
+// Hit-order pre-pass of a sampled job (sigma > 0).  checkCollision's answer is an
+// OR over (waypoint, pair), so the order of both is free; k_sspp_c2f's phase 1 tests a prefix of
+// the waypoint order and stops a candidate at its first touching pair, so waypoints and pairs
+// that settle the most sampled candidates should come first.  M host-sampled candidates of the
+// job's distribution (its sigma and limits; host normals: the order only steers the scans, never
+// their results), the pairs each touches at the first kGrid waypoints of the bisection order
+// (an even spread over the path); then, greedily, the waypoint that settles the most candidates
+// not yet settled (up to kPick of them, the rest in bisection order), and the pairs in the same
+// way over the contacts at the first n1 chosen waypoints (the rest in their previous order).
+static void hit_order(const sspp_scene* sc, std::vector<DPair>& pairs, std::vector<int>& wps,
+                      const double* knots, int nknots, int p, const double* ctrl0, int D, double sigma,
+                      const double* limits, int W, int n1) {
+    const int np = (int)pairs.size(), n = nknots - p - 1, nm = (int)sc->movers.size();
+    if (np < 1 || np > 64 || nm < 1 || nm > kMaxMovers) return;
+    constexpr int M = 128, kGrid = 33, kPick = 8;
+    const std::vector<int> grid(wps.begin(), wps.begin() + std::min<size_t>(wps.size(), kGrid));
+    const int ng = (int)grid.size();
     std::mt19937_64 rng(0x5EEDull);
     std::normal_distribution<double> N01(0.0, 1.0);
-    std::vector<uint64_t> hit(M, 0ull);
+    std::vector<uint64_t> hit((size_t)M * ng, 0ull);
     std::vector<double> c((size_t)n * D);
     for (int m = 0; m < M; ++m) {
         for (size_t e = 0; e < c.size(); ++e) c[e] = ctrl0[e];
         for (int jj = p; jj < n - p; ++jj)
             for (int d = 0; d < D; ++d) c[(size_t)jj * D + d] += sigma * N01(rng) * limits[d];
-        for (int w : wps) {
-            const double u = (double)w / W;
+        for (int gi = 0; gi < ng; ++gi) {
+            const double u = (double)grid[gi] / W;
             const int sp = span_of(u, p, knots, nknots);
             double N[kMaxP + 1];
             basis_funcs(u, p, sp, knots, N);
@@ -464,9 +462,9 @@ static std::vector<DPair> order_by_hits(const sspp_scene* sc, const std::vector<
                 quat2mat(qp + 3, mR[mv]);
                 for (int k = 0; k < 3; ++k) mp[mv][k] = qp[k];
             }
+            uint64_t bits = 0ull;
             for (int k = 0; k < np; ++k) {
-                if ((hit[m] >> k) & 1ull) continue;
-                const DPair& pr = in[k];
+                const DPair& pr = pairs[k];
                 const DGeom& G = sc->geoms[pr.gm];
                 const int mv = G.mover > 0 ? G.mover : 0;
                 double gp[3], gm[9], t3[3], op[3], om[9];
@@ -491,27 +489,55 @@ static std::vector<DPair> order_by_hits(const sspp_scene* sc, const std::vector<
                 const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
                 const int nc = gfirst ? collide<false>(G.type, gp, gm, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd)
                                       : collide<false>(pr.otype, op, om, pr.osize, G.type, gp, gm, G.size, pr.margin, &nd);
-                if (nc > 0) hit[m] |= 1ull << k;
+                if (nc > 0) bits |= 1ull << k;
             }
+            hit[(size_t)m * ng + gi] = bits;
         }
     }
-    std::vector<char> used(np, 0), settled(M, 0);
+    // waypoints
+    std::vector<char> settled(M, 0), used(ng, 0);
+    std::vector<int> pick;
+    for (int it = 0; it < kPick; ++it) {
+        int best = -1, bc = 0;
+        for (int gi = 0; gi < ng; ++gi) {
+            if (used[gi]) continue;
+            int cnt = 0;
+            for (int m = 0; m < M; ++m) cnt += !settled[m] && hit[(size_t)m * ng + gi] != 0ull;
+            if (cnt > bc) { bc = cnt; best = gi; }
+        }
+        if (best < 0) break;
+        used[best] = 1;
+        pick.push_back(best);
+        for (int m = 0; m < M; ++m) settled[m] |= hit[(size_t)m * ng + best] != 0ull;
+    }
+    if (pick.empty()) return;  // nothing touches: keep the bisection order and the pair order
+    std::vector<int> order;
+    std::vector<char> taken(W + 1, 0);
+    for (int gi : pick) { order.push_back(grid[gi]); taken[grid[gi]] = 1; }
+    for (int w : wps) if (!taken[w]) order.push_back(w);
+    wps.swap(order);
+    // pairs, over the contacts at the first n1 chosen waypoints
+    std::vector<uint64_t> cand(M, 0ull);
+    for (int m = 0; m < M; ++m)
+        for (size_t i = 0; i < pick.size() && (int)i < std::max(1, n1); ++i) cand[m] |= hit[(size_t)m * ng + pick[i]];
+    std::vector<char> pused(np, 0);
+    std::fill(settled.begin(), settled.end(), 0);
     std::vector<DPair> out;
     for (;;) {
         int best = -1, bc = 0;
         for (int k = 0; k < np; ++k) {
-            if (used[k]) continue;
+            if (pused[k]) continue;
             int cnt = 0;
-            for (int m = 0; m < M; ++m) cnt += !settled[m] && ((hit[m] >> k) & 1ull);
+            for (int m = 0; m < M; ++m) cnt += !settled[m] && ((cand[m] >> k) & 1ull);
             if (cnt > bc) { bc = cnt; best = k; }
         }
         if (best < 0) break;
-        used[best] = 1;
-        out.push_back(in[best]);
-        for (int m = 0; m < M; ++m) if ((hit[m] >> best) & 1ull) settled[m] = 1;
+        pused[best] = 1;
+        out.push_back(pairs[best]);
+        for (int m = 0; m < M; ++m) if ((cand[m] >> best) & 1ull) settled[m] = 1;
     }
-    for (int k = 0; k < np; ++k) if (!used[k]) out.push_back(in[k]);
-    return out;
+    for (int k = 0; k < np; ++k) if (!pused[k]) out.push_back(pairs[k]);
+    pairs.swap(out);
 }
 
 // Pairs a SAMPLED candidate can reach (job-level broadphase, exact).  sampleWithNoise moves
@@ -562,31 +588,6 @@ static void table_flags(const sspp_scene* sc, const std::vector<DPair>& t, int* 
     }
 }
 
-// (re)build the job's two pair tables for its current initial spline / sigma / limits: the full
-// table ordered for the mean path (pairs_for_job) and its sample-mode subset (reachable_pairs);
-// stream == nullptr: synchronous upload into fresh buffers, else asynchronous into the existing ones
-static int set_job_pairs(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, bool create,
-                         void* stream, size_t pin_off = 0);
-
-// Coarse-to-fine order of the collision waypoints 0..W: breadth-first interval bisection, so
-// every prefix is spread evenly over the path (k_sspp_c2f phase 1 tests a prefix).
-static std::vector<int> c2f_order(int W) {
-    std::vector<int> ord;
-    std::vector<std::pair<int, int>> cur{{0, W}}, next;
-    while (!cur.empty()) {
-        next.clear();
-        for (auto [lo, hi] : cur) {
-            if (lo > hi) continue;
-            const int mid = lo + (hi - lo) / 2;
-            ord.push_back(mid);
-            next.push_back({lo, mid - 1});
-            next.push_back({mid + 1, hi});
-        }
-        cur.swap(next);
-    }
-    return ord;
-}
-
 // Basis rows for a list of parameters (same A2.1/A2.2 code as the device header).
 static int upload_basis(const std::vector<double>& us, int p, const double* knots, int nknots,
                         double** d_tab, int** d_span) {
@@ -601,34 +602,48 @@ static int upload_basis(const std::vector<double>& us, int p, const double* knot
     return upload(d_span, sp.data(), sp.size());
 }
 
-// The job's pair tables (ordered; the sampled candidates' reachable subset).  create: allocate
-// and copy synchronously; otherwise queue the copies on `stream` from the pinned staging at
-// byte offset `pin_off` (the caller sized it for both tables).
-static int set_job_pairs(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, bool create,
-                         void* stream, size_t pin_off) {
+// phase-1 lanes per candidate of the throughput shape (one-wave workgroups)
+constexpr int kThroughputG1 = 4;
+
+// The job's scan orders for its initial spline / sigma / limits: the pair table ordered by the
+// mean-path gap (pairs_for_job), refined with the collision-waypoint order by the hit-order
+// pre-pass (order 2: sampled jobs at creation), and its sample-mode subset (reachable_pairs).
+// create: the waypoint order and both tables are (re)uploaded synchronously; otherwise the pair
+// tables are queued on `stream` from the pinned staging at byte offset `pin_off` (the caller
+// sized it for both) and the waypoint order stays.
+static int set_job_tables(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, int order,
+                          bool create, void* stream, size_t pin_off = 0) {
     const sspp_scene* sc = j->scene;
-    // SSPP_PAIR_ORDER: 0 = scene order (profiling), 1 = mean-path gap order, 2 = phase-1 hit order
-    // on top of it.  Default: 2 when the job is created (+0.55 ms of host work, paid once), 1 on
-    // sspp_job_update (a re-plan at a new query stays on the microsecond host path).
-    const char* po = getenv("SSPP_PAIR_ORDER");
-    const int order = po ? atoi(po) : (create ? 2 : 1);
-    j->h_pairs = order == 0 ? sc->pairs : pairs_for_job(sc, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D);
-    if (order == 2 && j->kind == 0) {
-        std::vector<int> wps = c2f_order(j->W);
-        wps.resize(std::min<size_t>(wps.size(), (size_t)std::max(1, j->g1)));
-        j->h_pairs = order_by_hits(sc, j->h_pairs, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D, sigma,
-                                   limits, wps, j->W);
+    std::vector<int> wps = c2f_order(j->W);
+    if (sc && !sc->pairs.empty()) {
+        j->h_pairs = order == 0 ? sc->pairs : pairs_for_job(sc, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D);
+        if (order == 2 && create) {
+            const auto t0 = std::chrono::steady_clock::now();
+            hit_order(sc, j->h_pairs, wps, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D, sigma, limits, j->W,
+                      kThroughputG1);
+            j->prepass_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+        j->h_pairs_s = reachable_pairs(sc, j->h_pairs, init_ctrl, j->n, j->D, j->p, sigma, limits, j->sampler);
+        table_flags(sc, j->h_pairs, &j->np_full, &j->cb_full, &j->og_full);
+        table_flags(sc, j->h_pairs_s, &j->np_samp, &j->cb_samp, &j->og_samp);
     }
-    const char* pr = getenv("SSPP_REACH");  // 0 = no job-level culling (profiling)
-    j->h_pairs_s = (pr && atoi(pr) == 0) ? j->h_pairs
-                                         : reachable_pairs(sc, j->h_pairs, init_ctrl, j->n, j->D, j->p, sigma, limits, j->sampler);
-    table_flags(sc, j->h_pairs, &j->np_full, &j->cb_full, &j->og_full);
-    table_flags(sc, j->h_pairs_s, &j->np_samp, &j->cb_samp, &j->og_samp);
+    j->pair_order = order;
+    if (create) {
+        j->wp_order = order == 2 ? 2 : 0;
+        j->h_wps = wps;
+        std::vector<double> uo;
+        for (int i : wps) uo.push_back((double)i / j->W);
+        if (j->d_otab) { (void)hipFree(j->d_otab); j->d_otab = nullptr; }
+        if (j->d_ospan) { (void)hipFree(j->d_ospan); j->d_ospan = nullptr; }
+        int rc = upload_basis(uo, j->p, j->h_knots.data(), j->nknots, &j->d_otab, &j->d_ospan);
+        if (rc) return rc;
+    }
+    if (!sc || sc->pairs.empty()) return SSPP_OK;
     const size_t bytes = sizeof(DPair) * j->h_pairs.size(), bytes_s = sizeof(DPair) * j->h_pairs_s.size();
     if (create) {
-        int rc;
-        if ((rc = upload(&j->d_pairs, j->h_pairs.data(), j->h_pairs.size()))) return rc;
-        HIPCHK(hipMalloc((void**)&j->d_pairs_s, std::max<size_t>(bytes, sizeof(DPair))));
+        if (!j->d_pairs) HIPCHK(hipMalloc((void**)&j->d_pairs, sizeof(DPair) * std::max<size_t>(1, sc->pairs.size())));
+        if (!j->d_pairs_s) HIPCHK(hipMalloc((void**)&j->d_pairs_s, sizeof(DPair) * std::max<size_t>(1, sc->pairs.size())));
+        HIPCHK(hipMemcpy(j->d_pairs, j->h_pairs.data(), bytes, hipMemcpyHostToDevice));
         if (bytes_s) HIPCHK(hipMemcpy(j->d_pairs_s, j->h_pairs_s.data(), bytes_s, hipMemcpyHostToDevice));
         return SSPP_OK;
     }
@@ -658,23 +673,20 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     if (max_batch < 1) return sspp::set_error(SSPP_E_INVAL, "max_batch must be >= 1");
     if (scene && (scene->mode != SSPP_MODE_QPOS || scene->dof != D))
         return sspp::set_error(SSPP_E_INVAL, "scene was not bound for this dof");
+    // the largest per-candidate footprint (caller splines, n x D doubles) must fit the latency
+    // shape's 4 candidates in 64 KiB of LDS
+    if ((size_t)4 * n * D * sizeof(double) + 4096 > 64 * 1024)
+        return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS (n_ctrl x dof)");
     auto* j = new sspp_job();
     j->kind = 0; j->scene = scene; j->D = D; j->p = p; j->n = n; j->W = W;
     j->nknots = n + p + 1; j->sigma = a->sigma; j->seed = a->seed; j->max_batch = max_batch;
     j->arc_all = a->arc_all ? 1 : 0;
+    j->sampler = a->sampler ? 1 : 0;
     j->h_knots.assign(a->knots, a->knots + j->nknots);
     j->nm = scene ? (int)scene->movers.size() : 1;
     if (j->nm < 1) j->nm = 1;
     j->lpc = lanes_for(W - 1);
-    j->cpb = kBlock / j->lpc;
-    // endpoints are candidate-independent when the knot vector is clamped (sampled mode)
-    bool clamped = true;
-    for (int i = 0; i <= p; ++i) clamped = clamped && a->knots[i] == a->knots[0] && a->knots[n + i] == a->knots[n + p];
-    j->shared_endpoints = clamped ? 1 : 0;
-    j->lds = sizeof(double) * ((size_t)j->cpb * n * D + kBlock / 64 + 4) + sizeof(int) * (j->cpb + 1);
-    if (j->lds > 160 * 1024) { delete j; return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS"); }
     int rc;
-    const int64_t nblk = (max_batch + j->cpb - 1) / j->cpb;
     std::vector<double> us;
     for (int i = 0; i <= W; ++i) us.push_back((double)i / W);            // collision grid
     for (int i = 0; i < W; ++i) us.push_back(W > 1 ? (double)i / (W - 1) : 0.0);  // arc-length grid
@@ -687,85 +699,18 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     }
     j->h_stage.assign(a->init_ctrl, a->init_ctrl + (size_t)n * D);
     j->h_stage.insert(j->h_stage.end(), a->limits, a->limits + D);
-    j->npert = (n - 2 * p) * D;
-    if (j->npert < 0) j->npert = 0;
-    {  // 1: k_sspp_c2f (default), 2: k_sspp_wq1 + k_sspp_wq2, 0: k_sspp
-        const char* e = getenv("SSPP_KERNEL");
-        const int kern = e ? atoi(e) : 1;
-        j->c2f = kern != 0;
-        j->wq = kern == 2;
-    }
-    j->sampler = a->sampler ? 1 : 0;
-    { const char* e = getenv("SSPP_SAMPLER"); if (e) j->sampler = atoi(e) ? 1 : 0; }
-    // fused survivor queue: opt-in (measured slower: the group queues' device-scope atomics cost
-    // more than the balance they buy)
-    { const char* e = getenv("SSPP_FQ"); j->fq = e ? atoi(e) : 0; }
-    { const char* e = getenv("SSPP_FQ_NPG"); j->fq_npg = e ? std::max(1, std::min(8, atoi(e))) : 1; }
-    { const char* e = getenv("SSPP_FQ_GS"); j->fq_gs = e ? std::max(1, std::min(256, atoi(e))) : 16; }
-    { const char* e = getenv("SSPP_P1CAP"); j->p1cap = e ? std::max(0, atoi(e)) : 0; }
-    // default: c2f draws inside the scoring kernel (SSPP_INSAMPLE=0: chip-wide k_sample_sspp; measured slower)
-    { const char* e = getenv("SSPP_INSAMPLE"); j->insample = e ? atoi(e) : (j->c2f ? 1 : 0); }
-    { const char* e = getenv("SSPP_HULL"); j->hull = e ? atoi(e) : 2; }
-    {
-        // defaults measured on MI355X (robocrane, 32 steps/launch, 4 streams):
-        // one-wave workgroups of 16 candidates x 4 phase-1 lanes — 1.84 G cand/s against 1.56 G
-        // for 8 x 8 and 1.40 G for 256 x 8 (the kernel is VALU-issue bound: fewer lanes per
-        // candidate waste fewer pair-loop iterations on lanes that have already hit)
-        const char* e = getenv("SSPP_G1");
-        int g1 = e ? atoi(e) : 4;
-        if (g1 != 4 && g1 != 8 && g1 != 16 && g1 != 32 && g1 != 64) g1 = 8;
-        const char* t = getenv("SSPP_NT");
-        int nt = t ? atoi(t) : 64;
-        if (nt != 64 && nt != 128 && nt != 256) nt = 64;
-        j->shape_forced = (e || t) ? 1 : 0;
-        j->g1 = g1;
-        j->nt2 = nt;
-        j->cpb2 = nt / g1;
-        j->n1 = std::min(g1, W + 1);
-        std::vector<int> ord = c2f_order(W);
-        std::vector<double> uo;
-        for (int i : ord) uo.push_back((double)i / W);
-        if ((rc = upload_basis(uo, p, a->knots, j->nknots, &j->d_otab, &j->d_ospan))) {
-            sspp_job_free(j);
-            return rc;
-        }
-        if (scene && !scene->pairs.empty() && (rc = set_job_pairs(j, a->init_ctrl, a->sigma, a->limits, true, nullptr))) {
-            sspp_job_free(j);
-            return rc;
-        }
-        const int nm = j->nm < 1 ? 1 : j->nm;
-        const int rbox = std::max(6 * nm, lanes_for(W - 1) / 64 + 1);  // k_sspp_c2f: s_box / s_vsum + s_arc
-        j->lds2 = sizeof(double) * ((size_t)j->cpb2 * (n * D + rbox) + D) +
-                  sizeof(unsigned long long) * j->cpb2 + sizeof(int) * (3 * j->cpb2 + 1);
-        if (j->lds2 > 64 * 1024) j->c2f = 0;
-    }
-    if (j->npert > 0 && !j->insample && j->c2f) {  // room for kMaxSteps steps, capped at 256 MiB
-        const size_t per_step = sizeof(double) * (size_t)max_batch * j->npert;
-        j->pert_steps = (int)std::max<size_t>(1, std::min<size_t>(kMaxSteps, ((size_t)256 << 20) / per_step));
-    }
-    if (j->npert > 0 && hipMalloc((void**)&j->d_pert, sizeof(double) * (size_t)max_batch * j->npert * j->pert_steps) != hipSuccess) {
+    // hit order only for jobs that sample (sigma > 0): a scoring job's candidates are the caller's
+    const int order = a->sigma != 0.0 ? 2 : 1;
+    if ((rc = set_job_tables(j, a->init_ctrl, a->sigma, a->limits, order, true, nullptr))) {
         sspp_job_free(j);
-        return sspp::set_error(SSPP_E_NOMEM, "hipMalloc sampler buffer");
+        return rc;
     }
-    // one record per workgroup: at most max_batch workgroups per step whatever the layout
-    // one record per workgroup and step: k_sspp has nblk workgroups per batch (one step per
-    // launch), k_sspp_c2f ceil(max_batch / cpb2) per step and up to kMaxSteps steps per launch
-    const int64_t nrec = std::max<int64_t>(nblk, ((max_batch + 15) / 16) * 4);  // grown per launch (c2f_reserve)
-    if (scene)
-        for (const DPair& pr : scene->pairs) {
-            const int t1 = scene->geoms[pr.gm].type, t2 = pr.otype;
-            if ((t1 == 5 && t2 == 6) || (t1 == 6 && t2 == 5)) j->has_cb = 1;
-        }
+    // one BlockBest per workgroup and step (grown per launch when a shape needs more)
+    const int64_t nrec = std::max<int64_t>(64, (max_batch + 3) / 4);
     j->part_cap = nrec;
     if (hipMalloc((void**)&j->d_part, sizeof(BlockBest) * nrec) != hipSuccess ||
         hipMalloc((void**)&j->d_sync, sizeof(ArgminSync) * kMaxSteps) != hipSuccess ||
-        hipMemset(j->d_sync, 0, sizeof(ArgminSync) * kMaxSteps) != hipSuccess ||
-        hipMalloc((void**)&j->d_dfr, sizeof(unsigned) * 2) != hipSuccess ||
-        hipMemset(j->d_dfr, 0, sizeof(unsigned) * 2) != hipSuccess ||
-        hipMalloc((void**)&j->d_wctr, sizeof(WqCtr)) != hipSuccess ||
-        hipMemset(j->d_wctr, 0, sizeof(WqCtr)) != hipSuccess ||
-        hipMalloc((void**)&j->d_wstp, sizeof(WqStep) * kMaxSteps) != hipSuccess ||
-        hipMemset(j->d_wstp, 0, sizeof(WqStep) * kMaxSteps) != hipSuccess) {
+        hipMemset(j->d_sync, 0, sizeof(ArgminSync) * kMaxSteps) != hipSuccess) {
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
     }
@@ -773,83 +718,23 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     return SSPP_OK;
 }
 
-// ---- k_sspp_wq launch: buffers sized for the launch, grid = resident one-wave workgroups
-static int wq_reserve(sspp_job* j, int64_t cands) {
-    if (cands <= j->wq_cap) return SSPP_OK;
-    (void)hipDeviceSynchronize();  // earlier launches may still use the old buffers
-    if (j->d_wsurv) (void)hipFree(j->d_wsurv);
-    if (j->d_wspert) (void)hipFree(j->d_wspert);
-    if (j->d_wqueue) (void)hipFree(j->d_wqueue);
-    if (j->d_wlist) (void)hipFree(j->d_wlist);
-    j->d_wsurv = nullptr; j->d_wspert = nullptr; j->d_wqueue = nullptr; j->d_wlist = nullptr; j->wq_cap = 0;
-    const size_t np = (size_t)std::max(1, j->npert);
-    if (hipMalloc((void**)&j->d_wsurv, sizeof(WqSurv) * cands) != hipSuccess ||
-        hipMalloc((void**)&j->d_wspert, sizeof(double) * np * cands) != hipSuccess ||
-        hipMalloc((void**)&j->d_wqueue, sizeof(unsigned) * kWqShards * cands) != hipSuccess ||
-        hipMalloc((void**)&j->d_wlist, sizeof(WqEnt) * cands) != hipSuccess ||
-        hipMemset(j->d_wqueue, 0, sizeof(unsigned) * kWqShards * cands) != hipSuccess)  // fused queue: 0 = empty
-        return sspp::set_error(SSPP_E_NOMEM, "hipMalloc work-queue buffers");
-    j->wq_cap = cands;
-    return SSPP_OK;
+// k_sspp_c2f launch shape (NT threads, G1 phase-1 lanes per candidate, 64 / G1 candidates per
+// wave), measured on MI355X: launches of many candidates are throughput-bound ->
+// one-wave workgroups of 16 candidates x 4 lanes; a launch of a few thousand (one plan() batch)
+// is latency-bound -> 4-wave workgroups of 4 candidates x 64 lanes: a whole wave per candidate in
+// phase 1, a survivor's remaining waypoints over 256 lanes in phase 2.  Forced shapes
+// (sspp_job_set_option) are for tests and tuning.
+static void c2f_shape(const sspp_job* j, int64_t cands, int* nt, int* g1) {
+    const bool lat = cands < 16384;
+    *nt = j->opt_nt ? j->opt_nt : (lat ? 256 : 64);
+    *g1 = j->opt_g1 ? j->opt_g1 : (lat ? 64 : kThroughputG1);
 }
 
-// candidates per tile (k_sspp_wq1 workgroup): the largest of 16 / 4 / 1 that still gives every
-// resident wave a tile (SSPP_WQ_CPW overrides); pair groups per survivor item: 2 when the launch
-// has no more tiles than resident waves (latency-bound), else 1 (SSPP_WQ_NPG overrides)
-static int run_wq(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B, int steps, int64_t step_stride,
-                  const SsppPtrs& o, hipStream_t st) {
-    int rc = wq_reserve(j, (int64_t)steps * B);
-    if (rc) return rc;
-    const int ndof = j->n * j->D, NB = 3 * std::max(1, j->nm);
-    const int64_t total = (int64_t)steps * B;
-    const int occ = 4096;  // resident one-wave workgroups at 4 waves per SIMD
-    static const int env_cpw = [] { const char* e = getenv("SSPP_WQ_CPW"); return e ? atoi(e) : 0; }();
-    static const int env_npg = [] { const char* e = getenv("SSPP_WQ_NPG"); return e ? atoi(e) : 0; }();
-    static const int env_n1 = [] { const char* e = getenv("SSPP_WQ_N1"); return e ? atoi(e) : 0; }();
-    int cpw = env_cpw == 1 || env_cpw == 2 || env_cpw == 4 || env_cpw == 8 || env_cpw == 16 ? env_cpw : 0;
-    if (!cpw) cpw = total / 16 >= occ ? 16 : (total / 4 >= occ ? 4 : 1);
-    while (cpw > 1 && (size_t)cpw * ndof * sizeof(double) > 16384) cpw /= 2;
-    SsppWQ k{};
-    k.sc = kscene_job(j, d_ctrl == nullptr);
-    k.has_scene = j->scene != nullptr && (k.sc.npairs > 0 || k.sc.static_block);
-    static const int ablate = [] { const char* e = getenv("SSPP_ABLATE"); return e ? atoi(e) : 0; }();
-    k.ablate = ablate;
-    k.sampler = j->sampler;
-    k.p = j->p; k.n = j->n; k.W = j->W; k.npert = j->npert;
-    k.sigma = j->sigma; k.seed = j->seed;
-    k.first_id = first_id; k.B = B; k.step_stride = step_stride;
-    k.steps = steps;
-    k.cap = j->wq_cap;
-    k.cpw = cpw; k.g1 = 64 / cpw;
-    k.npts = j->W + 1;
-    k.n1 = std::min(env_n1 > 0 ? std::min(env_n1, k.g1) : k.g1, k.npts);
-    k.lpc = lanes_for(j->W - 1);
-    k.nchunk = k.npts > k.n1 ? (k.npts - k.n1 + 63) / 64 : 1;
-    k.npg = env_npg > 0 ? std::min(env_npg, 8) : ((total + cpw - 1) / cpw <= occ ? 2 : 1);
-    if (k.sc.npairs > 64) k.npg = 1;
-    k.arc_all = j->arc_all;
-    k.hull = j->hull;
-    k.tps = (unsigned)((B + cpw - 1) / cpw);
-    k.ntiles = k.tps * (unsigned)steps;
-    k.nps = (unsigned)(k.nchunk * k.npg);
-    k.ctr = j->d_wctr; k.stp = j->d_wstp; k.surv = j->d_wsurv; k.spert = j->d_wspert; k.queue = j->d_wqueue;
-    k.list = j->d_wlist;
-    const size_t lds = sizeof(double) * ((size_t)cpw * ndof + 2 * NB);
-    hipError_t e = hipErrorInvalidValue;
-    switch (j->D) {
-#ifndef SSPP_DEV_ONLY
-        case 1: e = entry_wq<1>(k, j, o, lds, st); break;
-        case 2: e = entry_wq<2>(k, j, o, lds, st); break;
-        case 3: e = entry_wq<3>(k, j, o, lds, st); break;
-        case 4: e = entry_wq<4>(k, j, o, lds, st); break;
-        case 6: e = entry_wq<6>(k, j, o, lds, st); break;
-        case 9: e = entry_wq<9>(k, j, o, lds, st); break;
-#endif
-        case 7: e = entry_wq<7>(k, j, o, lds, st); break;
-    }
-    if (e != hipSuccess) return hip_fail(e, "k_sspp_wq launch");
-    (void)d_ctrl;
-    return SSPP_OK;
+static size_t c2f_lds(const sspp_job* j, int cpb, int nrd) {
+    const int nm = j->nm < 1 ? 1 : j->nm;
+    const int rbox = std::max(6 * nm, lanes_for(j->W - 1) / 64 + 1);
+    return sizeof(double) * ((size_t)j->n * j->D + (size_t)cpb * (nrd + rbox) + j->D) +
+           sizeof(unsigned long long) * cpb + sizeof(int) * (3 * cpb + 1);
 }
 
 static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B, double* d_arc,
@@ -859,38 +744,23 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     if (!j || j->kind != 0) return sspp::set_error(SSPP_E_INVAL, "not a SamplingPathPlanner job");
     if (B < 1 || B > j->max_batch) return sspp::set_error(SSPP_E_INVAL, "batch size out of range");
     if (!d_arc || !d_feasible) return sspp::set_error(SSPP_E_INVAL, "null output");
-    SsppK k{};
-    k.sc = kscene(j->scene, false);
-    k.has_scene = j->scene != nullptr;
-    k.p = j->p; k.n = j->n; k.W = j->W;
-    k.sigma = j->sigma; k.seed = j->seed;
-    k.first_id = first_id; k.B = B;
-    k.lpc = j->lpc; k.cpb = j->cpb; k.shared_endpoints = (d_ctrl == nullptr) ? j->shared_endpoints : 0;
-    static const int ablate = [] { const char* e = getenv("SSPP_ABLATE"); return e ? atoi(e) : 0; }();
-    k.ablate = ablate;
-    k.insample = j->insample;
-    k.sampler = j->sampler;
-    k.arc_all = j->arc_all;
-    SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
-    if (steps < 1 || steps > kMaxSteps || (steps > 1 && (!j->c2f || d_ctrl || (j->npert > 0 && !j->insample && steps > j->pert_steps))))
-        return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..64 (coarse-to-fine kernel, sampled candidates)");
+    if (steps < 1 || steps > kMaxSteps || (steps > 1 && d_ctrl))
+        return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..64 (sampled candidates)");
     hipStream_t st = (hipStream_t)stream;
-    if (j->wq && (d_ctrl || j->insample || j->npert == 0)) return run_wq(j, d_ctrl, first_id, B, steps, step_stride, o, st);
-    // k_sspp_c2f launch shape (NT threads, G1 phase-1 lanes per candidate, CPB = NT / G1
-    // candidates per workgroup), measured on MI355X: launches of many candidates
-    // are throughput-bound -> one-wave workgroups of 16 candidates x 4 lanes; a launch of a few
-    // thousand (one plan() batch) is latency-bound -> 4-wave workgroups of 4 candidates x 64
-    // lanes: a whole wave per candidate in phase 1, a survivor's remaining waypoints over 256
-    // lanes in phase 2 (single 4096 x 128 step: 45.7 -> 30.8 us)
-    int nt = j->nt2, g1 = j->g1;
-    if (j->c2f && !j->shape_forced) {
-        const bool lat = (int64_t)steps * B < 16384;
-        nt = lat ? 256 : 64;
-        g1 = lat ? 64 : 4;
+    int nt, g1;
+    c2f_shape(j, (int64_t)steps * B, &nt, &g1);
+    const int n = j->n, D = j->D, p = j->p;
+    const int r0 = d_ctrl ? 0 : std::min(p, n), r1 = d_ctrl ? n : std::max(r0, n - p);
+    const int nrd = (r1 - r0) * D;
+    int cpw = 64 / g1, cpb = (nt / 64) * cpw;
+    size_t lds = c2f_lds(j, cpb, nrd);
+    if (lds > 64 * 1024 && !j->opt_nt) {  // large splines: the latency shape's 4 candidates
+        nt = 256; g1 = 64; cpw = 1; cpb = 4;
+        lds = c2f_lds(j, cpb, nrd);
     }
-    const int cpb = j->c2f ? nt / g1 : j->cpb;
+    if (lds > 64 * 1024) return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS");
     const int nblk = (int)((B + cpb - 1) / cpb);
-    if (j->c2f && (int64_t)nblk * steps > j->part_cap) {  // one BlockBest per workgroup and step
+    if ((int64_t)nblk * steps > j->part_cap) {  // one BlockBest per workgroup and step
         (void)hipDeviceSynchronize();
         if (j->d_part) (void)hipFree(j->d_part);
         j->d_part = nullptr;
@@ -899,103 +769,36 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
             return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
         j->part_cap = (int64_t)nblk * steps;
     }
-    if (!d_ctrl && j->npert > 0 && !j->insample) {  // sampleWithNoise over the whole chip
-        const long long work = (long long)steps * B * (long long)(j->sampler ? (j->npert + 3) / 4 : (j->npert + 1) / 2);
-        hipLaunchKernelGGL(k_sample_sspp, dim3((unsigned)((work + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                           (unsigned long long)j->seed, (long long)first_id, (long long)step_stride,
-                           (long long)B, steps, j->D, j->p, j->npert, j->sigma, j->d_init, j->d_limits,
-                           j->d_pert, j->sampler);
-        hipError_t es = hipGetLastError();
-        if (es != hipSuccess) return hip_fail(es, "k_sample_sspp launch");
-    }
-    hipError_t e;
-    if (j->c2f) {
-        SsppC2F c{};
-        c.sc = kscene_job(j, d_ctrl == nullptr);
-        c.has_scene = j->scene != nullptr && (c.sc.npairs > 0 || c.sc.static_block);
-        c.ablate = k.ablate; c.insample = j->insample;
-        c.sampler = j->sampler;
-        c.p = j->p; c.n = j->n; c.W = j->W; c.sigma = j->sigma; c.seed = j->seed;
-        c.first_id = first_id; c.B = B;
-        c.g1 = g1; c.cpb = cpb; c.npts = j->W + 1; c.n1 = std::min(g1, j->W + 1);
-        c.nt = nt;
-        {
-            const int nm = j->nm < 1 ? 1 : j->nm;
-            const int rbox = std::max(6 * nm, lanes_for(j->W - 1) / 64 + 1);
-            c.lds = (int)(sizeof(double) * ((size_t)cpb * (j->n * j->D + rbox) + j->D) +
-                          sizeof(unsigned long long) * cpb + sizeof(int) * (3 * cpb + 1));
-        }
-        c.lpc = lanes_for(j->W - 1);
-        c.nblk_step = nblk;
-        c.step_stride = step_stride;
-        c.arc_all = j->arc_all;
-        c.hull = j->hull;
-        c.dfr = j->d_dfr;
-        c.ctrl_feas = j->ctrl_feas;
-        c.p1cap = j->p1cap;
-        // fused survivor queue: the throughput shape (one-wave workgroups) on sampled candidates
-        // whose pair table needs no later fixup (no cylinder-box deferral, <= 64 pairs)
-        if (j->fq && !j->wq && nt == 64 && !d_ctrl && j->insample && !j->arc_all && c.npts > c.n1 &&
-            c.has_scene && c.sc.npairs > 0 && c.sc.npairs <= 64 && !c.sc.cylbox && !c.sc.static_block &&
-            c.ablate == 0) {
-            // sized once for the largest launch this job can make (up to 2M candidates), so no
-            // later launch re-allocates (and synchronises) inside a timed loop
-            int rc = wq_reserve(j, std::max<int64_t>((int64_t)steps * B,
-                                                     std::min<int64_t>((int64_t)kMaxSteps * j->max_batch, 1 << 21)));
-            if (rc) return rc;
-            const int gs = j->fq_gs, gps = (nblk + gs - 1) / gs, gcap = gs * cpb;
-            const int64_t ngrp = std::max<int64_t>((int64_t)steps * gps,
-                                                   (int64_t)kMaxSteps * (((j->max_batch + cpb - 1) / cpb + gs - 1) / gs));
-            if (ngrp > j->fq_ngrp || ngrp * gcap > j->fq_nq) {
-                (void)hipDeviceSynchronize();  // earlier launches may still use the old buffers
-                if (j->d_fqgrp) (void)hipFree(j->d_fqgrp);
-                if (j->d_fqq) (void)hipFree(j->d_fqq);
-                j->d_fqgrp = nullptr; j->d_fqq = nullptr; j->fq_ngrp = 0; j->fq_nq = 0;
-                if (hipMalloc((void**)&j->d_fqgrp, sizeof(FqGroup) * ngrp) != hipSuccess ||
-                    hipMalloc((void**)&j->d_fqq, sizeof(unsigned) * ngrp * gcap) != hipSuccess ||
-                    hipMemset(j->d_fqgrp, 0, sizeof(FqGroup) * ngrp) != hipSuccess ||
-                    hipMemset(j->d_fqq, 0, sizeof(unsigned) * ngrp * gcap) != hipSuccess)
-                    return sspp::set_error(SSPP_E_NOMEM, "hipMalloc fused-queue buffers");
-                j->fq_ngrp = ngrp; j->fq_nq = ngrp * gcap;
-            }
-            c.fq = 1;
-            c.p1cap = 0;
-            c.fq_npg = std::min(j->fq_npg, c.sc.npairs);
-            c.fq_nchunk = (c.npts - c.n1 + 63) / 64;
-            c.fq_nps = (unsigned)(c.fq_nchunk * c.fq_npg);
-            c.fq_gs = gs; c.fq_gcap = gcap;
-            c.fq_grp = j->d_fqgrp; c.fq_queue = j->d_fqq;
-            c.fq_ctr = j->d_wctr; c.fq_stp = j->d_wstp; c.fq_surv = j->d_wsurv; c.fq_spert = j->d_wspert;
-            c.fq_list = j->d_wlist;
-        }
-        const int nb = nblk * steps;
-        e = hipErrorInvalidValue;
-        switch (j->D) {
+    SsppC2F c{};
+    c.sc = kscene_job(j, d_ctrl == nullptr);
+    c.has_scene = j->scene != nullptr && (c.sc.npairs > 0 || c.sc.static_block);
+    c.sampler = j->sampler;
+    c.p = p; c.n = n; c.W = j->W; c.sigma = j->sigma; c.seed = j->seed;
+    c.first_id = first_id; c.B = B;
+    c.g1 = g1; c.cpw = cpw; c.cpb = cpb; c.npts = j->W + 1; c.n1 = std::min(g1, j->W + 1);
+    c.lpc = lanes_for(j->W - 1);
+    c.nblk_step = nblk;
+    c.step_stride = step_stride;
+    c.arc_all = j->arc_all;
+    c.r0 = r0; c.r1 = r1;
+    c.nt = nt; c.lds = (int)lds;
+    c.ctrl_feas = j->ctrl_feas;
+    j->last_nt = nt; j->last_g1 = g1;
+    SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
+    const int nb = nblk * steps;
+    hipError_t e = hipErrorInvalidValue;
+    switch (j->D) {
 #ifndef SSPP_DEV_ONLY
-            case 1: e = entry_c2f<1>(c, j, o, nb, st); break;
-            case 2: e = entry_c2f<2>(c, j, o, nb, st); break;
-            case 3: e = entry_c2f<3>(c, j, o, nb, st); break;
-            case 4: e = entry_c2f<4>(c, j, o, nb, st); break;
-            case 6: e = entry_c2f<6>(c, j, o, nb, st); break;
-            case 9: e = entry_c2f<9>(c, j, o, nb, st); break;
+        case 1: e = entry_c2f<1>(c, j, o, nb, st); break;
+        case 2: e = entry_c2f<2>(c, j, o, nb, st); break;
+        case 3: e = entry_c2f<3>(c, j, o, nb, st); break;
+        case 4: e = entry_c2f<4>(c, j, o, nb, st); break;
+        case 6: e = entry_c2f<6>(c, j, o, nb, st); break;
+        case 9: e = entry_c2f<9>(c, j, o, nb, st); break;
 #endif
-            case 7: e = entry_c2f<7>(c, j, o, nb, st); break;
-        }
-    } else {
-        e = hipErrorInvalidValue;
-        switch (j->D) {
-#ifndef SSPP_DEV_ONLY
-            case 1: e = entry_sspp<1>(k, j, o, nblk, st); break;
-            case 2: e = entry_sspp<2>(k, j, o, nblk, st); break;
-            case 3: e = entry_sspp<3>(k, j, o, nblk, st); break;
-            case 4: e = entry_sspp<4>(k, j, o, nblk, st); break;
-            case 6: e = entry_sspp<6>(k, j, o, nblk, st); break;
-            case 9: e = entry_sspp<9>(k, j, o, nblk, st); break;
-#endif
-            case 7: e = entry_sspp<7>(k, j, o, nblk, st); break;
-        }
+        case 7: e = entry_c2f<7>(c, j, o, nb, st); break;
     }
-    if (e != hipSuccess) return hip_fail(e, "k_sspp launch");
+    if (e != hipSuccess) return hip_fail(e, "k_sspp_c2f launch");
     return SSPP_OK;
 }
 
@@ -1006,8 +809,10 @@ extern "C" int sspp_job_sample_score(sspp_job* j, int64_t first_id, int64_t B, d
 
 // Re-target a SamplingPathPlanner job to another plan() call with the same knots, dof and
 // check_points (the drop-in planner caches one job per shape): the initial control points,
-// sigma, limits and seed change; the per-job pair order is recomputed for the new mean path.
-// Uploads are asynchronous on `stream` from job-owned host copies (valid until the next update).
+// sigma, limits and seed change; the pair tables are re-ordered for the new mean path (gap
+// order: a re-plan stays on the microsecond host path, so the hit-order pre-pass of job
+// creation is not repeated, and the waypoint order stays the creation's).  Uploads are
+// asynchronous on `stream` from job-owned host copies (valid until the next update).
 extern "C" int sspp_job_update_sspp(sspp_job* j, const double* init_ctrl, double sigma,
                                     const double* limits, uint64_t seed, void* stream) {
     sspp::clear_error();
@@ -1021,7 +826,7 @@ extern "C" int sspp_job_update_sspp(sspp_job* j, const double* init_ctrl, double
         std::memcmp(j->h_stage.data(), init_ctrl, sizeof(double) * nd) == 0 &&
         std::memcmp(j->h_stage.data() + nd, limits, sizeof(double) * j->D) == 0)
         return SSPP_OK;
-    const bool pairs = j->d_pairs && j->scene && !j->h_knots.empty();
+    const bool pairs = j->d_pairs && j->scene;
     const size_t vbytes = sizeof(double) * (nd + j->D);
     const size_t need = vbytes + (pairs ? 2 * sizeof(DPair) * j->scene->pairs.size() : 0);
     // the pinned staging is the source of the previous update's copies until they complete
@@ -1045,7 +850,7 @@ extern "C" int sspp_job_update_sspp(sspp_job* j, const double* init_ctrl, double
     HIPCHK(hipMemcpyAsync(j->d_init, pv, sizeof(double) * nd, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(j->d_limits, pv + nd, sizeof(double) * j->D, hipMemcpyHostToDevice, st));
     if (pairs) {
-        const int rc = set_job_pairs(j, init_ctrl, sigma, limits, false, stream, vbytes);
+        const int rc = set_job_tables(j, init_ctrl, sigma, limits, j->pair_order == 0 ? 0 : 1, false, stream, vbytes);
         if (rc) return rc;
     }
     HIPCHK(hipEventRecord(j->upd_ev, st));
@@ -1057,6 +862,58 @@ extern "C" int sspp_job_score_ctrl(sspp_job* j, const double* d_ctrl, int64_t fi
                         double* d_arc, uint8_t* d_feasible, sspp_best* d_best, void* stream) {
     if (!d_ctrl) return sspp::set_error(SSPP_E_INVAL, "null control points");
     return run_sspp(j, d_ctrl, first_id, B, d_arc, d_feasible, nullptr, d_best, stream);
+}
+
+// Explicit launch options of a job (tests and tuning; nothing is read from the environment).
+extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
+    sspp::clear_error();
+    if (!j) return sspp::set_error(SSPP_E_INVAL, "null job");
+    switch (key) {
+        case SSPP_OPT_SHAPE_NT:
+            if (j->kind != 0 || !(value == 0 || value == 64 || value == 256))
+                return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SHAPE_NT: 0, 64 or 256");
+            j->opt_nt = (int)value;
+            return SSPP_OK;
+        case SSPP_OPT_SHAPE_G1:
+            if (j->kind != 0 || value < 0 || value > 64)
+                return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SHAPE_G1: 0 (per launch) or 1..64");
+            j->opt_g1 = (int)value;
+            return SSPP_OK;
+        case SSPP_OPT_ORDER: {
+            if (j->kind != 0 || value < 0 || value > 2) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_ORDER: 0, 1 or 2");
+            HIPCHK(hipDeviceSynchronize());  // earlier launches may still read the tables
+            const size_t nd = (size_t)j->n * j->D;
+            return set_job_tables(j, j->h_stage.data(), j->sigma, j->h_stage.data() + nd, (int)value, true, nullptr);
+        }
+        case SSPP_OPT_TSP_FORM:
+            if (j->kind != 1 || value < -1 || value > 2) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_FORM: -1..2");
+            j->tsp_form = (int)value;
+            return SSPP_OK;
+        case SSPP_OPT_TSP_GENERIC:
+            if (j->kind != 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_GENERIC: TaskSpacePlanner jobs only");
+            j->tsp_generic = value ? 1 : 0;
+            return SSPP_OK;
+    }
+    return sspp::set_error(SSPP_E_INVAL, "unknown or read-only option");
+}
+
+extern "C" int sspp_job_get_option(const sspp_job* j, int key, int64_t* value) {
+    if (!j || !value) return sspp::set_error(SSPP_E_INVAL, "null argument");
+    switch (key) {
+        case SSPP_OPT_SHAPE_NT: *value = j->opt_nt; return SSPP_OK;
+        case SSPP_OPT_SHAPE_G1: *value = j->opt_g1; return SSPP_OK;
+        case SSPP_OPT_ORDER: *value = j->pair_order; return SSPP_OK;
+        case SSPP_OPT_TSP_FORM: *value = j->kind == 1 ? j->last_form : -1; return SSPP_OK;
+        case SSPP_OPT_TSP_GENERIC: *value = j->tsp_generic; return SSPP_OK;
+        case SSPP_OPT_SAMPLER: *value = j->sampler; return SSPP_OK;
+        case SSPP_OPT_LAST_NT: *value = j->last_nt; return SSPP_OK;
+        case SSPP_OPT_LAST_G1: *value = j->last_g1; return SSPP_OK;
+        case SSPP_OPT_WP_ORDER: *value = j->wp_order; return SSPP_OK;
+        case SSPP_OPT_PREPASS_US: *value = (int64_t)(j->prepass_ms * 1e3); return SSPP_OK;
+        case SSPP_OPT_NPAIRS: *value = j->np_samp; return SSPP_OK;
+        case SSPP_OPT_CYLBOX: *value = j->cb_samp; return SSPP_OK;
+    }
+    return sspp::set_error(SSPP_E_INVAL, "unknown option");
 }
 
 extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args* a, int64_t max_batch,
@@ -1124,7 +981,7 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     if (!d_L || !d_Cnf || !d_Cwf || !d_status || !d_cost)
         return sspp::set_error(SSPP_E_INVAL, "null output");
     TspK k{};
-    k.sc = kscene(j->scene, true);
+    k.sc = kscene(j->scene, true, j->tsp_generic != 0);
     k.n = j->n; k.K = j->K; k.cp = j->cp;
     for (int i = 0; i < 4; ++i) { k.start[i] = j->start[i]; k.end[i] = j->end[i]; k.lo[i] = j->lo[i]; k.hi[i] = j->hi[i]; }
     k.z_min = j->z_min; k.seed = j->seed; k.first_id = first_id; k.B = B;
@@ -1143,14 +1000,14 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     // small batches (the anytime CES loop) take the pair-split kernel: one workgroup per
     // candidate, the scene's pairs spread over 8 waves (same outputs, bit for bit)
     // and, with more than 8 pairs, ceil(npairs / 8) workgroups per candidate (k_tsp_pp2).
-    // SSPP_TSP_PP: 0 never, 1 single-workgroup form only, 2 the multi-workgroup form when it applies
-    const char* pp_s = getenv("SSPP_TSP_PP");
-    const int pp_env = pp_s ? atoi(pp_s) : -1;
+    // The form is an explicit job option (SSPP_OPT_TSP_FORM: 0 k_tsp, 1 the single-workgroup
+    // split, 2 the multi-workgroup split where it applies; -1 = by batch size)
+    const int pp_opt = j->tsp_form;
     const bool pp_ok = j->cp <= 64 && k.sc.npairs <= 64 && B <= j->part_cap;
-    const bool pp = pp_ok && (pp_env < 0 ? B <= kTspPpMaxBatch : pp_env > 0);
+    const bool pp = pp_ok && (pp_opt < 0 ? B <= kTspPpMaxBatch : pp_opt > 0);
     const int npg = (k.sc.npairs + 7) / 8;
     int mode = pp ? 1 : 0;
-    if (pp && npg > 1 && pp_env != 1 && B <= kTspPpMaxBatch) {
+    if (pp && npg > 1 && pp_opt != 1 && B <= kTspPpMaxBatch) {
         if (!j->d_pp_arrive) {
             const int64_t cap = std::min<int64_t>(j->max_batch, kTspPpMaxBatch);
             if (hipMalloc((void**)&j->d_pp_nd, sizeof(unsigned) * 4096 * (size_t)cap) != hipSuccess ||
@@ -1166,6 +1023,7 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
         }
     }
     const int nblk = mode == 2 ? (int)B * npg : mode == 1 ? (int)B : (int)((B + j->cpb - 1) / j->cpb);
+    j->last_form = mode;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e0 = entry_tsp<0>(k, j, nblk, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, d_status,
                                  d_best, st, mode);
@@ -1203,10 +1061,19 @@ extern "C" int sspp_job_tsp_score_vias(sspp_job* j, const double* d_vias, int64_
                    nullptr, d_best, stream);
 }
 
-extern "C" int sspp_job_info(const sspp_job* j, int* lpc, int* cpb, int* threads, size_t* lds) {
+extern "C" int sspp_job_info(const sspp_job* j, int* lpc, int* cpb_out, int* threads, size_t* lds) {
     if (!j) return sspp::set_error(SSPP_E_INVAL, "null job");
+    if (j->kind == 0) {  // the last k_sspp_c2f launch's shape (before any launch: the throughput shape)
+        const int nt = j->last_nt ? j->last_nt : 64, g1 = j->last_g1 ? j->last_g1 : kThroughputG1;
+        const int cpb = (nt / 64) * (64 / g1);
+        if (lpc) *lpc = g1;
+        if (cpb_out) *cpb_out = cpb;
+        if (threads) *threads = nt;
+        if (lds) *lds = c2f_lds(j, cpb, std::max(0, j->n - 2 * j->p) * j->D);
+        return SSPP_OK;
+    }
     if (lpc) *lpc = j->lpc;
-    if (cpb) *cpb = j->cpb;
+    if (cpb_out) *cpb_out = j->cpb;
     if (threads) *threads = kBlock;
     if (lds) *lds = j->lds;
     return SSPP_OK;
@@ -1222,16 +1089,8 @@ extern "C" void sspp_job_free(sspp_job* j) {
     if (j->d_pairs_s) (void)hipFree(j->d_pairs_s);
     if (j->d_ospan) (void)hipFree(j->d_ospan);
     if (j->d_part) (void)hipFree(j->d_part);
-    if (j->d_pert) (void)hipFree(j->d_pert);
     if (j->d_sync) (void)hipFree(j->d_sync);
-    if (j->d_dfr) (void)hipFree(j->d_dfr);
-    if (j->d_wctr) (void)hipFree(j->d_wctr);
-    if (j->d_wstp) (void)hipFree(j->d_wstp);
-    if (j->d_wsurv) (void)hipFree(j->d_wsurv);
-    if (j->d_wspert) (void)hipFree(j->d_wspert);
-    if (j->d_wqueue) (void)hipFree(j->d_wqueue);
-    if (j->d_wlist) (void)hipFree(j->d_wlist);
-    for (void* q : {(void*)j->d_pp_nd, (void*)j->d_pp_term, (void*)j->d_pp_arrive, (void*)j->d_fqgrp, (void*)j->d_fqq})
+    for (void* q : {(void*)j->d_pp_nd, (void*)j->d_pp_term, (void*)j->d_pp_arrive})
         if (q) (void)hipFree(q);
     if (j->upd_ev) {
         (void)hipEventSynchronize(j->upd_ev);
@@ -1336,18 +1195,6 @@ extern "C" int sspp_debug_c2f_stats(unsigned long long* out, int reset) {
 #endif
 
 #ifdef SSPP_WG_TIMING
-extern "C" int sspp_debug_wq_times(unsigned long long* tiles, unsigned long long* items, int n) {
-    hipDeviceSynchronize();
-    hipMemcpyFromSymbol(tiles, HIP_SYMBOL(g_wq_t), sizeof(unsigned long long) * (size_t)n);
-    hipMemcpyFromSymbol(items, HIP_SYMBOL(g_wq_i), sizeof(unsigned long long) * (size_t)n);
-    return 0;
-}
-extern "C" int sspp_debug_wq_reset(void) {
-    static unsigned long long z[8 << 16];
-    hipMemcpyToSymbol(HIP_SYMBOL(g_wq_t), z, sizeof z);
-    hipMemcpyToSymbol(HIP_SYMBOL(g_wq_i), z, sizeof z);
-    return 0;
-}
 extern "C" int sspp_debug_wg_times(unsigned long long* out, int n) {
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_t), sizeof(unsigned long long) * (size_t)n);
@@ -1359,15 +1206,6 @@ extern "C" int sspp_debug_wg_phases(unsigned long long* out, int n) {  // 8 per 
     return 0;
 }
 #endif
-
-// k_sspp_wq's spin-timeout word of a job (0: every wait of the hand-off protocol was satisfied;
-// a bounded spin that gave up sets 1 (idle claim loop) or 2 (survivor record never published))
-extern "C" int sspp_debug_job_error(const sspp_job* j) {
-    if (!j || !j->d_wctr) return 0;
-    unsigned e = 0;
-    if (hipMemcpy(&e, &j->d_wctr->error, sizeof(e), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    return (int)e;
-}
 
 extern "C" int sspp_device_count(int* n) {
     int c = 0;

@@ -194,6 +194,15 @@ class _Job:
         return dict(lanes_per_candidate=a.value, candidates_per_block=b.value,
                     block_threads=c.value, lds_bytes=d.value)
 
+    def set_option(self, key, value):
+        """Explicit launch option (include/sspp_hip.h SSPP_OPT_*; tests and tuning)."""
+        check(lib().sspp_job_set_option(self._h, int(key), int(value)), "job set_option")
+
+    def get_option(self, key):
+        v = C.c_int64()
+        check(lib().sspp_job_get_option(self._h, int(key), C.byref(v)), "job get_option")
+        return int(v.value)
+
     def __del__(self):
         if getattr(self, "_h", None) and _lib._lib is not None:
             _lib._lib.sspp_job_free(self._h)
@@ -245,6 +254,22 @@ class SsppJob(_Job):
         B = ctrl.shape[0]
         check(lib().sspp_job_score_ctrl(self._h, _ptr(ctrl), int(first_id), int(B), _ptr(arc),
                                         _ptr(feasible), _ptr(best), _stream(stream)), "score_ctrl")
+
+    def set_shape(self, nt=0, g1=0):
+        """Force the k_sspp_c2f launch shape (threads per workgroup 64 / 256, phase-1 lanes per
+        candidate); 0, 0 = chosen per launch.  Every shape gives the same results."""
+        self.set_option(_lib.OPT_SHAPE_NT, nt)
+        self.set_option(_lib.OPT_SHAPE_G1, g1)
+
+    def config(self):
+        """The job's effective configuration, read back from the library."""
+        g = self.get_option
+        return dict(sampler="fp32" if g(_lib.OPT_SAMPLER) else "fp64",
+                    shape="%dx%d" % (g(_lib.OPT_LAST_NT), g(_lib.OPT_LAST_G1)),
+                    pair_order={0: "scene", 1: "gap", 2: "hit"}[g(_lib.OPT_ORDER)],
+                    waypoint_order={0: "bisection", 2: "hit"}[g(_lib.OPT_WP_ORDER)],
+                    prepass_ms=g(_lib.OPT_PREPASS_US) / 1e3, sampled_pairs=g(_lib.OPT_NPAIRS),
+                    cylinder_box=bool(g(_lib.OPT_CYLBOX)))
 
 
 class TspJob(_Job):
@@ -366,6 +391,10 @@ class CesPlanner:
         if getattr(self, "_h", None) and _lib._lib is not None:
             _lib._lib.sspp_ces_free(self._h)
             self._h = None
+
+    def set_option(self, key, value):
+        """Explicit option (SSPP_OPT_CES_FUSED); every setting gives bit-identical iterations."""
+        check(lib().sspp_ces_set_option(self._h, int(key), int(value)), "ces set_option")
 
     def begin(self, start, end, iterate, stream=None):
         self._se = (_f64(start, 4), _f64(end, 4))

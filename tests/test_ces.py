@@ -338,15 +338,14 @@ def test_config5_multigoal_full_size_each_iteration(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("unfused", [0, 1])
-def test_icra_anytime_size_each_iteration(cuda, monkeypatch, unfused):
+def test_icra_anytime_size_each_iteration(cuda, unfused):
     """The reference's ICRA anytime configuration (src/main_icra_benchmark.cpp:151-179: 15
     samples x 40 checks, 1 via, gripper on robocrane.xml, block_green -> block_orange): 20
     iterations, each against the oracle.  17 slots take the one-launch update (ranking inside
-    k_ces_update); SSPP_CES_UNFUSED=1 forces rank + scatter + update — both bit-identical."""
+    k_ces_update); the SSPP_OPT_CES_FUSED = 0 option forces rank + scatter + update — both
+    bit-identical."""
     import bench
     import sspp_amd as S
-    if unfused:
-        monkeypatch.setenv("SSPP_CES_UNFUSED", "1")
     cfg = bench.ICRA
     model = S.Model(ROBOCRANE)
     body = model.body_id(bench.ICRA_BODY)
@@ -360,6 +359,8 @@ def test_icra_anytime_size_each_iteration(cuda, monkeypatch, unfused):
                               "init_points", "collision_weight", "z_min", "sigma_floor", "var_ema_beta",
                               "mean_lr")}
     pl = S.CesPlanner(scene, limits_min=lo, limits_max=hi, **kw)
+    if unfused:
+        pl.set_option(S.OPT_CES_FUSED, 0)
     ocfg = dict(frac=cfg["elite_fraction"], inc=cfg["stddev_increase_factor"],
                 dec=cfg["stddev_decay_factor"], sigma_floor=cfg["sigma_floor"], var_beta=cfg["var_ema_beta"],
                 mean_lr=cfg["mean_lr"], sd_min=cfg["stddev_min"], sd_max=cfg["stddev_max"],

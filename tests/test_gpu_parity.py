@@ -2,8 +2,9 @@
 
 Bars (BASELINE.json north_star): per-candidate costs within 1e-5 of the oracle — the kernels
 follow the oracle's operation order, so the tests hold them to 1e-12 (SamplingPathPlanner)
-and 1e-9 (TaskSpacePlanner, whose control points come from a precomputed collocation inverse
-instead of a per-candidate QR solve); feasibility flags and the selected index bit-identical.
+and 1e-9 (TaskSpacePlanner: control points from the same Householder QR replay as the oracle;
+costs summed in the canonical lane order); feasibility flags and the selected index
+bit-identical.
 """
 import os
 
@@ -55,40 +56,27 @@ def run_sspp(job, B, first=0, with_ctrl=True):
     return res
 
 
-# scoring kernels: ("2", candidates per tile, pair groups per item) — the work-queue k_sspp_wq
-# (default); ("1", SSPP_G1, SSPP_NT) — coarse-to-fine k_sspp_c2f with several phase-1 lane-group
-# sizes; ("0", ...) — the one-waypoint-per-lane k_sspp
-KERNELS = [("2", "16", "1"), ("2", "4", "2"), ("2", "1", "3"), ("2", "16", "4"),
-           ("1", "4", "64"), ("1", "8", "64"), ("1", "16", "256"), ("1", "64", "64"),
-           ("1", "16", "128"), ("0", "16", "256")]
+# k_sspp_c2f launch shapes (threads per workgroup, phase-1 lanes per candidate), forced through
+# the job option SSPP_OPT_SHAPE_NT / _G1; (0, 0) = the shape the library picks per launch
+# (256 x 64 below 16384 candidates per launch, 64 x 4 above).  Every shape must give the
+# oracle's results.
+SHAPES = [(0, 0), (64, 4), (64, 3), (64, 8), (64, 16), (64, 64), (256, 64), (256, 16)]
 
 
-def set_kernel(monkeypatch, kernel, a, b):
-    monkeypatch.setenv("SSPP_KERNEL", kernel)
-    if kernel == "2":
-        monkeypatch.setenv("SSPP_WQ_CPW", a)
-        monkeypatch.setenv("SSPP_WQ_NPG", b)
-    else:
-        monkeypatch.setenv("SSPP_G1", a)
-        monkeypatch.setenv("SSPP_NT", b)
-
-
-def wq_error(job):
-    """k_sspp_wq's spin-timeout word (0: every wait of the hand-off protocol was satisfied)."""
-    import sspp_amd._lib as L
-    return int(L.lib().sspp_debug_job_error(job._h))
+def set_shape(job, nt, g1):
+    job.set_shape(nt, g1)
 
 
 @pytest.mark.parametrize("arc_all", [False, True])
-@pytest.mark.parametrize("kernel,g1,nt", KERNELS)
+@pytest.mark.parametrize("nt,g1", SHAPES)
 @pytest.mark.parametrize("B,W", [(4096, 128), (257, 128), (1, 128), (300, 50), (100, 256), (64, 2)])
-def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g1, nt, B, W, arc_all):
+def test_robocrane_sample_score_matches_oracle(robocrane, nt, g1, B, W, arc_all):
     import sspp_amd as S
-    set_kernel(monkeypatch, kernel, g1, nt)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=0x5EED, max_batch=B,
                     arc_all=arc_all)
+    set_shape(job, nt, g1)
     r = run_sspp(job, B, first=1000)
     # sampling parity (Philox + FP64 Box-Muller restated on the host): bit-identical
     ctrl_o = O.sample_sspp(ctrl0, 3, 0.08, np.ones(7), 0x5EED, 1000, B)
@@ -104,7 +92,6 @@ def test_robocrane_sample_score_matches_oracle(robocrane, monkeypatch, kernel, g
     assert idx == (idx_o + 1000 if idx_o >= 0 else -1)
     if idx_o >= 0:
         assert abs(cost - best_o) <= COST_TOL
-    assert wq_error(job) == 0
 
 
 def test_robocrane_config2_is_nontrivial(robocrane):
@@ -118,18 +105,18 @@ def test_robocrane_config2_is_nontrivial(robocrane):
     assert 0 < nfeas < 4096, nfeas  # SURVEY config 2 (sigma 0.08): ~0.3% clear the brick stack
 
 
-@pytest.mark.parametrize("kernel,g1,nt", KERNELS)
-def test_score_ctrl_mode_matches_oracle(robocrane, monkeypatch, kernel, g1, nt):
+@pytest.mark.parametrize("nt,g1", SHAPES)
+def test_score_ctrl_mode_matches_oracle(robocrane, nt, g1):
     """Caller-supplied splines (checkCollision + computeArcLength on arbitrary ctrl)."""
     import sspp_amd as S
     import torch
-    set_kernel(monkeypatch, kernel, g1, nt)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     rng = np.random.default_rng(7)
     B = 777
     ctrl = ctrl0[None] + rng.normal(0, 0.05, size=(B, 10, 7))  # endpoints perturbed too
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=B)
+    set_shape(job, nt, g1)
     out = job.alloc(B)
     job.score_ctrl(torch.from_numpy(ctrl).cuda(), 0, out["arc"], out["feasible"], out["best"])
     torch.cuda.synchronize()
@@ -177,6 +164,53 @@ def test_robot_path_d9_p2_golden(cuda, golden):
     assert _np(out["feasible"]).all()
 
 
+def test_reference_robot_path_fixture_on_gpu(cuda):
+    """The reference's saved robot path (scripts/bspline_params.npy, main_bspline.py:198-209;
+    fixture tests/golden/robot_path.json): D = 9, degree 2.  The GPU's computeArcLength equals
+    the reference's BSplines.bspline chord sum to 1e-12 and the oracle's exactly, alone and
+    among other candidates of the same launch (ragged batch of 5)."""
+    import json
+    import sspp_amd as S
+    import torch
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "robot_path.json")))
+    knots, ctrl = np.array(d["knots"]), np.array(d["ctrl"])
+    job = S.SsppJob(None, knots, 2, ctrl, 0.0, np.ones(9), d["W"], max_batch=5)
+    cands = np.stack([ctrl, ctrl[::-1], ctrl * 0.5, ctrl + 0.1, ctrl])
+    out = job.alloc(5)
+    job.score_ctrl(torch.from_numpy(np.ascontiguousarray(cands)).cuda(), 0, out["arc"], out["feasible"],
+                   out["best"])
+    torch.cuda.synchronize()
+    arc = _np(out["arc"])
+    assert abs(arc[0] - d["arc_length"]) <= 1e-12 and arc[4] == arc[0]
+    arc_o, _ = O.sspp_score(None, knots, 2, cands, d["W"])
+    assert np.array_equal(arc, arc_o)
+    assert S.decode_best(out["best"])[1] == O.argmin(arc_o, np.ones(5, np.uint8))[0]
+
+
+def test_non_finite_arc_is_never_best(cuda):
+    """findBestPath (include/sspp.h:171-192) takes a path only when its cost is below the running
+    minimum from +inf: feasible candidates with an infinite or NaN arc length count as feasible
+    but are never selected — on the device argmin as in the oracle."""
+    import sspp_amd as S
+    import torch
+    knots, ctrl0 = linear_init(np.zeros(2), np.ones(2), 10)
+    B = 300
+    rng = np.random.default_rng(5)
+    ctrl = ctrl0[None] + rng.normal(0, 0.05, size=(B, 10, 2))
+    ctrl[0, 4, 0] = np.inf     # lowest ids: would win a tie-break if they were eligible
+    ctrl[1, 5, 1] = np.nan
+    ctrl[2:7] *= 1e300         # arc overflows to +inf
+    job = S.SsppJob(None, knots, 3, ctrl0, 0.0, np.ones(2), 50, max_batch=B)
+    out = job.alloc(B)
+    job.score_ctrl(torch.from_numpy(ctrl).cuda(), 0, out["arc"], out["feasible"], out["best"])
+    torch.cuda.synchronize()
+    arc = _np(out["arc"])
+    assert not np.isfinite(arc[:7]).any() and np.isfinite(arc[7:]).all()
+    idx_o, best_o = O.argmin(arc, np.ones(B, np.uint8))
+    cost, idx, cnt = S.decode_best(out["best"])
+    assert idx == idx_o >= 7 and cost == best_o and cnt == B
+
+
 def stacking_problem(B, cp=128, seed=0x5EED, K=1):
     import sspp_amd as S
     model = S.Model(STACKING)
@@ -216,11 +250,10 @@ def test_stacking_tsp_matches_oracle(cuda, B, cp, K):
         assert 0 < st.sum() < B  # both outcomes present
 
 
-@pytest.mark.parametrize("kernel,g1,nt", KERNELS)
-def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1, nt):
+@pytest.mark.parametrize("nt,g1", SHAPES)
+def test_planner_scene_sspp(cuda, nt, g1):
     """planner.xml: block1 (free) vs static wall/block2, 7-DoF window, path through the wall."""
     import sspp_amd as S
-    set_kernel(monkeypatch, kernel, g1, nt)
     model = S.Model(PLANNER)
     scene = S.Scene(model, 0, 7)
     oscene = O.Scene(mjcf_ref.load(PLANNER), 0, 7)
@@ -229,6 +262,7 @@ def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1, nt):
     knots, ctrl0 = linear_init(start, end, 10)
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.3, np.array([1, 1, 1, .2, .2, .2, .2]), 100,
                     seed=3, max_batch=2048)
+    set_shape(job, nt, g1)
     r = run_sspp(job, 2048)
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 100)
     np.testing.assert_array_equal(r["feasible"], feas_o)
@@ -236,25 +270,24 @@ def test_planner_scene_sspp(cuda, monkeypatch, kernel, g1, nt):
     assert r["best"][1] == O.argmin(arc_o, feas_o)[0]
 
 
-@pytest.mark.parametrize("kernel,g1,nt", KERNELS)
-def test_cylinder_box_sspp(robocrane, monkeypatch, kernel, g1, nt):
+@pytest.mark.parametrize("nt,g1", SHAPES)
+def test_cylinder_box_sspp(robocrane, nt, g1):
     """The block grazing the gripper's col_mount cylinder cap (and col_base box): the scan loops
-    leave cylinder-box pairs that pass the bounding-sphere test undecided, and the exact test
-    settles them — k_sspp_wq in the survivor's last item (out of line), k_sspp_c2f in the
-    k_sspp_cbfix launch queued after it (candidates written as feasible = 2 until then).
-    Feasibility, arcs and the argmin must equal the oracle's exact test."""
+    leave cylinder-box pairs that pass the bounding-sphere test undecided, and k_sspp_c2f's
+    settle step (the exact test, out of line, same launch) decides them for the candidates with
+    no other contact.  Feasibility, arcs and the argmin must equal the oracle's exact test."""
     import sspp_amd as S
-    set_kernel(monkeypatch, kernel, g1, nt)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(GRAZE_START, GRAZE_END, 10)
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.01, GRAZE_LIMITS, 128, seed=11, max_batch=2048)
+    assert job.config()["cylinder_box"]
+    set_shape(job, nt, g1)
     r = run_sspp(job, 2048)
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 128)
     np.testing.assert_array_equal(r["feasible"], feas_o)
     assert 0 < feas_o.sum() < 2048
     assert arc_err(r["arc"], arc_o) <= COST_TOL
     assert r["best"][1] == O.argmin(arc_o, feas_o)[0]
-    assert wq_error(job) == 0
     # the cylinder-box pair decides some candidates: without it they would be feasible
     oscene_nocyl = O.Scene(mjcf_ref.load(ROBOCRANE), 0, 7, skip_types=(5,))
     _, feas_nc = O.sspp_score(oscene_nocyl, knots, 3, r["ctrl"], 128)
@@ -266,18 +299,14 @@ GRAZE_END = np.array([2.2, 2.2, 0.656, 1, 0, 0, 0])
 GRAZE_LIMITS = np.array([1, 1, 1, .2, .2, .2, .2])
 
 
-@pytest.mark.parametrize("kernel,insample", [("2", "1"), ("1", "1"), ("1", "0")])
 @pytest.mark.parametrize("spl", [3, 16])
-def test_cylinder_box_multistep(robocrane, monkeypatch, kernel, insample, spl):
+def test_cylinder_box_multistep(robocrane, spl):
     """The grazing cylinder-box workload through the step executor (SsppSteps, G = 19 steps,
-    spl steps per launch, 2 streams): step > 0 indexing of the exact cylinder-box decisions
-    (k_sspp_wq items / k_sspp_c2f's k_sspp_cbfix merge into per-step records), both sampler
-    paths of k_sspp_c2f.  Every step's argmin record and its per-candidate feasibility equal the
-    oracle on that step's candidates, and some candidates turn on the cylinder-box pair."""
+    spl steps per launch, 2 streams): step > 0 indexing of the settle step's exact decisions.
+    Every step's argmin record and its per-candidate feasibility equal the oracle on that
+    step's candidates, and some candidates turn on the cylinder-box pair."""
     import sspp_amd as S
     import torch
-    monkeypatch.setenv("SSPP_KERNEL", kernel)
-    monkeypatch.setenv("SSPP_INSAMPLE", insample)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(GRAZE_START, GRAZE_END, 10)
     B, G, stride, first = 1024, 19, 3 * 1024, 7 * 1024
@@ -313,24 +342,19 @@ def test_cylinder_box_multistep(robocrane, monkeypatch, kernel, insample, spl):
         ctrl = O.sample_sspp(ctrl0, 3, 0.01, GRAZE_LIMITS, 11, first + i * stride, B)
         _, feas_o = O.sspp_score(oscene, knots, 3, ctrl, 128)
         np.testing.assert_array_equal(feas[0][k * B:(k + 1) * B].cpu().numpy(), feas_o)
-    for j in jobs:
-        assert wq_error(j) == 0
 
 
-@pytest.mark.parametrize("kernel", ["0", "1"])
-@pytest.mark.parametrize("insample", [0, 1])
-def test_fused_argmin_back_to_back(robocrane, monkeypatch, insample, kernel):
+@pytest.mark.parametrize("nt,g1", [(0, 0), (64, 4)])
+def test_fused_argmin_back_to_back(robocrane, nt, g1):
     """100 batches queued back to back: each launch's in-kernel argmin (sharded arrival
-    counters, re-armed by the last workgroup) must equal the argmin of that batch's outputs.
-    insample=1 draws the candidates inside the scoring kernel: same candidates, same results."""
+    counters, re-armed by the last workgroup) must equal the argmin of that batch's outputs."""
     import sspp_amd as S
     import torch
     _, scene, _ = robocrane
-    monkeypatch.setenv("SSPP_INSAMPLE", str(insample))
-    monkeypatch.setenv("SSPP_KERNEL", kernel)
     knots, ctrl0 = linear_init(START7, END7, 10)
     B, steps = 4096, 100
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.12, np.ones(7), 128, max_batch=B)
+    set_shape(job, nt, g1)
     arc = torch.empty((steps, B), dtype=torch.float64, device="cuda")
     feas = torch.empty((steps, B), dtype=torch.uint8, device="cuda")
     best = torch.empty((steps, 4), dtype=torch.int64, device="cuda")
@@ -373,25 +397,17 @@ def test_step_executor_matches_eager(robocrane, spl):
         jobs[0].sample_score(first + i * stride, B, ref["arc"], ref["feasible"], ref["best"])
         torch.cuda.synchronize()
         assert S.decode_best(got[i]) == S.decode_best(ref["best"]), i
-    for j in jobs:
-        assert wq_error(j) == 0
 
 
-@pytest.mark.parametrize("fq,npg,gs", [("0", "1", "16"), ("1", "1", "16"), ("1", "2", "16"), ("1", "4", "4"),
-                                       ("1", "1", "1"), ("1", "2", "256")])
 @pytest.mark.parametrize("sigma,spl", [(0.08, 20), (0.08, 32), (0.02, 16), (0.3, 20)])
-def test_fused_queue_matches_oracle(robocrane, monkeypatch, fq, npg, gs, sigma, spl):
-    """k_sspp_c2f's fused survivor queue (the executor's one-wave launches of many steps): every
-    step's per-candidate feasibility and arc length equal the oracle's on the same Philox
-    candidates, and every step's argmin record the oracle's argmin — with the queue off (the
-    in-workgroup phase 2), on with groups of 1 to 256 workgroups, and with survivor items split
-    into 2 / 4 pair groups.  sigma 0.02
-    leaves most candidates surviving phase 1, sigma 0.3 almost none."""
+def test_multistep_launch_matches_oracle(robocrane, sigma, spl):
+    """The executor's launches of many steps (the one-wave throughput shape, the bench's launch):
+    every step's per-candidate feasibility and arc length equal the oracle's on the same Philox
+    candidates, and every step's argmin record the oracle's argmin, over two launches back to
+    back (re-armed argmin counters).  sigma 0.02 leaves most candidates surviving phase 1,
+    sigma 0.3 almost none."""
     import sspp_amd as S
     import torch
-    monkeypatch.setenv("SSPP_FQ", fq)
-    monkeypatch.setenv("SSPP_FQ_NPG", npg)
-    monkeypatch.setenv("SSPP_FQ_GS", gs)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     B, G, stride, first = 4096, spl, 4096, 7 * 4096
@@ -400,9 +416,10 @@ def test_fused_queue_matches_oracle(robocrane, monkeypatch, fq, npg, gs, sigma, 
     feas = [torch.empty(spl * B, dtype=torch.uint8, device="cuda")]
     ex = S.SsppSteps([job], [torch.cuda.current_stream()], B, arcs, feas, steps_per_launch=spl)
     best = torch.zeros((G, 4), dtype=torch.int64, device="cuda")
-    for rep in range(2):  # the second launch reuses the re-armed queue and step counters
+    for rep in range(2):
         ex.enqueue(G, first + rep * G * stride, stride, best)
         torch.cuda.synchronize()
+        assert job.config()["shape"] == "64x4"
         arc, fe, got = arcs[0].cpu().numpy(), feas[0].cpu().numpy(), best.cpu()
         for i in (0, 7, G - 1):
             f0 = first + (rep * G + i) * stride
@@ -413,41 +430,62 @@ def test_fused_queue_matches_oracle(robocrane, monkeypatch, fq, npg, gs, sigma, 
             k, _ = O.argmin(arc_o, feas_o)
             d = S.decode_best(got[i])
             assert d[1] == (f0 + k if k >= 0 else -1) and d[2] == int(feas_o.sum()), (rep, i, d, k)
-    assert wq_error(job) == 0
 
 
-@pytest.mark.parametrize("cap", ["1", "2", "3"])
-@pytest.mark.parametrize("nt,g1", [("64", "4"), ("256", "64")])
-def test_phase1_cap_matches_oracle(robocrane, monkeypatch, cap, nt, g1):
-    """k_sspp_c2f with phase 1 capped at `cap` pair iterations (SSPP_P1CAP): the candidates it
-    leaves undecided go to phase 2 with every waypoint; feasibility, arcs and the argmin stay
-    the oracle's."""
+def test_default_shape_single_step_matches_oracle(robocrane):
+    """BASELINE configs[1] exactly as a plan() batch runs it: 4096 x 128, no forced shape (the
+    library picks the latency shape, 256 x 64), hit order from the creation pre-pass; every
+    candidate against the oracle."""
     import sspp_amd as S
-    monkeypatch.setenv("SSPP_P1CAP", cap)
-    monkeypatch.setenv("SSPP_NT", nt)
-    monkeypatch.setenv("SSPP_G1", g1)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
-    B = 4096
-    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=B)
-    r = run_sspp(job, B, first=99 * B)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=4096)
+    r = run_sspp(job, 4096, first=12345)
+    cfg = job.config()
+    assert cfg["shape"] == "256x64" and cfg["pair_order"] == "hit" and cfg["waypoint_order"] == "hit"
+    assert np.array_equal(r["ctrl"], O.sample_sspp(ctrl0, 3, 0.08, np.ones(7), 0x5EED, 12345, 4096))
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 128)
     np.testing.assert_array_equal(r["feasible"], feas_o)
     assert arc_err(r["arc"], arc_o) <= COST_TOL
     k, _ = O.argmin(arc_o, feas_o)
-    assert r["best"][1] == (99 * B + k if k >= 0 else -1)
+    assert r["best"][1] == (12345 + k if k >= 0 else -1) and r["best"][2] == int(feas_o.sum())
 
 
-@pytest.mark.parametrize("kernel", ["2", "1"])
-def test_fp32_sampler_opt_in(robocrane, monkeypatch, kernel):
+def test_environment_does_not_change_results(robocrane, monkeypatch):
+    """The library reads no environment variables: names that earlier builds read (sampler,
+    ablation, kernel and shape switches) leave a default job's results unchanged."""
+    import sspp_amd as S
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+
+    def run():
+        job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=2048)
+        return run_sspp(job, 2048, first=777), job.config()
+
+    base, cfg0 = run()
+    for k, v in dict(SSPP_SAMPLER="1", SSPP_ABLATE="64", SSPP_KERNEL="2", SSPP_G1="16", SSPP_NT="128",
+                     SSPP_PAIR_ORDER="0", SSPP_REACH="0", SSPP_HULL="0", SSPP_INSAMPLE="0").items():
+        monkeypatch.setenv(k, v)
+    again, cfg1 = run()
+    assert cfg0 == cfg1 and cfg0["sampler"] == "fp64"
+    for k in ("ctrl", "arc", "feasible"):
+        assert np.array_equal(base[k], again[k]), k
+    assert base["best"] == again["best"]
+    arc_o, feas_o = O.sspp_score(oscene, knots, 3, base["ctrl"], 128)
+    np.testing.assert_array_equal(base["feasible"], feas_o)
+
+
+@pytest.mark.parametrize("nt,g1", [(0, 0), (64, 4)])
+def test_fp32_sampler_opt_in(robocrane, nt, g1):
     """The opt-in FP32 Box-Muller quads (sampler = 1): candidates bit-identical to the oracle's
     or_normal_quad, scoring parity as with the FP64 default, and the two samplers differ."""
     import sspp_amd as S
-    monkeypatch.setenv("SSPP_KERNEL", kernel)
     _, scene, oscene = robocrane
     knots, ctrl0 = linear_init(START7, END7, 10)
     B = 1500
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=B, sampler=S.SAMPLER_FP32)
+    set_shape(job, nt, g1)
+    assert job.config()["sampler"] == "fp32"
     r = run_sspp(job, B, first=321)
     want = O.sample_sspp(ctrl0, 3, 0.08, np.ones(7), 0x5EED, 321, B, sampler=O.SAMPLER_FP32)
     assert np.array_equal(r["ctrl"], want)
@@ -518,15 +556,15 @@ def test_config4_full_size_shards(robocrane):
     assert arc_err(a[sub], arc_o) <= COST_TOL
 
 
-@pytest.mark.parametrize("hull", ["0", "1", "2"])
-def test_hull_modes_identical(robocrane, monkeypatch, hull):
-    """The candidate hull broadphase is exact: off / before phase 1 / survivors only give the
-    same per-candidate results, equal to the oracle."""
+@pytest.mark.parametrize("order", [0, 1, 2])
+def test_scan_orders_identical(robocrane, order):
+    """The pair / waypoint scan order (SSPP_OPT_ORDER: scene + bisection, mean-path gap, hit
+    order) steers only how soon a contact is found: per-candidate results equal the oracle."""
     import sspp_amd as S
     _, scene, oscene = robocrane
-    monkeypatch.setenv("SSPP_HULL", hull)
     knots, ctrl0 = linear_init(START7, END7, 10)
     job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=2048)
+    job.set_option(S.OPT_ORDER, order)
     r = run_sspp(job, 2048, first=4096)
     arc_o, feas_o = O.sspp_score(oscene, knots, 3, r["ctrl"], 128)
     np.testing.assert_array_equal(r["feasible"], feas_o)
@@ -569,7 +607,7 @@ def test_gripper_tsp_matches_oracle(cuda, goal):
 @pytest.mark.parametrize("xml,body,B,cp", [("robocrane.xml", "gripper_collision_with_block/", 17, 40),
                                            ("robocrane.xml", "gripper_collision_with_block/", 300, 64),
                                            ("stacking.xml", "block1", 200, 48)])
-def test_tsp_kernel_forms_identical(cuda, monkeypatch, xml, body, B, cp):
+def test_tsp_kernel_forms_identical(cuda, xml, body, B, cp):
     """k_tsp, the single-workgroup pair split (k_tsp_pp) and the multi-workgroup split (k_tsp_pp2,
     48 gripper pairs over 6 workgroups per candidate) give bit-identical per-candidate results and
     argmin records, and match the oracle."""
@@ -592,7 +630,7 @@ def test_tsp_kernel_forms_identical(cuda, monkeypatch, xml, body, B, cp):
                    z_min=0.0, max_batch=B)
     res = {}
     for mode in ("0", "1", "2"):
-        monkeypatch.setenv("SSPP_TSP_PP", mode)
+        job.set_option(S.OPT_TSP_FORM, int(mode))
         q = job.alloc(B, device="cuda", with_vias=True)
         job.sample_score(0, B, q["L"], q["Cnf"], q["Cwf"], q["status"], q["cost"], q["best"],
                          vias_out=q["vias"])

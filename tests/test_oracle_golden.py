@@ -3,6 +3,8 @@
 Golden vectors: tests/golden/bsplines_golden.npz, generated from the reference's
 sspp/BSplines.py and sspp/CubicPath.py by tests/golden/make_golden.py.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -192,3 +194,18 @@ def test_robot_path_d9_p2_golden(golden):
     assert np.abs(pts - golden["robot_pts"]).max() <= 1e-13
     arc, _ = O.sspp_score(None, knots, 2, ctrl[None], 128)
     assert abs(arc[0] - golden["robot_arc"][0]) <= 1e-12
+
+
+def test_reference_robot_path_fixture():
+    """The reference's saved robot path (scripts/bspline_params.npy, main_bspline.py:198-209;
+    tests/golden/make_robot_path.py): 7 joint angles + 2 passive joints, degree 2, knots
+    [0,0,0,.2,.4,.6,.8,1,1,1].  The oracle's spline evaluation equals the reference's
+    BSplines.bspline on 128 points and its computeArcLength the chord sum over them."""
+    import json
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "robot_path.json")))
+    knots, ctrl, k = np.array(d["knots"]), np.array(d["ctrl"]), d["k"]
+    assert ctrl.shape == (7, 9) and k == 2
+    pts = np.array([O.spline_eval(knots, k, ctrl, u) for u in d["u"]])
+    assert np.abs(pts - np.array(d["bspline"])).max() <= 1e-13
+    arc, feas = O.sspp_score(None, knots, k, ctrl[None], d["W"])
+    assert feas[0] == 1 and abs(arc[0] - d["arc_length"]) <= 1e-12
