@@ -513,7 +513,10 @@ SSPP_HD int bb_clip_count_up(const double* pa, const double* ma, const double* e
 // Returns the number of those with dist < -1e-3, at least 1 (no clipped point is deeper than the
 // SAT depth).  Every array is indexed with compile-time indices (run-time choices are selects),
 // so everything stays in registers.
-SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double* ea,
+// box_box_deep_class: the decision part — -1 not deep, 6 one contact (edge-edge axis), 0..5 the
+// reference face fi whose contact polygon bb_clip_count counts; box_box_deep_count composes the
+// two (k_tsp's deferred form runs the polygon later, for the compacted deep items only).
+SSPP_HD int box_box_deep_class(const double* pa, const double* ma, const double* ea,
                                const double* pb, const double* mb, const double* eb) {
     double A[3][3], Bc[3][3], T[3], t[3], R[3][3], AR[3][3];
 #pragma unroll
@@ -531,7 +534,7 @@ SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double*
     for (int i = 0; i < 3; ++i) {  // faces of A
         const double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
         const double sep = fabs(t[i]) - (ea[i] + rb);
-        if (sep >= kDeep) return 0;
+        if (sep >= kDeep) return -1;
         if (sep > best_face) { best_face = sep; fi = i; }
     }
 #pragma unroll
@@ -539,7 +542,7 @@ SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double*
         const double pr = fabs(fma(t[2], R[2][j], fma(t[1], R[1][j], t[0] * R[0][j])));
         const double ra = fma(ea[2], AR[2][j], fma(ea[1], AR[1][j], ea[0] * AR[0][j]));
         const double sep = pr - (ra + eb[j]);
-        if (sep >= kDeep) return 0;
+        if (sep >= kDeep) return -1;
         if (sep > best_face) { best_face = sep; fi = 3 + j; }
     }
     bool edge = false;  // some edge axis separates by more than best_face + 1e-12
@@ -564,15 +567,21 @@ SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double*
                 rb = fma(eb[k], fabs(dot3(bk, L)), rb);
             }
             const double num = pr - (ra + rb), len = sqrt(len2);
-            if (num >= kDeep * len) return 0;
+            if (num >= kDeep * len) return -1;
             edge = edge || num > fthr * len;
         }
     }
-    if (edge) return 1;
+    return edge ? 6 : fi;
+}
+SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double* ea,
+                               const double* pb, const double* mb, const double* eb) {
+    const int c = box_box_deep_class(pa, ma, ea, pb, mb, eb);
+    if (c < 0) return 0;
+    if (c == 6) return 1;
 #ifdef SSPP_NO_MANIFOLD  // measurement variant only: the SAT decision without the contact polygon
     return 1;
 #endif
-    return bb_clip_count(pa, ma, ea, pb, mb, eb, fi);
+    return bb_clip_count(pa, ma, ea, pb, mb, eb, c);
 }
 
 // box_box_deep_count for two UPRIGHT boxes: each rotation has m[2] = m[5] = m[6] = m[7] = 0
@@ -583,7 +592,7 @@ SSPP_HD int box_box_deep_count(const double* pa, const double* ma, const double*
 // is exact), so this returns bit for bit what box_box_deep_count returns on such boxes, with a
 // quarter of the SAT arithmetic: the 8 non-degenerate edge axes are z (4), A's and B's
 // horizontal axes (2 + 2); the ninth (A_z x B_z) has length 0 and is skipped there too.
-SSPP_HD int box_box_deep_count_up(const double* pa, const double* ma, const double* ea,
+SSPP_HD int box_box_deep_class_up(const double* pa, const double* ma, const double* ea,
                                   const double* pb, const double* mb, const double* eb) {
     const double T0 = pb[0] - pa[0], T1 = pb[1] - pa[1], T2 = pb[2] - pa[2];
     const double t0 = fma(ma[3], T1, ma[0] * T0), t1 = fma(ma[4], T1, ma[1] * T0), t2 = ma[8] * T2;
@@ -595,23 +604,23 @@ SSPP_HD int box_box_deep_count_up(const double* pa, const double* ma, const doub
     int fi;
     // faces of A
     sep = fabs(t0) - (ea[0] + fma(eb[1], A01, eb[0] * A00));
-    if (sep >= kDeep) return 0;
+    if (sep >= kDeep) return -1;
     best_face = sep; fi = 0;
     sep = fabs(t1) - (ea[1] + fma(eb[1], A11, eb[0] * A10));
-    if (sep >= kDeep) return 0;
+    if (sep >= kDeep) return -1;
     if (sep > best_face) { best_face = sep; fi = 1; }
     sep = fabs(t2) - (ea[2] + eb[2] * A22);
-    if (sep >= kDeep) return 0;
+    if (sep >= kDeep) return -1;
     if (sep > best_face) { best_face = sep; fi = 2; }
     // faces of B
     sep = fabs(fma(t1, R10, t0 * R00)) - (fma(ea[1], A10, ea[0] * A00) + eb[0]);
-    if (sep >= kDeep) return 0;
+    if (sep >= kDeep) return -1;
     if (sep > best_face) { best_face = sep; fi = 3; }
     sep = fabs(fma(t1, R11, t0 * R01)) - (fma(ea[1], A11, ea[0] * A01) + eb[1]);
-    if (sep >= kDeep) return 0;
+    if (sep >= kDeep) return -1;
     if (sep > best_face) { best_face = sep; fi = 4; }
     sep = fabs(t2 * R22) - (ea[2] * A22 + eb[2]);
-    if (sep >= kDeep) return 0;
+    if (sep >= kDeep) return -1;
     if (sep > best_face) { best_face = sep; fi = 5; }
     bool edge = false;
     const double fthr = best_face + 1e-12;
@@ -624,27 +633,33 @@ SSPP_HD int box_box_deep_count_up(const double* pa, const double* ma, const doub
         return 1;
     };
     // (i, j) = (0, 0), (0, 1): L = (0, -0, R1j), along z
-    if (!ax(R10 * R10, fabs(t2 * R10), ea[2] * fabs(R10), eb[2] * fabs(R22 * R10))) return 0;
-    if (!ax(R11 * R11, fabs(t2 * R11), ea[2] * fabs(R11), eb[2] * fabs(R22 * R11))) return 0;
+    if (!ax(R10 * R10, fabs(t2 * R10), ea[2] * fabs(R10), eb[2] * fabs(R22 * R10))) return -1;
+    if (!ax(R11 * R11, fabs(t2 * R11), ea[2] * fabs(R11), eb[2] * fabs(R22 * R11))) return -1;
     // (0, 2): L = (0, -R22, 0)
     if (!ax(R22 * R22, fabs(t1 * -R22), ea[1] * A22,
-            fma(eb[1], fabs(R11 * -R22), eb[0] * fabs(R10 * -R22)))) return 0;
+            fma(eb[1], fabs(R11 * -R22), eb[0] * fabs(R10 * -R22)))) return -1;
     // (1, 0), (1, 1): L = (0, 0, -R0j), along z
-    if (!ax(R00 * R00, fabs(t2 * -R00), ea[2] * A00, eb[2] * fabs(R22 * -R00))) return 0;
-    if (!ax(R01 * R01, fabs(t2 * -R01), ea[2] * A01, eb[2] * fabs(R22 * -R01))) return 0;
+    if (!ax(R00 * R00, fabs(t2 * -R00), ea[2] * A00, eb[2] * fabs(R22 * -R00))) return -1;
+    if (!ax(R01 * R01, fabs(t2 * -R01), ea[2] * A01, eb[2] * fabs(R22 * -R01))) return -1;
     // (1, 2): L = (R22, 0, -0)
     if (!ax(R22 * R22, fabs(t0 * R22), ea[0] * A22,
-            fma(eb[1], fabs(R01 * R22), eb[0] * fabs(R00 * R22)))) return 0;
+            fma(eb[1], fabs(R01 * R22), eb[0] * fabs(R00 * R22)))) return -1;
     // (2, 0), (2, 1): L = (-R1j, R0j, 0), horizontal; (2, 2) has L = 0
     if (!ax(fma(R00, R00, -R10 * -R10), fabs(fma(t1, R00, t0 * -R10)), fma(ea[1], A00, ea[0] * A10),
-            fma(eb[1], fabs(fma(R11, R00, R01 * -R10)), eb[0] * fabs(fma(R10, R00, R00 * -R10))))) return 0;
+            fma(eb[1], fabs(fma(R11, R00, R01 * -R10)), eb[0] * fabs(fma(R10, R00, R00 * -R10))))) return -1;
     if (!ax(fma(R01, R01, -R11 * -R11), fabs(fma(t1, R01, t0 * -R11)), fma(ea[1], A01, ea[0] * A11),
-            fma(eb[1], fabs(fma(R11, R01, R01 * -R11)), eb[0] * fabs(fma(R10, R01, R00 * -R11))))) return 0;
-    if (edge) return 1;
+            fma(eb[1], fabs(fma(R11, R01, R01 * -R11)), eb[0] * fabs(fma(R10, R01, R00 * -R11))))) return -1;
+    return edge ? 6 : fi;
+}
+SSPP_HD int box_box_deep_count_up(const double* pa, const double* ma, const double* ea,
+                                  const double* pb, const double* mb, const double* eb) {
+    const int c = box_box_deep_class_up(pa, ma, ea, pb, mb, eb);
+    if (c < 0) return 0;
+    if (c == 6) return 1;
 #ifdef SSPP_NO_MANIFOLD
     return 1;
 #endif
-    return bb_clip_count_up(pa, ma, ea, pb, mb, eb, fi);
+    return bb_clip_count_up(pa, ma, ea, pb, mb, eb, c);
 }
 
 // Both rotations upright (see box_box_deep_count_up)?

@@ -563,15 +563,27 @@ __device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const doub
 // over several lanes can be summed afterwards in pair order, bit-identical to the sum.  REC 1:
 // rec_nd is unsigned char (LDS, k_tsp_pp); REC 2: rec_nd is unsigned and both are written with
 // write-through agent-scope stores (another workgroup reads them, k_tsp_pp2).
+// REC 3 (DEEP, MODE 1, NM 1; k_tsp<..., DEF>): every pair k < npairs gets a record — rec_nd[k]
+// = its deep-contact count, or kBbPend + fi for a deep box-box pair whose contact polygon (face fi)
+// is counted later by the workgroup over its compacted deferred pairs (bb_clip_count(_up)) —
+// and rec_term[k] its cost term; rec_pose receives the mover pose (position, the five non-zero
+// entries of the yaw rotation) those later counts recompute the geom poses from.
+constexpr int kBbPend = 16;
 template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, int CB = 1, int REC = 0, bool UP = false>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                              unsigned long long mask, double* cost, int* stop = nullptr,
-                             void* rec_nd = nullptr, double* rec_term = nullptr) {
+                             void* rec_nd = nullptr, double* rec_term = nullptr, double* rec_pose = nullptr) {
+    static_assert(REC != 3 || (DEEP && MODE == 1 && NM == 1), "deferred box-box polygons: yaw-only single mover");
     static_assert(!ONEGEOM || NM == 1, "single moving geom implies a single mover");
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
     double mp[NM][3], mR[NM][9];
     mover_poses<D, NM, MODE>(q, (cmover_t)T.movers, mp, mR);
+    if (REC == 3) {
+        rec_pose[0] = mp[0][0]; rec_pose[1] = mp[0][1]; rec_pose[2] = mp[0][2];
+        rec_pose[3] = mR[0][0]; rec_pose[4] = mR[0][1]; rec_pose[5] = mR[0][3]; rec_pose[6] = mR[0][4];
+        rec_pose[7] = mR[0][8];
+    }
     double acc = 0.0;
     int cur = -1;
     double gp[3], gmat[9];
@@ -623,9 +635,21 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                 have_rot = true;
             }
             const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
-            if (gfirst) nc = collide<DEEP, CB, DEEP, false, UP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
-            else nc = collide<DEEP, CB, DEEP, false, UP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+            if (REC == 3 && G.type == 6 && pr.otype == 6) {
+                // box-box: the SAT decision now, the contact polygon later (collide's DEEP path
+                // runs box_box_deep_count(_up) unconditionally: margin >= 0 > kDeep)
+                const int c = gfirst ? (UP ? box_box_deep_class_up(gp, gmat, G.size, op, om, pr.osize)
+                                           : box_box_deep_class(gp, gmat, G.size, op, om, pr.osize))
+                                     : (UP ? box_box_deep_class_up(op, om, pr.osize, gp, gmat, G.size)
+                                           : box_box_deep_class(op, om, pr.osize, gp, gmat, G.size));
+                nd = c < 0 ? 0 : (c == 6 ? 1 : kBbPend + c);
+            } else if (gfirst) {
+                nc = collide<DEEP, CB, DEEP, false, UP>(G.type, gp, gmat, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd);
+            } else {
+                nc = collide<DEEP, CB, DEEP, false, UP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
+            }
         }
+        if (REC == 3) ((unsigned char*)rec_nd)[k] = (unsigned char)nd;
         if (!DEEP) {
             // the loop trip is wave-uniform, so every active lane reaches this vote
             if (__ballot(nc > 0) != 0ull) return 1;
@@ -637,6 +661,8 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             const double term = -1.0 / (cd + 1e-4);
             if (REC == 1) {
                 ((unsigned char*)rec_nd)[k] = (unsigned char)nd;
+                rec_term[k] = term;
+            } else if (REC == 3) {
                 rec_term[k] = term;
             } else if (REC == 2) {
                 __hip_atomic_store((unsigned*)rec_nd + k, (unsigned)nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1461,9 +1487,19 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
 #ifndef SSPP_TSP_WAVES_PER_EU_MG  // several moving geoms (their per-geom poses stay live)
 #define SSPP_TSP_WAVES_PER_EU_MG 2
 #endif
-template <int NM, bool ONEGEOM, int CB, bool UP = false>
-__global__ __launch_bounds__(kBlock, CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
-                                             : (ONEGEOM ? SSPP_TSP_WAVES_PER_EU : SSPP_TSP_WAVES_PER_EU_MG)) void k_tsp(
+// DEF (one waypoint per lane, at most kDefPairs pairs): box-box contact polygons deferred — the
+// waypoint loop records every pair's count / term (REC 3), the workgroup then counts the
+// polygons of its compacted deep box-box pairs (all lanes busy, instead of the lanes of each
+// wave that happen to hold one), and each lane sums its records in pair order: the same additions
+// in the same order as the inline form, so the costs are bit-identical.
+constexpr int kDefPairs = 8;
+#ifndef SSPP_TSP_WAVES_PER_EU_DEF
+#define SSPP_TSP_WAVES_PER_EU_DEF 4
+#endif
+template <int NM, bool ONEGEOM, int CB, bool UP = false, bool DEF = false>
+__global__ __launch_bounds__(kBlock, DEF ? SSPP_TSP_WAVES_PER_EU_DEF
+                                         : (CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
+                                                    : (ONEGEOM ? SSPP_TSP_WAVES_PER_EU : SSPP_TSP_WAVES_PER_EU_MG))) void k_tsp(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
     const double* __restrict__ sigma, const double* __restrict__ vias_in,
@@ -1481,6 +1517,13 @@ __global__ __launch_bounds__(kBlock, CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
     double* s_wsum = s_ctrl + cpb * ndof;    // [3][4]
     double* s_best = s_wsum + 3 * (kBlock / 64);
     int* s_stat = (int*)(s_best + 4);        // [cpb]
+    // DEF: per-lane records [kBlock][np] (terms, counts), mover poses [kBlock][8], deferred list
+    const int npr = DEF ? a.sc.npairs : 0;
+    double* s_rterm = (double*)(s_stat + ((cpb + 1) & ~1));
+    double* s_rpose = s_rterm + kBlock * npr;
+    unsigned char* s_rnd = (unsigned char*)(s_rpose + (DEF ? kBlock * 8 : 0));
+    int* s_items = (int*)(s_rnd + ((kBlock * npr + 3) & ~3));
+    int* s_nitems = s_items + kBlock * npr;
 
     const long long nvalid = min((long long)cpb, a.B - cand0);
     const long long nfx = a.ces ? (long long)*a.nfixed : 0;  // uniform: scalar load
@@ -1495,7 +1538,74 @@ __global__ __launch_bounds__(kBlock, CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
     // cp <= lpc: one waypoint per lane, so s((i-1)du) is the previous lane's s(i du); take it
     // by shuffle (bit-identical: same eval_pt inputs) except on a wave's first lane
     const bool one_pass = cp <= lpc;
-    if (valid) {
+    if (DEF) {  // host-checked: one waypoint per lane (cp <= lpc), np <= kDefPairs, NM == 1
+        if (tid == 0) *s_nitems = 0;
+        unsigned char* rn = s_rnd + tid * npr;
+        double* rt = s_rterm + tid * npr;
+        for (int k = 0; k < npr; ++k) rn[k] = 0;
+        const bool has = valid && lane < cp;
+        double pz = 0.0;
+        if (has) {
+            const int i = lane + 1;
+            double pv[4], pc[4];
+            eval_pt<D, P>(myc, tab + i * P1, span[i], pc);
+#pragma unroll
+            for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pc[d], 1, 64);
+            if ((tid & 63) == 0) eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
+            aL = aL + dist_nd<D>(pv, pc);
+            pz = pc[2];
+            point_collide<D, NM, 1, true, ONEGEOM, CB, 3, UP>(pc, a.sc, T, mask, nullptr, nullptr, rn, rt,
+                                                             s_rpose + tid * 8);
+        }
+        __syncthreads();
+        // compact the deferred (lane, pair) records: one wave ballot + one LDS add per wave
+        for (int e0 = 0; e0 < kBlock * npr; e0 += kBlock) {  // workgroup-uniform
+            const int e = e0 + tid;
+            const bool pend = e < kBlock * npr && s_rnd[e] >= kBbPend;
+            const unsigned long long m = __ballot(pend);
+            int base = 0;
+            if ((tid & 63) == 0 && m) base = atomicAdd(s_nitems, __popcll(m));
+            base = __shfl(base, 0, 64);
+            if (pend) s_items[base + __popcll(m & ((1ull << (tid & 63)) - 1ull))] = e;
+        }
+        __syncthreads();
+        const int nit = *s_nitems;
+        const cgeom_t geoms = (cgeom_t)T.geoms;
+        const cpair_t pairs = (cpair_t)T.pairs;
+        for (int it = tid; it < nit; it += kBlock) {
+            const int e = s_items[it], ln = e / npr, k = e - ln * npr;
+            const int fi = s_rnd[e] - kBbPend;
+            const double* ps = s_rpose + ln * 8;
+            const double mp0[3] = {ps[0], ps[1], ps[2]};
+            const double mR0[9] = {ps[3], ps[4], 0.0, ps[5], ps[6], 0.0, 0.0, 0.0, ps[7]};
+            const DPair pr = pairs[k];
+            const DGeom G = geoms[pr.gm];
+            double gp[3], gm[9];
+            geom_pos_t<true>(mp0, mR0, G, gp);
+            geom_rot_t<true>(mR0, G, gm);
+            const bool gfirst = G.orig < pr.oorig;  // both boxes
+            const int nd = gfirst ? (UP ? bb_clip_count_up(gp, gm, G.size, pr.opos, pr.omat, pr.osize, fi)
+                                        : bb_clip_count(gp, gm, G.size, pr.opos, pr.omat, pr.osize, fi))
+                                  : (UP ? bb_clip_count_up(pr.opos, pr.omat, pr.osize, gp, gm, G.size, fi)
+                                        : bb_clip_count(pr.opos, pr.omat, pr.osize, gp, gm, G.size, fi));
+            s_rnd[e] = (unsigned char)nd;
+        }
+        __syncthreads();
+        if (has) {  // this waypoint's cost: the records in pair order (point_collide's sum)
+            double acc = 0.0;
+            for (int k = 0; k < npr; ++k) {
+                const int nd = rn[k];
+                if (nd == 0) continue;
+                const double term = rt[k];
+                for (int r = 0; r < nd; ++r) acc = acc + term;
+            }
+            const double c = acc + a.sc.static_cost;
+            const double deficit = (a.floor_z_min + a.floor_margin) - pz;
+            const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
+            aC = aC + c;
+            aW = aW + (c + fp);
+        }
+    } else if (valid) {
         for (int j = lane; j < cp; j += lpc) {
             const int i = j + 1;
             double pv[4], pc[4];
@@ -1760,6 +1870,11 @@ __global__ __launch_bounds__(64 * G, 2) void k_tsp_pp2(
 
 // TaskSpacePlanner batches up to this size take k_tsp_pp (one workgroup per candidate)
 constexpr int64_t kTspPpMaxBatch = 512;
+// extra LDS of k_tsp<..., DEF>: records (terms, counts), poses, the deferred list and its count
+inline size_t tsp_def_lds(int np) {
+    return sizeof(double) * (size_t)kBlock * (np + 8) + (((size_t)kBlock * np + 3) & ~(size_t)3) +
+           sizeof(int) * ((size_t)kBlock * np + 1) + 16;
+}
 
 inline int lanes_for(int items) {
     int l = ((items + 63) / 64) * 64;
@@ -1969,7 +2084,7 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
 #undef SSPP_LAUNCH_TSPPP2
         return hipGetLastError();
     }
-    if (pp) {  // k_tsp_pp: one 8-wave workgroup per candidate (cp <= 64, npairs <= 64)
+    if (pp == 1) {  // k_tsp_pp: one 8-wave workgroup per candidate (cp <= 64, npairs <= 64)
         const size_t lds = sizeof(double) * ((size_t)2 * j->n * 4 + 64 * 64) + 64 * 64;
 #define SSPP_LAUNCH_TSPPP(OG, CBV)                                                                       \
         hipLaunchKernelGGL((k_tsp_pp<1, OG, CBV, 8>), dim3(nblk), dim3(512), lds, st, k, tt, j->d_tab,   \
@@ -1986,21 +2101,34 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
 #undef SSPP_LAUNCH_TSPPP
         return hipGetLastError();
     }
-#define SSPP_LAUNCH_TSP(OG, CBV, UPV)                                                                  \
-    hipLaunchKernelGGL((k_tsp<1, OG, CBV, UPV>), dim3(nblk), dim3(kBlock), j->lds, st, k, tt, j->d_tab, \
+#define SSPP_LAUNCH_TSP(OG, CBV, UPV, DEFV)                                                             \
+    hipLaunchKernelGGL((k_tsp<1, OG, CBV, UPV, DEFV>), dim3(nblk), dim3(kBlock), lds, st, k, tt, j->d_tab, \
                        j->d_span, j->d_Minv, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, \
                        d_status, j->d_part, j->d_sync, d_best)
     const bool og = k.sc.onegeom && k.sc.npairs > 0;
     const int cbm = k.sc.cylbox ? (k.sc.cbup ? 2 : 1) : 0;
     const bool up = k.sc.upright && cbm != 1;
-    if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false);
-    else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true); else SSPP_LAUNCH_TSP(true, 2, false); }
-    else if (og && up) SSPP_LAUNCH_TSP(true, 0, true);
-    else if (og) SSPP_LAUNCH_TSP(true, 0, false);
-    else if (cbm == 1) SSPP_LAUNCH_TSP(false, 1, false);
-    else if (cbm == 2) { if (up) SSPP_LAUNCH_TSP(false, 2, true); else SSPP_LAUNCH_TSP(false, 2, false); }
-    else if (up) SSPP_LAUNCH_TSP(false, 0, true);
-    else SSPP_LAUNCH_TSP(false, 0, false);
+    // pp == 3: the deferred-polygon form (host-checked: one waypoint per lane, <= kDefPairs pairs)
+    const size_t lds = pp == 3 ? j->lds + tsp_def_lds(k.sc.npairs) : j->lds;
+    if (pp == 3) {
+        if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false, true);
+        else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true, true); else SSPP_LAUNCH_TSP(true, 2, false, true); }
+        else if (og && up) SSPP_LAUNCH_TSP(true, 0, true, true);
+        else if (og) SSPP_LAUNCH_TSP(true, 0, false, true);
+        else if (cbm == 1) SSPP_LAUNCH_TSP(false, 1, false, true);
+        else if (cbm == 2) { if (up) SSPP_LAUNCH_TSP(false, 2, true, true); else SSPP_LAUNCH_TSP(false, 2, false, true); }
+        else if (up) SSPP_LAUNCH_TSP(false, 0, true, true);
+        else SSPP_LAUNCH_TSP(false, 0, false, true);
+        return hipGetLastError();
+    }
+    if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false, false);
+    else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true, false); else SSPP_LAUNCH_TSP(true, 2, false, false); }
+    else if (og && up) SSPP_LAUNCH_TSP(true, 0, true, false);
+    else if (og) SSPP_LAUNCH_TSP(true, 0, false, false);
+    else if (cbm == 1) SSPP_LAUNCH_TSP(false, 1, false, false);
+    else if (cbm == 2) { if (up) SSPP_LAUNCH_TSP(false, 2, true, false); else SSPP_LAUNCH_TSP(false, 2, false, false); }
+    else if (up) SSPP_LAUNCH_TSP(false, 0, true, false);
+    else SSPP_LAUNCH_TSP(false, 0, false, false);
 #undef SSPP_LAUNCH_TSP
     return hipGetLastError();
 }

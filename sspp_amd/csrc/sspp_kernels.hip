@@ -886,7 +886,7 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
             return set_job_tables(j, j->h_stage.data(), j->sigma, j->h_stage.data() + nd, (int)value, true, nullptr);
         }
         case SSPP_OPT_TSP_FORM:
-            if (j->kind != 1 || value < -1 || value > 2) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_FORM: -1..2");
+            if (j->kind != 1 || value < -1 || value > 3) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_FORM: -1..3");
             j->tsp_form = (int)value;
             return SSPP_OK;
         case SSPP_OPT_TSP_GENERIC:
@@ -1004,7 +1004,7 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     // split, 2 the multi-workgroup split where it applies; -1 = by batch size)
     const int pp_opt = j->tsp_form;
     const bool pp_ok = j->cp <= 64 && k.sc.npairs <= 64 && B <= j->part_cap;
-    const bool pp = pp_ok && (pp_opt < 0 ? B <= kTspPpMaxBatch : pp_opt > 0);
+    const bool pp = pp_ok && (pp_opt < 0 ? B <= kTspPpMaxBatch : (pp_opt == 1 || pp_opt == 2));
     const int npg = (k.sc.npairs + 7) / 8;
     int mode = pp ? 1 : 0;
     if (pp && npg > 1 && pp_opt != 1 && B <= kTspPpMaxBatch) {
@@ -1022,6 +1022,13 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
             k.rec_nd = j->d_pp_nd; k.rec_term = j->d_pp_term; k.arrive = j->d_pp_arrive; k.npg = npg;
         }
     }
+    // the deferred-polygon form of k_tsp (mode 3): one waypoint per lane, few pairs, some of them
+    // box-box (the polygons it defers); the default for such batches above the pair-split sizes
+    bool has_bb = false;
+    for (const DPair& pr : j->scene->pairs) has_bb |= j->scene->geoms[pr.gm].type == 6 && pr.otype == 6;
+    const bool def_ok = j->cp <= j->lpc && k.sc.npairs >= 1 && k.sc.npairs <= kDefPairs && has_bb &&
+                        j->lds + tsp_def_lds(k.sc.npairs) <= 64 * 1024;
+    if (mode == 0 && def_ok && (pp_opt < 0 || pp_opt == 3)) mode = 3;
     const int nblk = mode == 2 ? (int)B * npg : mode == 1 ? (int)B : (int)((B + j->cpb - 1) / j->cpb);
     j->last_form = mode;
     hipStream_t st = (hipStream_t)stream;

@@ -226,11 +226,15 @@ def stacking_problem(B, cp=128, seed=0x5EED, K=1):
     return model, scene, job, oscene, start, end, mean, sigma, lo, hi
 
 
-@pytest.mark.parametrize("B,cp,K", [(16384, 128, 1), (333, 40, 1), (200, 64, 3), (50, 300, 2)])
-def test_stacking_tsp_matches_oracle(cuda, B, cp, K):
+@pytest.mark.parametrize("form", [-1, 0])
+@pytest.mark.parametrize("B,cp,K", [(16384, 128, 1), (333, 40, 1), (200, 64, 3), (50, 300, 2), (1000, 256, 1)])
+def test_stacking_tsp_matches_oracle(cuda, B, cp, K, form):
+    """form -1: the library's choice (k_tsp with deferred box-box polygons where it applies:
+    one waypoint per lane), 0: the inline k_tsp."""
     import sspp_amd as S
     import torch
     model, scene, job, oscene, start, end, mean, sigma, lo, hi = stacking_problem(B, cp, K=K)
+    job.set_option(S.OPT_TSP_FORM, form)
     out = job.alloc(B, with_vias=True)
     job.sample_score(5, B, out["L"], out["Cnf"], out["Cwf"], out["status"], out["cost"],
                      out["best"], vias_out=out["vias"])
@@ -248,6 +252,8 @@ def test_stacking_tsp_matches_oracle(cuda, B, cp, K):
     assert idx == (idx_o + 5 if idx_o >= 0 else -1)
     if B >= 1000:
         assert 0 < st.sum() < B  # both outcomes present
+    if form < 0 and cp <= 256 and B > 512:
+        assert job.get_option(S.OPT_TSP_FORM) == 3  # the deferred form ran
 
 
 @pytest.mark.parametrize("nt,g1", SHAPES)
@@ -629,14 +635,14 @@ def test_tsp_kernel_forms_identical(cuda, xml, body, B, cp):
     job = S.TspJob(scene, start, end, 1, cp, mean=mean, sigma=sigma, lo=np.array(lo), hi=np.array(hi),
                    z_min=0.0, max_batch=B)
     res = {}
-    for mode in ("0", "1", "2"):
+    for mode in ("0", "1", "2", "3"):
         job.set_option(S.OPT_TSP_FORM, int(mode))
         q = job.alloc(B, device="cuda", with_vias=True)
         job.sample_score(0, B, q["L"], q["Cnf"], q["Cwf"], q["status"], q["cost"], q["best"],
                          vias_out=q["vias"])
         torch.cuda.synchronize()
         res[mode] = {k: v.cpu().numpy() for k, v in q.items()}
-    for mode in ("1", "2"):
+    for mode in ("1", "2", "3"):
         for k in ("L", "Cnf", "Cwf", "cost", "status", "vias", "best"):
             np.testing.assert_array_equal(res[mode][k], res["0"][k], err_msg="%s %s" % (mode, k))
     osc = O.Scene(mjcf_ref.load(path), 1, bid)
