@@ -37,6 +37,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+# kernel revision: PMC records (profiles/*_latest.json) measured on another revision of the
+# kernels are not attached to a line (tools/update_latest.py stamps them)
+KERNEL_REV = "r04"
 FP64_PEAK_TFLOPS = 78.6    # FP64 vector (VALU) spec
 
 
@@ -752,7 +755,7 @@ def main(argv=None):
     tf = os.path.join(ROOT, "profiles", "traffic_latest.json")
     if os.path.exists(tf):
         rec = json.load(open(tf)).get(pmc_key)
-        if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and \
+        if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and rec.get("rev") == KERNEL_REV and \
                 rec.get("candidates_per_launch") == per_launch:
             traffic, traffic_src = rec["hbm_bytes_per_launch"], rec["source"]
 
@@ -772,7 +775,7 @@ def main(argv=None):
         ff = os.path.join(ROOT, "profiles", "fp64_latest.json")
         if os.path.exists(ff):
             rec = json.load(open(ff)).get(pmc_key)
-            if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and \
+            if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and rec.get("rev") == KERNEL_REV and \
                     rec.get("candidates_per_launch", per_launch) == per_launch:
                 exec_per, exec_src = rec["fp64_flops_per_candidate"], rec["source"]
                 ach_exec = exec_per * per_launch / kernel_s / 1e12

@@ -1,4 +1,4 @@
-"""Fold a PMC evidence run (tools/gpu_round2_pmc.sh) into profiles/traffic_latest.json and
+"""Fold a PMC evidence run (tools/runs/gpu_pmc.sh) into profiles/traffic_latest.json and
 profiles/fp64_latest.json, which bench.py reads for roofline.traffic / roofline_fp64.
     python tools/update_latest.py gpurun_out/TAG profiles/PREFIX
 Per config: the dominant kernel's launches of the roofline shape (the most frequent grid),
@@ -10,6 +10,9 @@ import csv
 import json
 import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import KERNEL_REV  # noqa: E402  (records of another kernel revision are not attached)
 
 # record keys: the bench config, or config_b<batch>_w<waypoints> off the default shape
 KERNEL = {"robocrane": "k_sspp_c2f", "stacking": "k_tsp", "multigoal": "k_tsp",
@@ -60,7 +63,7 @@ def main(src, prefix):
                        grid=f["grid"], vgpr=f["VGPR_Count"], sgpr=f["SGPR_Count"],
                        scratch_per_lane=f["Scratch_Size"], lds=f["LDS_Block_Size"])
             res["hbm_bytes_per_launch"] = 1024.0 * (2.0 * f["FETCH_SIZE"] + w["WRITE_SIZE"])
-            traffic[cfg] = {"kernel": kern, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
+            traffic[cfg] = {"kernel": kern, "rev": KERNEL_REV, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
                             "candidates_per_launch": PER_LAUNCH[cfg],
                             "source": "%s_%s_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
                                       "FETCH x2 gfx950 correction; %s)" % (prefix, cfg, STEPS[cfg])}
@@ -72,7 +75,7 @@ def main(src, prefix):
                          m["SQ_INSTS_VALU_TRANS_F64"] + 2 * m["SQ_INSTS_VALU_FMA_F64"])
             res["fp64_flops_per_launch"] = fl
             res["fp64_flops_per_candidate"] = fl / PER_LAUNCH[cfg]
-            fp64[cfg] = {"kernel": kern, "fp64_flops_per_candidate": res["fp64_flops_per_candidate"],
+            fp64[cfg] = {"kernel": kern, "rev": KERNEL_REV, "fp64_flops_per_candidate": res["fp64_flops_per_candidate"],
                          "candidates_per_launch": PER_LAUNCH[cfg],
                          "source": "%s_%s_pmc.json: 64 x (ADD+MUL+TRANS+2 FMA)_F64 wave instructions per "
                                    "launch / %d candidates" % (prefix, cfg, PER_LAUNCH[cfg])}

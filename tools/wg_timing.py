@@ -26,9 +26,10 @@ run(5)
 torch.cuda.synchronize()
 run(steps)
 torch.cuda.synchronize()
-nt, g1 = int(os.environ.get("SSPP_NT", "64" if steps * 4096 >= 16384 else "256")), \
-    int(os.environ.get("SSPP_G1", "4" if steps * 4096 >= 16384 else "64"))
-nwg = steps * (B // (nt // g1))  # candidates per workgroup: NT / G1
+cfg = ctx["job"].config()  # the shape the timed launch ran
+nt, g1 = (int(x) for x in cfg["shape"].split("x"))
+cpb = (nt // 64) * (64 // g1)
+nwg = steps * ((B + cpb - 1) // cpb)
 buf = (C.c_ulonglong * (4 * nwg))()
 _lib.lib().__getattr__("sspp_debug_wg_times")(buf, 4 * nwg)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 4).astype(np.int64)
