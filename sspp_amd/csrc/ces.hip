@@ -488,11 +488,21 @@ struct sspp_ces {
     int* d_nsucc = nullptr;
     double *d_LT = nullptr, *d_LH = nullptr;
     hipStream_t last = nullptr;         // stream of the last enqueued operation (sspp_ces_read waits on it)
+    bool mixed = false;                 // operations since the last read used more than one stream
+    bool any_op = false;
     unsigned char* h_stage = nullptr;   // pinned: k_ces_stage's output
     size_t stage_bytes = 0;
     long long staged_iter = -1;         // iteration whose results k_ces_update already staged
     int fused = 1;                      // SSPP_OPT_CES_FUSED (sspp_ces_set_option)
 };
+
+// every enqueuing entry point notes its stream: sspp_ces_read waits on the last one, or on the
+// whole device when the operations since the previous read were spread over several streams
+static void note_stream(sspp_ces* p, hipStream_t s) {
+    if (p->any_op && s != p->last) p->mixed = true;
+    p->any_op = true;
+    p->last = s;
+}
 
 static CesK ces_k(const sspp_ces* p) {
     CesK c{};
@@ -643,7 +653,7 @@ int sspp_ces_begin(sspp_ces* p, const double* start, const double* end, int iter
         s = s < p->cfg.sigma_floor ? p->cfg.sigma_floor : s;
         r.sigma0 = s;
     }
-    p->last = (hipStream_t)stream;
+    note_stream(p, (hipStream_t)stream);
     p->staged_iter = -1;
     hipLaunchKernelGGL(k_ces_begin, dim3(1), dim3(128), 0, (hipStream_t)stream, ces_k(p), iterate ? 1 : 0,
                        r, p->d_hdr, p->d_mean, p->d_sigma, p->d_lbest, p->d_fixed);
@@ -663,7 +673,7 @@ int sspp_ces_eval(sspp_ces* p, int rank, void* stream) {
     ev.first_id = p->iter * (long long)p->cfg.samples;
     for (int i = 0; i < 4; ++i) { ev.start[i] = p->start[i]; ev.end[i] = p->end[i]; }
     const size_t o = (size_t)rank * p->spr;
-    p->last = (hipStream_t)stream;
+    note_stream(p, (hipStream_t)stream);
     p->staged_iter = -1;
     return sspp::tsp_eval_ces(p->job, &ev, p->spr, p->d_L + o, p->d_Cnf + o, p->d_Cwf + o,
                               p->d_status + o, p->d_cost + o, p->d_vias + o * 4 * p->K, stream);
@@ -674,7 +684,7 @@ int sspp_ces_update(sspp_ces* p, void* stream) {
     if (!p) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_update: null planner");
     const int nt = (p->nslots + kRankTile - 1) / kRankTile;
     hipStream_t st = (hipStream_t)stream;
-    p->last = st;
+    note_stream(p, st);
     const int fused = p->nslots <= kCesThreads && p->fused;
     if (!fused) {
         hipLaunchKernelGGL(k_ces_rank, dim3(nt, nt), dim3(kRankTile), 0, st, p->nslots, p->d_cost,
@@ -726,7 +736,7 @@ int sspp_ces_unpack(sspp_ces* p, const double* d_in, void* stream) {
     const int KD = 4 * p->K;
     const long long tot = (long long)p->nslots * (5 + KD);
     const int g = (int)std::min<long long>((tot + 255) / 256, 1024);
-    p->last = (hipStream_t)stream;
+    note_stream(p, (hipStream_t)stream);
     p->staged_iter = -1;
     hipLaunchKernelGGL(k_ces_unpack, dim3(g), dim3(256), 0, (hipStream_t)stream, p->nslots, KD, d_in,
                        p->d_L, p->d_Cnf, p->d_Cwf, p->d_cost, p->d_status, p->d_vias);
@@ -749,9 +759,16 @@ int sspp_ces_read(sspp_ces* p, sspp_ces_state* st, double* L, double* Cnf, doubl
     sspp::clear_error();
     if (!p || !st) return sspp::set_error(SSPP_E_INVAL, "sspp_ces_read: null argument");
     // one staging launch behind the planner's last operation (none when the last update staged
-    // its iteration itself), one wait on that stream
+    // its iteration itself), one wait on that stream — preceded by a device-wide wait when the
+    // operations since the previous read ran on more than one stream (the staging must see them
+    // all, and the earlier streams may be gone by now: the device wait needs none of them)
     const int n = p->nslots, KD = 4 * p->K;
     hipError_t e = hipSuccess;
+    if (p->mixed) {
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) return hip_err(e, "sspp_ces_read");
+        p->mixed = false;
+    }
     if (p->staged_iter != p->iter) {
         const long long tot = 4LL * n + (long long)n * KD + 3LL * KD + p->cap + n;
         const int g = (int)std::min<long long>((tot + 255) / 256, 256);
