@@ -1496,10 +1496,10 @@ constexpr int kDefPairs = 8;
 #ifndef SSPP_TSP_WAVES_PER_EU_DEF
 #define SSPP_TSP_WAVES_PER_EU_DEF 4
 #endif
-template <int NM, bool ONEGEOM, int CB, bool UP = false, bool DEF = false>
-__global__ __launch_bounds__(kBlock, DEF ? SSPP_TSP_WAVES_PER_EU_DEF
-                                         : (CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
-                                                    : (ONEGEOM ? SSPP_TSP_WAVES_PER_EU : SSPP_TSP_WAVES_PER_EU_MG))) void k_tsp(
+template <int NM, bool ONEGEOM, int CB, bool UP = false, int DEF = 0>
+__global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
+                                              : (CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
+                                                         : (ONEGEOM ? SSPP_TSP_WAVES_PER_EU : SSPP_TSP_WAVES_PER_EU_MG))) void k_tsp(
     TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
     const double* __restrict__ sigma, const double* __restrict__ vias_in,
@@ -1517,8 +1517,8 @@ __global__ __launch_bounds__(kBlock, DEF ? SSPP_TSP_WAVES_PER_EU_DEF
     double* s_wsum = s_ctrl + cpb * ndof;    // [3][4]
     double* s_best = s_wsum + 3 * (kBlock / 64);
     int* s_stat = (int*)(s_best + 4);        // [cpb]
-    // DEF: per-lane records [kBlock][np] (terms, counts), mover poses [kBlock][8], deferred list
-    const int npr = DEF ? a.sc.npairs : 0;
+    // DEF 1: per-lane records [kBlock][np] (terms, counts), mover poses [kBlock][8], deferred list
+    const int npr = DEF == 1 ? a.sc.npairs : 0;
     double* s_rterm = (double*)(s_stat + ((cpb + 1) & ~1));
     double* s_rpose = s_rterm + kBlock * npr;
     unsigned char* s_rnd = (unsigned char*)(s_rpose + (DEF ? kBlock * 8 : 0));
@@ -1538,7 +1538,7 @@ __global__ __launch_bounds__(kBlock, DEF ? SSPP_TSP_WAVES_PER_EU_DEF
     // cp <= lpc: one waypoint per lane, so s((i-1)du) is the previous lane's s(i du); take it
     // by shuffle (bit-identical: same eval_pt inputs) except on a wave's first lane
     const bool one_pass = cp <= lpc;
-    if (DEF) {  // host-checked: one waypoint per lane (cp <= lpc), np <= kDefPairs, NM == 1
+    if (DEF == 1) {  // host-checked: one waypoint per lane (cp <= lpc), np <= kDefPairs, NM == 1
         if (tid == 0) *s_nitems = 0;
         unsigned char* rn = s_rnd + tid * npr;
         double* rt = s_rterm + tid * npr;
@@ -2109,26 +2109,20 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
     const int cbm = k.sc.cylbox ? (k.sc.cbup ? 2 : 1) : 0;
     const bool up = k.sc.upright && cbm != 1;
     // pp == 3: the deferred-polygon form (host-checked: one waypoint per lane, <= kDefPairs pairs)
-    const size_t lds = pp == 3 ? j->lds + tsp_def_lds(k.sc.npairs) : j->lds;
-    if (pp == 3) {
-        if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false, true);
-        else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true, true); else SSPP_LAUNCH_TSP(true, 2, false, true); }
-        else if (og && up) SSPP_LAUNCH_TSP(true, 0, true, true);
-        else if (og) SSPP_LAUNCH_TSP(true, 0, false, true);
-        else if (cbm == 1) SSPP_LAUNCH_TSP(false, 1, false, true);
-        else if (cbm == 2) { if (up) SSPP_LAUNCH_TSP(false, 2, true, true); else SSPP_LAUNCH_TSP(false, 2, false, true); }
-        else if (up) SSPP_LAUNCH_TSP(false, 0, true, true);
-        else SSPP_LAUNCH_TSP(false, 0, false, true);
-        return hipGetLastError();
-    }
-    if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false, false);
-    else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true, false); else SSPP_LAUNCH_TSP(true, 2, false, false); }
-    else if (og && up) SSPP_LAUNCH_TSP(true, 0, true, false);
-    else if (og) SSPP_LAUNCH_TSP(true, 0, false, false);
-    else if (cbm == 1) SSPP_LAUNCH_TSP(false, 1, false, false);
-    else if (cbm == 2) { if (up) SSPP_LAUNCH_TSP(false, 2, true, false); else SSPP_LAUNCH_TSP(false, 2, false, false); }
-    else if (up) SSPP_LAUNCH_TSP(false, 0, true, false);
-    else SSPP_LAUNCH_TSP(false, 0, false, false);
+    const int def = pp == 3 ? 1 : 0;
+    const size_t lds = def ? j->lds + tsp_def_lds(k.sc.npairs) : j->lds;
+#define SSPP_LAUNCH_TSP_ALL(DEFV)                                                                         \
+    if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false, DEFV);                                            \
+    else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true, DEFV); else SSPP_LAUNCH_TSP(true, 2, false, DEFV); } \
+    else if (og && up) SSPP_LAUNCH_TSP(true, 0, true, DEFV);                                              \
+    else if (og) SSPP_LAUNCH_TSP(true, 0, false, DEFV);                                                   \
+    else if (cbm == 1) SSPP_LAUNCH_TSP(false, 1, false, DEFV);                                            \
+    else if (cbm == 2) { if (up) SSPP_LAUNCH_TSP(false, 2, true, DEFV); else SSPP_LAUNCH_TSP(false, 2, false, DEFV); } \
+    else if (up) SSPP_LAUNCH_TSP(false, 0, true, DEFV);                                                   \
+    else SSPP_LAUNCH_TSP(false, 0, false, DEFV);
+    if (def == 1) { SSPP_LAUNCH_TSP_ALL(1) }
+    else { SSPP_LAUNCH_TSP_ALL(0) }
+#undef SSPP_LAUNCH_TSP_ALL
 #undef SSPP_LAUNCH_TSP
     return hipGetLastError();
 }

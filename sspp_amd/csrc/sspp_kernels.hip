@@ -1023,7 +1023,9 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
         }
     }
     // the deferred-polygon form of k_tsp (mode 3): one waypoint per lane, few pairs, some of them
-    // box-box (the polygons it defers); the default for such batches above the pair-split sizes
+    // box-box (the polygons it defers); the default for such batches above the pair-split sizes.
+    // (A form in rounds for many pairs — the gripper's 48 — measured more registers than the
+    // inline narrowphase: the polygons of divergent pairs need the pair data in VGPRs.)
     bool has_bb = false;
     for (const DPair& pr : j->scene->pairs) has_bb |= j->scene->geoms[pr.gm].type == 6 && pr.otype == 6;
     const bool def_ok = j->cp <= j->lpc && k.sc.npairs >= 1 && k.sc.npairs <= kDefPairs && has_bb &&
