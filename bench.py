@@ -69,6 +69,9 @@ def parse(argv=None):
                     help="robocrane sampleWithNoise normals: fp64 Box-Muller (default, bit-exact "
                          "oracle) or the opt-in fp32 quad sampler")
     ap.add_argument("--budgets-ms", default="10,20,50", help="tsp-anytime: wall-clock budgets")
+    ap.add_argument("--shape", default="",
+                    help="robocrane: force the k_sspp_c2f launch shape NTxG1 (e.g. 64x4; tuning, "
+                         "default: chosen per launch by the library); the line reports it")
     ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--steps-per-launch", type=int, default=32,
                     help="native mode: independent steps (each its own B candidates, outputs and "
@@ -96,6 +99,10 @@ def setup_robocrane(args, device):
     sampler = S.SAMPLER_FP32 if args.sampler == "fp32" else S.SAMPLER_FP64
     jobs = [S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), W, seed=S.DEFAULT_SEED, max_batch=B,
                       sampler=sampler) for _ in range(args.streams)]
+    if args.shape:
+        nt, g1 = (int(x) for x in args.shape.lower().split("x"))
+        for j in jobs:
+            j.set_shape(nt, g1)
     bufs = [j.alloc(B, device=device) for j in jobs]
     job = jobs[0]
 

@@ -218,6 +218,29 @@ def test_device_plan_iterations_equals_stepping(cuda):
 
 
 @pytest.mark.gpu
+def test_read_after_operations_on_several_streams(cuda):
+    """begin / eval / update each on its own (then destroyed) stream: read() still returns the
+    finished iteration (it waits on the whole device when the planner's operations since the
+    previous read used more than one stream), equal to the same iteration on one stream."""
+    import torch
+    a, _, _, start, end = stacking_planner(2000)
+    b, _, _, _, _ = stacking_planner(2000)
+    for t in range(3):
+        s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+        a.begin(start, end, t > 0, stream=s1)
+        s2.wait_stream(s1)
+        a.eval(stream=s2)
+        s3.wait_stream(s2)
+        a.update(stream=s3)
+        del s1, s2, s3
+        ra = a.read()
+        b.step(start, end, iterate=t > 0)
+        rb = b.read()
+        for k in ("mean", "sigma", "last_best", "cost", "status", "vias", "elites"):
+            np.testing.assert_array_equal(ra[k], rb[k], err_msg="%s at %d" % (k, t))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
 def test_multirank_exchange_equals_single_rank(cuda, world):
     """world ranks emulated in one process: each evaluates its slots, the packed records are

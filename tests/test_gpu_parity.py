@@ -473,6 +473,7 @@ def test_environment_does_not_change_results(robocrane, monkeypatch):
                      SSPP_PAIR_ORDER="0", SSPP_REACH="0", SSPP_HULL="0", SSPP_INSAMPLE="0").items():
         monkeypatch.setenv(k, v)
     again, cfg1 = run()
+    cfg0.pop("prepass_ms"), cfg1.pop("prepass_ms")  # host timing
     assert cfg0 == cfg1 and cfg0["sampler"] == "fp64"
     for k in ("ctrl", "arc", "feasible"):
         assert np.array_equal(base[k], again[k]), k
