@@ -964,6 +964,44 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
     return ghit;
 }
 
+// ================================================================ hit census (job creation)
+// The waypoint order of k_sspp_c2f's phase 1 is chosen from where sampled candidates of the
+// job's own distribution touch the scene: one workgroup per census candidate draws it
+// (sampleWithNoise, the job's sigma / limits, an independent seed) and tests every collision
+// waypoint u = i / W, one per lane, against the sampled-candidate pair table (scan_pairs; a
+// cylinder-box pair left undecided counts as no contact: the census only steers the order).
+// Output: hit bits [M][ceil((W+1) / 64)], bit i = contact at waypoint i.
+constexpr int kCensusThreads = 256;
+template <int D, int NM, int P, bool ONEGEOM>
+__global__ __launch_bounds__(kCensusThreads) void k_sspp_census(
+    KScene sc, SceneT T, int n, int W, int sampler, double sigma, unsigned long long seed,
+    const double* __restrict__ tab, const int* __restrict__ span, const double* __restrict__ init_ctrl,
+    const double* __restrict__ limits, unsigned long long* __restrict__ hits) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int P1 = P + 1;
+    const int tid = threadIdx.x, m = blockIdx.x, ndof = n * D, nw = (W + 64) >> 6;
+    const int r0 = P < n ? P : n, r1 = n - P > r0 ? n - P : r0, nrd = (r1 - r0) * D;
+    double* s_fix = smem;             // [n][D]
+    double* s_own = s_fix + ndof;     // [r1 - r0][D]
+    double* s_lim = s_own + nrd;      // [D]
+    for (int e = tid; e < ndof; e += kCensusThreads) s_fix[e] = init_ctrl[e];
+    if (tid < D) s_lim[tid] = limits[tid];
+    for (int w = tid; w < nw; w += kCensusThreads) hits[(long long)m * nw + w] = 0ull;
+    __syncthreads();
+    for (int it = tid; it < sample_items(sampler, nrd); it += kCensusThreads)
+        sample_item_to(sampler, seed, (unsigned long long)m, it, nrd, D, sigma, s_lim, s_fix + r0 * D, s_own);
+    __syncthreads();
+    for (int j0 = 0; j0 <= W; j0 += kCensusThreads) {  // workgroup-uniform
+        const int j = j0 + tid;
+        const bool live = j <= W;
+        double q[D];
+        eval_split_g<D, P>(smem, ndof, 0, r0, r1, tab + (live ? j : 0) * P1, span[live ? j : 0], q);
+        bool dfr = false;
+        const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, ~0ull, ~0ull, 1ull << (tid & 63), nullptr, sc, T, dfr);
+        if (h && live) atomicOr(hits + (long long)m * nw + (j >> 6), 1ull << (j & 63));
+    }
+}
+
 #ifndef SSPP_CB_INLINE
 #define SSPP_CB_INLINE __attribute__((noinline))
 #endif
@@ -2061,6 +2099,37 @@ hipError_t entry_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int
 #endif
 }
 
+// the hit census of a sampled job (k_sspp_census): M candidates, every collision waypoint
+template <int D, int NM, int P>
+hipError_t launch_census(const sspp_job* j, int M, unsigned long long seed, unsigned long long* d_hits,
+                         hipStream_t st) {
+    const KScene sc = kscene_job(j, true);
+    const SceneT T = scene_t_job(j, true);
+    const int r0 = std::min(P, j->n), r1 = std::max(r0, j->n - P);
+    const size_t lds = sizeof(double) * ((size_t)j->n * D + (size_t)(r1 - r0) * D + D);
+    if (NM == 1 && sc.onegeom && sc.npairs > 0)
+        hipLaunchKernelGGL((k_sspp_census<D, 1, P, true>), dim3(M), dim3(kCensusThreads), lds, st, sc, T, j->n, j->W,
+                           j->sampler, j->sigma, seed, j->d_tab, j->d_span, j->d_init, j->d_limits, d_hits);
+    else
+        hipLaunchKernelGGL((k_sspp_census<D, NM, P, false>), dim3(M), dim3(kCensusThreads), lds, st, sc, T, j->n,
+                           j->W, j->sampler, j->sigma, seed, j->d_tab, j->d_span, j->d_init, j->d_limits, d_hits);
+    return hipGetLastError();
+}
+template <int D>
+hipError_t entry_census(const sspp_job* j, int M, unsigned long long seed, unsigned long long* d_hits, hipStream_t st) {
+    if (j->nm == 2) {
+        if constexpr (D == 9) return j->p == 3 ? launch_census<9, 2, 3>(j, M, seed, d_hits, st)
+                                               : launch_census<9, 2, 2>(j, M, seed, d_hits, st);
+        return hipErrorInvalidValue;
+    }
+#ifdef SSPP_DEV_ONLY
+    if (j->p != 3) return hipErrorInvalidValue;
+    return launch_census<D, 1, 3>(j, M, seed, d_hits, st);
+#else
+    return j->p == 3 ? launch_census<D, 1, 3>(j, M, seed, d_hits, st) : launch_census<D, 1, 2>(j, M, seed, d_hits, st);
+#endif
+}
+
 // TaskSpacePlanner evaluation (k_tsp), its own translation unit (SSPK_D = 0)
 template <int Unused>
 hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* mean, const double* sigma,
@@ -2128,7 +2197,8 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
 }
 
 #define SSPK_ENTRY_DECL(X, D)                                                                             \
-    X template hipError_t entry_c2f<D>(const SsppC2F&, const sspp_job*, const SsppPtrs&, int, hipStream_t);
+    X template hipError_t entry_c2f<D>(const SsppC2F&, const sspp_job*, const SsppPtrs&, int, hipStream_t); \
+    X template hipError_t entry_census<D>(const sspp_job*, int, unsigned long long, unsigned long long*, hipStream_t);
 #define SSPK_TSP_DECL(X)                                                                                  \
     X template hipError_t entry_tsp<0>(const TspK&, const sspp_job*, int, const double*, const double*,    \
                                        const double*, double*, double*, double*, double*, double*, uint8_t*, \

@@ -415,33 +415,104 @@ static std::vector<int> c2f_order(int W) {
     return ord;
 }
 
-// Hit-order pre-pass of a sampled job (sigma > 0).  checkCollision's answer is an
-// OR over (waypoint, pair), so the order of both is free; k_sspp_c2f's phase 1 tests a prefix of
-// the waypoint order and stops a candidate at its first touching pair, so waypoints and pairs
-// that settle the most sampled candidates should come first.  M host-sampled candidates of the
-// job's distribution (its sigma and limits; host normals: the order only steers the scans, never
-// their results), the pairs each touches at the first kGrid waypoints of the bisection order
-// (an even spread over the path); then, greedily, the waypoint that settles the most candidates
-// not yet settled (up to kPick of them, the rest in bisection order), and the pairs in the same
-// way over the contacts at the first n1 chosen waypoints (the rest in their previous order).
-static void hit_order(const sspp_scene* sc, std::vector<DPair>& pairs, std::vector<int>& wps,
-                      const double* knots, int nknots, int p, const double* ctrl0, int D, double sigma,
-                      const double* limits, int W, int n1) {
+// Hit order of a sampled job (sigma > 0).  checkCollision's answer is an OR over
+// (waypoint, pair), so the order of both is free; k_sspp_c2f's phase 1 tests a prefix of the
+// waypoint order and stops a candidate at its first touching pair, so the waypoints and pairs
+// that settle the most sampled candidates should come first.  The orders only steer the scans,
+// never their results.
+//
+// Waypoints: the GPU census (k_sspp_census) of kCensus candidates of the job's own distribution
+// (an independent Philox seed) gives, per candidate, the collision waypoints in contact.  The
+// first n1 waypoints (phase 1 tests them together) are the n1-set leaving the fewest candidates
+// untouched: a greedy set improved by single swaps until no swap helps; then, greedily, the
+// waypoint that settles the most candidates not yet settled (up to kPick in all), the rest in
+// bisection order.
+constexpr int kCensus = 2048, kPick = 12;
+static void waypoints_from_census(const std::vector<uint64_t>& hits, int M, int W, int n1, std::vector<int>& wps) {
+    const int nw = (W + 64) >> 6, npts = W + 1, mw = (M + 63) / 64;
+    // per waypoint: the candidates in contact there, as bits
+    std::vector<uint64_t> col((size_t)npts * mw, 0ull);
+    for (int m = 0; m < M; ++m)
+        for (int i = 0; i < npts; ++i)
+            if ((hits[(size_t)m * nw + (i >> 6)] >> (i & 63)) & 1ull) col[(size_t)i * mw + (m >> 6)] |= 1ull << (m & 63);
+    auto untouched = [&](const std::vector<int>& S) {
+        int c = 0;
+        for (int w = 0; w < mw; ++w) {
+            uint64_t acc = 0ull;
+            for (int i : S) acc |= col[(size_t)i * mw + w];
+            const uint64_t valid = (w == mw - 1 && (M & 63)) ? ((1ull << (M & 63)) - 1ull) : ~0ull;
+            c += __builtin_popcountll(~acc & valid);
+        }
+        return c;
+    };
+    n1 = std::max(1, std::min(n1, npts));
+    std::vector<int> S;
+    for (int r = 0; r < n1; ++r) {  // greedy
+        int bi = -1, bc = M + 1;
+        for (int i = 0; i < npts; ++i) {
+            if (std::find(S.begin(), S.end(), i) != S.end()) continue;
+            S.push_back(i);
+            const int c = untouched(S);
+            S.pop_back();
+            if (c < bc) { bc = c; bi = i; }
+        }
+        S.push_back(bi);
+    }
+    int cur = untouched(S);
+    for (int pass = 0; pass < 16; ++pass) {  // single swaps
+        int bpos = -1, bi = -1, bc = cur;
+        for (int pos = 0; pos < n1; ++pos) {
+            const int keep = S[pos];
+            for (int i = 0; i < npts; ++i) {
+                if (std::find(S.begin(), S.end(), i) != S.end()) continue;
+                S[pos] = i;
+                const int c = untouched(S);
+                if (c < bc) { bc = c; bpos = pos; bi = i; }
+            }
+            S[pos] = keep;
+        }
+        if (bpos < 0) break;
+        S[bpos] = bi;
+        cur = bc;
+    }
+    std::vector<int> order = S;
+    while ((int)order.size() < kPick && (int)order.size() < npts) {  // greedy continuation
+        int bi = -1, bc = untouched(order);
+        for (int i = 0; i < npts; ++i) {
+            if (std::find(order.begin(), order.end(), i) != order.end()) continue;
+            order.push_back(i);
+            const int c = untouched(order);
+            order.pop_back();
+            if (c < bc) { bc = c; bi = i; }
+        }
+        if (bi < 0) break;
+        order.push_back(bi);
+    }
+    std::vector<char> taken(npts, 0);
+    for (int i : order) taken[i] = 1;
+    for (int w : wps) if (!taken[w]) order.push_back(w);
+    wps.swap(order);
+}
+
+// Pairs: M host-sampled candidates of the job's distribution (host normals), the pairs each
+// touches at the phase-1 waypoints `pick`; greedily the pair that settles the most candidates not
+// yet settled, the rest in their previous order.
+static void pairs_by_hits(const sspp_scene* sc, std::vector<DPair>& pairs, const double* knots, int nknots, int p,
+                          const double* ctrl0, int D, double sigma, const double* limits, int W,
+                          const std::vector<int>& pick) {
     const int np = (int)pairs.size(), n = nknots - p - 1, nm = (int)sc->movers.size();
-    if (np < 1 || np > 64 || nm < 1 || nm > kMaxMovers) return;
-    constexpr int M = 128, kGrid = 33, kPick = 8;
-    const std::vector<int> grid(wps.begin(), wps.begin() + std::min<size_t>(wps.size(), kGrid));
-    const int ng = (int)grid.size();
+    if (np < 2 || np > 64 || nm < 1 || nm > kMaxMovers || pick.empty()) return;
+    constexpr int M = 256;
     std::mt19937_64 rng(0x5EEDull);
     std::normal_distribution<double> N01(0.0, 1.0);
-    std::vector<uint64_t> hit((size_t)M * ng, 0ull);
+    std::vector<uint64_t> cand(M, 0ull);
     std::vector<double> c((size_t)n * D);
     for (int m = 0; m < M; ++m) {
         for (size_t e = 0; e < c.size(); ++e) c[e] = ctrl0[e];
         for (int jj = p; jj < n - p; ++jj)
             for (int d = 0; d < D; ++d) c[(size_t)jj * D + d] += sigma * N01(rng) * limits[d];
-        for (int gi = 0; gi < ng; ++gi) {
-            const double u = (double)grid[gi] / W;
+        for (int w : pick) {
+            const double u = (double)w / W;
             const int sp = span_of(u, p, knots, nknots);
             double N[kMaxP + 1];
             basis_funcs(u, p, sp, knots, N);
@@ -462,8 +533,8 @@ static void hit_order(const sspp_scene* sc, std::vector<DPair>& pairs, std::vect
                 quat2mat(qp + 3, mR[mv]);
                 for (int k = 0; k < 3; ++k) mp[mv][k] = qp[k];
             }
-            uint64_t bits = 0ull;
             for (int k = 0; k < np; ++k) {
+                if ((cand[m] >> k) & 1ull) continue;
                 const DPair& pr = pairs[k];
                 const DGeom& G = sc->geoms[pr.gm];
                 const int mv = G.mover > 0 ? G.mover : 0;
@@ -489,54 +560,26 @@ static void hit_order(const sspp_scene* sc, std::vector<DPair>& pairs, std::vect
                 const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
                 const int nc = gfirst ? collide<false>(G.type, gp, gm, G.size, pr.otype, op, om, pr.osize, pr.margin, &nd)
                                       : collide<false>(pr.otype, op, om, pr.osize, G.type, gp, gm, G.size, pr.margin, &nd);
-                if (nc > 0) bits |= 1ull << k;
+                if (nc > 0) cand[m] |= 1ull << k;
             }
-            hit[(size_t)m * ng + gi] = bits;
         }
     }
-    // waypoints
-    std::vector<char> settled(M, 0), used(ng, 0);
-    std::vector<int> pick;
-    for (int it = 0; it < kPick; ++it) {
-        int best = -1, bc = 0;
-        for (int gi = 0; gi < ng; ++gi) {
-            if (used[gi]) continue;
-            int cnt = 0;
-            for (int m = 0; m < M; ++m) cnt += !settled[m] && hit[(size_t)m * ng + gi] != 0ull;
-            if (cnt > bc) { bc = cnt; best = gi; }
-        }
-        if (best < 0) break;
-        used[best] = 1;
-        pick.push_back(best);
-        for (int m = 0; m < M; ++m) settled[m] |= hit[(size_t)m * ng + best] != 0ull;
-    }
-    if (pick.empty()) return;  // nothing touches: keep the bisection order and the pair order
-    std::vector<int> order;
-    std::vector<char> taken(W + 1, 0);
-    for (int gi : pick) { order.push_back(grid[gi]); taken[grid[gi]] = 1; }
-    for (int w : wps) if (!taken[w]) order.push_back(w);
-    wps.swap(order);
-    // pairs, over the contacts at the first n1 chosen waypoints
-    std::vector<uint64_t> cand(M, 0ull);
-    for (int m = 0; m < M; ++m)
-        for (size_t i = 0; i < pick.size() && (int)i < std::max(1, n1); ++i) cand[m] |= hit[(size_t)m * ng + pick[i]];
-    std::vector<char> pused(np, 0);
-    std::fill(settled.begin(), settled.end(), 0);
+    std::vector<char> used(np, 0), settled(M, 0);
     std::vector<DPair> out;
     for (;;) {
         int best = -1, bc = 0;
         for (int k = 0; k < np; ++k) {
-            if (pused[k]) continue;
+            if (used[k]) continue;
             int cnt = 0;
             for (int m = 0; m < M; ++m) cnt += !settled[m] && ((cand[m] >> k) & 1ull);
             if (cnt > bc) { bc = cnt; best = k; }
         }
         if (best < 0) break;
-        pused[best] = 1;
+        used[best] = 1;
         out.push_back(pairs[best]);
         for (int m = 0; m < M; ++m) if ((cand[m] >> best) & 1ull) settled[m] = 1;
     }
-    for (int k = 0; k < np; ++k) if (!pused[k]) out.push_back(pairs[k]);
+    for (int k = 0; k < np; ++k) if (!used[k]) out.push_back(pairs[k]);
     pairs.swap(out);
 }
 
@@ -611,21 +654,69 @@ constexpr int kThroughputG1 = 4;
 // create: the waypoint order and both tables are (re)uploaded synchronously; otherwise the pair
 // tables are queued on `stream` from the pinned staging at byte offset `pin_off` (the caller
 // sized it for both) and the waypoint order stays.
+// both pair tables to the device, synchronously (job creation, option changes)
+static int upload_pairs_sync(sspp_job* j) {
+    const sspp_scene* sc = j->scene;
+    const size_t cap = sizeof(DPair) * std::max<size_t>(1, sc->pairs.size());
+    if (!j->d_pairs) HIPCHK(hipMalloc((void**)&j->d_pairs, cap));
+    if (!j->d_pairs_s) HIPCHK(hipMalloc((void**)&j->d_pairs_s, cap));
+    HIPCHK(hipMemcpy(j->d_pairs, j->h_pairs.data(), sizeof(DPair) * j->h_pairs.size(), hipMemcpyHostToDevice));
+    if (!j->h_pairs_s.empty())
+        HIPCHK(hipMemcpy(j->d_pairs_s, j->h_pairs_s.data(), sizeof(DPair) * j->h_pairs_s.size(), hipMemcpyHostToDevice));
+    return SSPP_OK;
+}
+
+// the hit census (k_sspp_census) of M candidates: hit bits [M][ceil((W + 1) / 64)] to the host
+static int run_census(sspp_job* j, int M, std::vector<uint64_t>& hits) {
+    const int nw = (j->W + 64) >> 6;
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc((void**)&d, sizeof(unsigned long long) * (size_t)M * nw));
+    const unsigned long long seed = j->seed ^ 0xC3A5C85C97CB3127ull;  // independent of the job's candidates
+    hipError_t e = hipErrorInvalidValue;
+    switch (j->D) {
+#ifndef SSPP_DEV_ONLY
+        case 1: e = entry_census<1>(j, M, seed, d, nullptr); break;
+        case 2: e = entry_census<2>(j, M, seed, d, nullptr); break;
+        case 3: e = entry_census<3>(j, M, seed, d, nullptr); break;
+        case 4: e = entry_census<4>(j, M, seed, d, nullptr); break;
+        case 6: e = entry_census<6>(j, M, seed, d, nullptr); break;
+        case 9: e = entry_census<9>(j, M, seed, d, nullptr); break;
+#endif
+        case 7: e = entry_census<7>(j, M, seed, d, nullptr); break;
+    }
+    hits.assign((size_t)M * nw, 0ull);
+    if (e == hipSuccess) e = hipMemcpy(hits.data(), d, sizeof(uint64_t) * hits.size(), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "k_sspp_census");
+    return SSPP_OK;
+}
+
 static int set_job_tables(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, int order,
                           bool create, void* stream, size_t pin_off = 0) {
     const sspp_scene* sc = j->scene;
     std::vector<int> wps = c2f_order(j->W);
     if (sc && !sc->pairs.empty()) {
         j->h_pairs = order == 0 ? sc->pairs : pairs_for_job(sc, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D);
-        if (order == 2 && create) {
-            const auto t0 = std::chrono::steady_clock::now();
-            hit_order(sc, j->h_pairs, wps, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D, sigma, limits, j->W,
-                      kThroughputG1);
-            j->prepass_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        }
         j->h_pairs_s = reachable_pairs(sc, j->h_pairs, init_ctrl, j->n, j->D, j->p, sigma, limits, j->sampler);
         table_flags(sc, j->h_pairs, &j->np_full, &j->cb_full, &j->og_full);
         table_flags(sc, j->h_pairs_s, &j->np_samp, &j->cb_samp, &j->og_samp);
+        if (order == 2 && create && !j->h_pairs_s.empty()) {
+            // the census scans the sampled table in gap order; then both orders, and the
+            // sampled table again (reachable_pairs keeps the order it is given)
+            const auto t0 = std::chrono::steady_clock::now();
+            int rc = upload_pairs_sync(j);
+            if (rc) return rc;
+            std::vector<uint64_t> hits;
+            if ((rc = run_census(j, kCensus, hits))) return rc;
+            waypoints_from_census(hits, kCensus, j->W, kThroughputG1, wps);
+            const std::vector<int> pick(wps.begin(), wps.begin() + std::min<size_t>(wps.size(), kThroughputG1));
+            pairs_by_hits(sc, j->h_pairs, j->h_knots.data(), j->nknots, j->p, init_ctrl, j->D, sigma, limits, j->W,
+                          pick);
+            j->h_pairs_s = reachable_pairs(sc, j->h_pairs, init_ctrl, j->n, j->D, j->p, sigma, limits, j->sampler);
+            table_flags(sc, j->h_pairs, &j->np_full, &j->cb_full, &j->og_full);
+            table_flags(sc, j->h_pairs_s, &j->np_samp, &j->cb_samp, &j->og_samp);
+            j->prepass_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
     }
     j->pair_order = order;
     if (create) {
@@ -640,13 +731,7 @@ static int set_job_tables(sspp_job* j, const double* init_ctrl, double sigma, co
     }
     if (!sc || sc->pairs.empty()) return SSPP_OK;
     const size_t bytes = sizeof(DPair) * j->h_pairs.size(), bytes_s = sizeof(DPair) * j->h_pairs_s.size();
-    if (create) {
-        if (!j->d_pairs) HIPCHK(hipMalloc((void**)&j->d_pairs, sizeof(DPair) * std::max<size_t>(1, sc->pairs.size())));
-        if (!j->d_pairs_s) HIPCHK(hipMalloc((void**)&j->d_pairs_s, sizeof(DPair) * std::max<size_t>(1, sc->pairs.size())));
-        HIPCHK(hipMemcpy(j->d_pairs, j->h_pairs.data(), bytes, hipMemcpyHostToDevice));
-        if (bytes_s) HIPCHK(hipMemcpy(j->d_pairs_s, j->h_pairs_s.data(), bytes_s, hipMemcpyHostToDevice));
-        return SSPP_OK;
-    }
+    if (create) return upload_pairs_sync(j);
     if (pin_off + bytes + bytes_s > j->h_pin_bytes) return sspp::set_error(SSPP_E_NOMEM, "pair staging too small");
     hipStream_t st = (hipStream_t)stream;
     unsigned char* pa = j->h_pin + pin_off;
