@@ -1264,18 +1264,24 @@ __global__ __launch_bounds__(NT, (NT == 64 && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU :
             const int grp = gp > 1 ? lt / stride : 0;   // wave-uniform: stride is a multiple of 64
             const int it = lt - grp * stride;
             const unsigned long long gmask = gp > 1 ? gsel << grp : ~0ull;
+            // waypoint-major items: item it = (waypoint jj of the order) x ns + survivor si, so a
+            // pass holds the most telling remaining waypoints of every survivor (an infeasible
+            // survivor is usually decided in the first pass; later passes then skip it)
             bool live = it < items;
-            const int si = live ? it / R : 0;
+            const int jj = live ? it / ns : 0;
+            const int si = live ? it - jj * ns : 0;
             const int s = s_surv[si];
-            const int j = j0 + (live ? it - si * R : 0);
+            const int j = j0 + jj;
             live = live && __hip_atomic_load(s_feas + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+            // a pass whose survivors have all been decided costs nothing (no spline / pose work)
+            if (__ballot(live) == 0ull) continue;
             // lanes of this wave that work on the same survivor
-            const int wave_it0 = base + (tid & ~63) - grp * stride;
-            int lo = si * R - wave_it0, hi = (si + 1) * R - wave_it0;
-            lo = lo < 0 ? 0 : lo;
-            hi = hi > 64 ? 64 : hi;
             unsigned long long gb = 0ull;
-            if (it < items && hi > lo) gb = (hi - lo >= 64) ? ~0ull : (((1ull << (hi - lo)) - 1ull) << lo);
+            for (int q = 0; q < ns; ++q) {  // wave-uniform
+                const unsigned long long m = __ballot(it < items && si == q);
+                if (si == q) gb = m;
+            }
+            if (it >= items) gb = 0ull;
             double q[D];
             eval_split_g<D, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], q);
             bool dfr = false;
