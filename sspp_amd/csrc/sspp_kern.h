@@ -1071,6 +1071,9 @@ __device__ SSPP_CB_INLINE bool c2f_cb_exact(const double* sm, int mine, int fix,
 #ifndef SSPP_C2F_WAVES_PER_EU_WIDE
 #define SSPP_C2F_WAVES_PER_EU_WIDE 4
 #endif
+// Workgroups of up to 128 threads run at SSPP_C2F_WAVES_PER_EU (96 VGPRs, no spill); the 256-thread
+// latency shape carries the phase-2 pair groups (few survivor items over many lanes), which
+// cost registers (at 5 waves per SIMD they spill), and runs at SSPP_C2F_WAVES_PER_EU_WIDE.
 // profiling builds only (tools/build_variant.sh -DSSPP_ABLATE=mask): 1 no sampling, 2 no
 // collision, 4 no arc, 8 no phase 2, 16 no phase 1, 64 return at entry (launch cost only)
 #ifndef SSPP_ABLATE
@@ -1079,7 +1082,7 @@ __device__ SSPP_CB_INLINE bool c2f_cb_exact(const double* sm, int mine, int fix,
 // CBX: the pair table has cylinder-box pairs, so the kernel carries the settle step (its
 // out-of-line exact test costs the whole kernel registers: 96 -> 128 VGPRs and scratch)
 template <int D, int NM, int P, bool ONEGEOM, int NT, bool CBX>
-__global__ __launch_bounds__(NT, (NT == 64 && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU : SSPP_C2F_WAVES_PER_EU_WIDE) void k_sspp_c2f(
+__global__ __launch_bounds__(NT, (NT <= 128 && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU : SSPP_C2F_WAVES_PER_EU_WIDE) void k_sspp_c2f(
     SsppC2F a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
     const double* __restrict__ atab, const int* __restrict__ aspan,
     const double* __restrict__ init_ctrl, const double* __restrict__ limits,
@@ -1264,7 +1267,7 @@ __global__ __launch_bounds__(NT, (NT == 64 && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU :
         // scanning the pairs k = g (mod gp).  A contact in any group clears the survivor's flag,
         // which stops the others; the result is the same OR over (waypoint, pair).
         int gp = 1, stride = items;
-        if (np <= 64 && items > 0) {
+        if (NT == 256 && np <= 64 && items > 0) {
             const int s64 = (items + 63) & ~63;
             while (gp < 8 && s64 * gp * 2 <= NT) gp *= 2;
             if (gp > 1) stride = s64;
@@ -2094,11 +2097,12 @@ hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o,
     return hipGetLastError();
 }
 
-// two workgroup sizes: one-wave workgroups (throughput shapes) and 4-wave workgroups (a single
-// plan() batch, latency shape); DESIGN.md §5
+// three workgroup sizes: one- and two-wave workgroups (throughput shapes) and 4-wave workgroups
+// (a single plan() batch, latency shape); DESIGN.md §5
 template <int D, int NM, int P>
 hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
     if (k.nt == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
+    if (k.nt == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st);
     return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
 }
 

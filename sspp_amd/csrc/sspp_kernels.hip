@@ -955,8 +955,8 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
     if (!j) return sspp::set_error(SSPP_E_INVAL, "null job");
     switch (key) {
         case SSPP_OPT_SHAPE_NT:
-            if (j->kind != 0 || !(value == 0 || value == 64 || value == 256))
-                return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SHAPE_NT: 0, 64 or 256");
+            if (j->kind != 0 || !(value == 0 || value == 64 || value == 128 || value == 256))
+                return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SHAPE_NT: 0, 64, 128 or 256");
             j->opt_nt = (int)value;
             return SSPP_OK;
         case SSPP_OPT_SHAPE_G1:
