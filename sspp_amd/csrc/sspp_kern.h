@@ -1082,7 +1082,13 @@ __device__ SSPP_CB_INLINE bool c2f_cb_exact(const double* sm, int mine, int fix,
 // CBX: the pair table has cylinder-box pairs, so the kernel carries the settle step (its
 // out-of-line exact test costs the whole kernel registers: 96 -> 128 VGPRs and scratch)
 template <int D, int NM, int P, bool ONEGEOM, int NT, bool CBX>
-__global__ __launch_bounds__(NT, (NT <= 128 && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU : SSPP_C2F_WAVES_PER_EU_WIDE) void k_sspp_c2f(
+#ifndef SSPP_C2F_FIVE_MAX  // profiling builds: the largest workgroup at SSPP_C2F_WAVES_PER_EU
+#define SSPP_C2F_FIVE_MAX 128
+#endif
+#ifndef SSPP_C2F_GP_NT     // profiling builds: the workgroup size that carries the pair groups
+#define SSPP_C2F_GP_NT 256
+#endif
+__global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU : SSPP_C2F_WAVES_PER_EU_WIDE) void k_sspp_c2f(
     SsppC2F a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
     const double* __restrict__ atab, const int* __restrict__ aspan,
     const double* __restrict__ init_ctrl, const double* __restrict__ limits,
@@ -1267,7 +1273,7 @@ __global__ __launch_bounds__(NT, (NT <= 128 && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU 
         // scanning the pairs k = g (mod gp).  A contact in any group clears the survivor's flag,
         // which stops the others; the result is the same OR over (waypoint, pair).
         int gp = 1, stride = items;
-        if (NT == 256 && np <= 64 && items > 0) {
+        if (NT == SSPP_C2F_GP_NT && np <= 64 && items > 0) {
             const int s64 = (items + 63) & ~63;
             while (gp < 8 && s64 * gp * 2 <= NT) gp *= 2;
             if (gp > 1) stride = s64;

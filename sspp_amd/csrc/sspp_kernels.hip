@@ -645,8 +645,9 @@ static int upload_basis(const std::vector<double>& us, int p, const double* knot
     return upload(d_span, sp.data(), sp.size());
 }
 
-// phase-1 lanes per candidate of the throughput shape (one-wave workgroups)
-constexpr int kThroughputG1 = 4;
+// the throughput shape: 2-wave workgroups of 32 candidates x 4 phase-1 lanes (DESIGN.md §5:
+// against one-wave workgroups of 16, a survivor's remaining waypoints spread over 128 lanes)
+constexpr int kThroughputNT = 128, kThroughputG1 = 4;
 
 // The job's scan orders for its initial spline / sigma / limits: the pair table ordered by the
 // mean-path gap (pairs_for_job), refined with the collision-waypoint order by the hit-order
@@ -805,13 +806,13 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
 
 // k_sspp_c2f launch shape (NT threads, G1 phase-1 lanes per candidate, 64 / G1 candidates per
 // wave), measured on MI355X: launches of many candidates are throughput-bound ->
-// one-wave workgroups of 16 candidates x 4 lanes; a launch of a few thousand (one plan() batch)
+// 2-wave workgroups of 32 candidates x 4 lanes; a launch of a few thousand (one plan() batch)
 // is latency-bound -> 4-wave workgroups of 4 candidates x 64 lanes: a whole wave per candidate in
 // phase 1, a survivor's remaining waypoints over 256 lanes in phase 2.  Forced shapes
 // (sspp_job_set_option) are for tests and tuning.
 static void c2f_shape(const sspp_job* j, int64_t cands, int* nt, int* g1) {
     const bool lat = cands < 16384;
-    *nt = j->opt_nt ? j->opt_nt : (lat ? 256 : 64);
+    *nt = j->opt_nt ? j->opt_nt : (lat ? 256 : kThroughputNT);
     *g1 = j->opt_g1 ? j->opt_g1 : (lat ? 64 : kThroughputG1);
 }
 
@@ -1158,7 +1159,7 @@ extern "C" int sspp_job_tsp_score_vias(sspp_job* j, const double* d_vias, int64_
 extern "C" int sspp_job_info(const sspp_job* j, int* lpc, int* cpb_out, int* threads, size_t* lds) {
     if (!j) return sspp::set_error(SSPP_E_INVAL, "null job");
     if (j->kind == 0) {  // the last k_sspp_c2f launch's shape (before any launch: the throughput shape)
-        const int nt = j->last_nt ? j->last_nt : 64, g1 = j->last_g1 ? j->last_g1 : kThroughputG1;
+        const int nt = j->last_nt ? j->last_nt : kThroughputNT, g1 = j->last_g1 ? j->last_g1 : kThroughputG1;
         const int cpb = (nt / 64) * (64 / g1);
         if (lpc) *lpc = g1;
         if (cpb_out) *cpb_out = cpb;

@@ -60,7 +60,7 @@ def run_sspp(job, B, first=0, with_ctrl=True):
 # the job option SSPP_OPT_SHAPE_NT / _G1; (0, 0) = the shape the library picks per launch
 # (256 x 64 below 16384 candidates per launch, 64 x 4 above).  Every shape must give the
 # oracle's results.
-SHAPES = [(0, 0), (64, 4), (64, 3), (64, 8), (64, 16), (64, 64), (256, 64), (256, 16)]
+SHAPES = [(0, 0), (128, 4), (64, 4), (64, 3), (64, 8), (64, 16), (64, 64), (256, 64), (256, 16)]
 
 
 def set_shape(job, nt, g1):
@@ -425,7 +425,7 @@ def test_multistep_launch_matches_oracle(robocrane, sigma, spl):
     for rep in range(2):
         ex.enqueue(G, first + rep * G * stride, stride, best)
         torch.cuda.synchronize()
-        assert job.config()["shape"] == "64x4"
+        assert job.config()["shape"] == "128x4"
         arc, fe, got = arcs[0].cpu().numpy(), feas[0].cpu().numpy(), best.cpu()
         for i in (0, 7, G - 1):
             f0 = first + (rep * G + i) * stride
