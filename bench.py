@@ -69,6 +69,9 @@ def parse(argv=None):
                     help="robocrane sampleWithNoise normals: fp64 Box-Muller (default, bit-exact "
                          "oracle) or the opt-in fp32 quad sampler")
     ap.add_argument("--budgets-ms", default="10,20,50", help="tsp-anytime: wall-clock budgets")
+    ap.add_argument("--tsp-form", type=int, default=None,
+                    help="stacking: force the k_tsp form (SSPP_OPT_TSP_FORM 0..3; tuning, every form "
+                         "gives bit-identical results)")
     ap.add_argument("--shape", default="",
                     help="robocrane: force the k_sspp_c2f launch shape NTxG1 (e.g. 64x4; tuning, "
                          "default: chosen per launch by the library); the line reports it")
@@ -161,6 +164,9 @@ def setup_stacking(args, device):
     B = args.batch or 16384
     jobs = [S.TspJob(scene, start, end, K, cp, mean=mean, sigma=sigma, lo=lo, hi=hi, z_min=0.0,
                      max_batch=B) for _ in range(args.streams)]
+    if args.tsp_form is not None:
+        for j in jobs:
+            j.set_option(S.OPT_TSP_FORM, args.tsp_form)
     bufs = [j.alloc(B, device=device) for j in jobs]
     job = jobs[0]
 
@@ -178,8 +184,11 @@ def setup_stacking(args, device):
     flops_per = (2 * cp + 1) * 2 * 3 * D + cp * (3 * D + 1) + cp * (40 + 42 + 48 + 2 * 450)
     meta = dict(workload="stacking.xml TaskSpacePlanner (block1), K=1 via, sigma 0.2",
                 candidates_per_gpu=B, waypoints=cp, vias=K, degree=2, dof=4)
+    # the k_tsp form of the timed launches (SSPP_OPT_TSP_FORM read-back: 0 inline narrowphase,
+    # 3 deferred box-box contact polygons, ...)
     ctx = dict(kind="tsp", job=job, start=start, end=end, mean=mean, sigma=sigma, lo=lo, hi=hi,
-               cp=cp, scene_path=model.path, body=model.body_id("block1"))
+               cp=cp, scene_path=model.path, body=model.body_id("block1"),
+               effective=lambda: dict(tsp_form=int(job.get_option(S.OPT_TSP_FORM))))
     return B, step, kernel_only, bytes_per, flops_per, meta, ctx
 
 

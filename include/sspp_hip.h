@@ -208,7 +208,7 @@ void sspp_job_free(sspp_job* job);
 /* Explicit job options (tests and tuning; the library reads no environment variables).
  * Nothing here changes a result: every option selects among bit-identical evaluation orders or
  * kernel forms.  sspp_job_get_option also reads back the effective configuration.          */
-#define SSPP_OPT_SHAPE_NT 1     /* k_sspp_c2f threads per workgroup: 64 or 256; 0 = per launch  */
+#define SSPP_OPT_SHAPE_NT 1     /* k_sspp_c2f threads per workgroup: 64, 128 or 256; 0 = per launch */
 #define SSPP_OPT_SHAPE_G1 2     /* phase-1 lanes per candidate 1..64; 0 = per launch            */
 #define SSPP_OPT_ORDER 3        /* scan order: 0 scene / bisection, 1 mean-path gap (pairs),
                                    2 hit order (waypoints + pairs, host pre-pass; the default of

@@ -1221,7 +1221,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             if (tid == 0) s_surv[cpb] = __popcll(m);
         }
         __syncthreads();
-        const int ns = s_surv[cpb];
+        int ns = s_surv[cpb];
         if (tid == 0) C2F_STAT(6, ns);
 #ifdef SSPP_WG_TIMING
         wg_ns = ns;
@@ -1265,53 +1265,78 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             if (tid < ns) s_mask[s_surv[tid]] = ~0ull;
             __syncthreads();
         }
-        unsigned long long umask = 0ull;
-        for (int i = 0; i < ns; ++i) umask |= s_mask[s_surv[i]];
-        const int items = ns * R;
-        // Few items for many lanes (a single-step launch's 4-wave workgroup with one survivor):
-        // gp pair groups, each a 64-aligned copy of the item range on its own waves, group g
-        // scanning the pairs k = g (mod gp).  A contact in any group clears the survivor's flag,
-        // which stops the others; the result is the same OR over (waypoint, pair).
-        int gp = 1, stride = items;
-        if (NT == SSPP_C2F_GP_NT && np <= 64 && items > 0) {
-            const int s64 = (items + 63) & ~63;
-            while (gp < 8 && s64 * gp * 2 <= NT) gp *= 2;
-            if (gp > 1) stride = s64;
-        }
-        const unsigned long long gsel = gp == 2 ? 0x5555555555555555ull
-                                      : gp == 4 ? 0x1111111111111111ull
-                                      : gp == 8 ? 0x0101010101010101ull : ~0ull;
-        const int total = gp > 1 ? stride * gp : items;
-        for (int base = 0; base < total; base += NT) {  // workgroup-uniform trip count
-            const int lt = base + tid;
-            const int grp = gp > 1 ? lt / stride : 0;   // wave-uniform: stride is a multiple of 64
-            const int it = lt - grp * stride;
-            const unsigned long long gmask = gp > 1 ? gsel << grp : ~0ull;
-            // waypoint-major items: item it = (waypoint jj of the order) x ns + survivor si, so a
-            // pass holds the most telling remaining waypoints of every survivor (an infeasible
-            // survivor is usually decided in the first pass; later passes then skip it)
-            bool live = it < items;
-            const int jj = live ? it / ns : 0;
-            const int si = live ? it - jj * ns : 0;
-            const int s = s_surv[si];
-            const int j = j0 + jj;
-            live = live && __hip_atomic_load(s_feas + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-            // a pass whose survivors have all been decided costs nothing (no spline / pose work)
-            if (__ballot(live) == 0ull) continue;
-            // lanes of this wave that work on the same survivor
-            unsigned long long gb = 0ull;
-            for (int q = 0; q < ns; ++q) {  // wave-uniform
-                const unsigned long long m = __ballot(it < items && si == q);
-                if (si == q) gb = m;
+        // Rounds: each round gives every live survivor the next cnt waypoints of the order
+        // (cnt = NT / live survivors, so a round is one pass of the workgroup), then drops the
+        // survivors it decided.  An infeasible survivor is usually decided by its first waypoints,
+        // so the feasible ones then get the whole workgroup instead of a share of lanes that
+        // idle on decided candidates.
+        for (int jb = 0;;) {  // workgroup-uniform
+            if (jb > 0) {
+                __syncthreads();  // this round's flag updates are visible
+                if (tid < 64) {   // in-place compaction by one wave (reads precede the writes)
+                    const int s = tid < ns ? s_surv[tid] : 0;
+                    const bool f = tid < ns && s_feas[s] != 0;
+                    const unsigned long long m = __ballot(f);
+                    if (f) s_surv[__popcll(m & ((1ull << tid) - 1ull))] = s;
+                    if (tid == 0) s_surv[cpb] = __popcll(m);
+                }
+                __syncthreads();
+                ns = __builtin_amdgcn_readfirstlane(s_surv[cpb]);
             }
-            if (it >= items) gb = 0ull;
-            double q[D];
-            eval_split_g<D, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], q);
-            bool dfr = false;
-            const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s] & gmask, umask & gmask, gb, s_feas + s,
-                                                      a.sc, TT, dfr);
-            if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (ns == 0) break;
+            const int cnt = min(R - jb, max(1, NT / ns));
+            unsigned long long um = 0ull;
+            for (int i = 0; i < ns; ++i) um |= s_mask[s_surv[i]];
+            const unsigned long long umask =  // workgroup-uniform: scalar registers
+                ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(um >> 32)) << 32) |
+                (unsigned)__builtin_amdgcn_readfirstlane((int)um);
+            const int items = ns * cnt;
+            // Few items for many lanes (a single-step launch's 4-wave workgroup with one survivor):
+            // gp pair groups, each a 64-aligned copy of the item range on its own waves, group g
+            // scanning the pairs k = g (mod gp).  A contact in any group clears the survivor's flag,
+            // which stops the others; the result is the same OR over (waypoint, pair).
+            int gp = 1, stride = items;
+            if (NT == SSPP_C2F_GP_NT && np <= 64 && items > 0) {
+                const int s64 = (items + 63) & ~63;
+                while (gp < 8 && s64 * gp * 2 <= NT) gp *= 2;
+                if (gp > 1) stride = s64;
+            }
+            const unsigned long long gsel = gp == 2 ? 0x5555555555555555ull
+                                          : gp == 4 ? 0x1111111111111111ull
+                                          : gp == 8 ? 0x0101010101010101ull : ~0ull;
+            // one pass: items <= NT (cnt <= NT / ns), and with pair groups stride * gp <= NT
+            {
+                const int grp = gp > 1 ? tid / stride : 0;   // wave-uniform: stride is a multiple of 64
+                const int it = tid - grp * stride;
+                const unsigned long long gmask = gp > 1 ? gsel << grp : ~0ull;
+                // waypoint-major items: item it = (waypoint jj of the round) x ns + survivor si, so
+                // a pass holds the most telling remaining waypoints of every survivor
+                bool live = it < items;
+                const int jj = live ? it / ns : 0;
+                const int si = live ? it - jj * ns : 0;
+                const int s = s_surv[si];
+                const int j = j0 + jb + jj;
+                live = live && __hip_atomic_load(s_feas + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+                // a wave whose survivors have all been decided skips the spline / pose work
+                if (__ballot(live) != 0ull) {
+                    // lanes of this wave that work on the same survivor
+                    unsigned long long gb = 0ull;
+                    for (int q = 0; q < ns; ++q) {  // wave-uniform
+                        const unsigned long long m = __ballot(it < items && si == q);
+                        if (si == q) gb = m;
+                    }
+                    if (it >= items) gb = 0ull;
+                    double q[D];
+                    eval_split_g<D, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], q);
+                    bool dfr = false;
+                    const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s] & gmask, umask & gmask, gb,
+                                                              s_feas + s, a.sc, TT, dfr);
+                    if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            jb += cnt;
+            if (jb >= R) break;
         }
     }
     WG_PH(4);

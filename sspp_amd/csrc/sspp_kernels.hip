@@ -649,12 +649,6 @@ static int upload_basis(const std::vector<double>& us, int p, const double* knot
 // against one-wave workgroups of 16, a survivor's remaining waypoints spread over 128 lanes)
 constexpr int kThroughputNT = 128, kThroughputG1 = 4;
 
-// The job's scan orders for its initial spline / sigma / limits: the pair table ordered by the
-// mean-path gap (pairs_for_job), refined with the collision-waypoint order by the hit-order
-// pre-pass (order 2: sampled jobs at creation), and its sample-mode subset (reachable_pairs).
-// create: the waypoint order and both tables are (re)uploaded synchronously; otherwise the pair
-// tables are queued on `stream` from the pinned staging at byte offset `pin_off` (the caller
-// sized it for both) and the waypoint order stays.
 // both pair tables to the device, synchronously (job creation, option changes)
 static int upload_pairs_sync(sspp_job* j) {
     const sspp_scene* sc = j->scene;
@@ -692,6 +686,12 @@ static int run_census(sspp_job* j, int M, std::vector<uint64_t>& hits) {
     return SSPP_OK;
 }
 
+// The job's scan orders for its initial spline / sigma / limits: the pair table ordered by the
+// mean-path gap (pairs_for_job), refined with the collision-waypoint order by the hit-order
+// pre-pass (order 2: sampled jobs at creation), and its sample-mode subset (reachable_pairs).
+// create: the waypoint order and both tables are (re)uploaded synchronously; otherwise the pair
+// tables are queued on `stream` from the pinned staging at byte offset `pin_off` (the caller
+// sized it for both) and the waypoint order stays.
 static int set_job_tables(sspp_job* j, const double* init_ctrl, double sigma, const double* limits, int order,
                           bool create, void* stream, size_t pin_off = 0) {
     const sspp_scene* sc = j->scene;

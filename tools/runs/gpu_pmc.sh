@@ -23,5 +23,6 @@ for c in $CFGS; do
   run $c/p1 "$F64" $A
   run $c/occ/p1 "$OCC" $A
   run $c/occ/p2 MeanOccupancyPerCU $A
+  run $c/util "VALUUtilization SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU" $A
 done
 echo DONE
