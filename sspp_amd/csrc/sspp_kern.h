@@ -187,6 +187,41 @@ __device__ __forceinline__ unsigned long long hull_mask(const double* ctrl, int 
     return mask;
 }
 
+// Wave-level broadphase (k_tsp: one waypoint per lane, a wave holds consecutive waypoints of one
+// candidate, a single mover whose position is q[0..2]).  The AABB of the mover positions the
+// wave's lanes evaluate — the points themselves, exact — takes the place of the control points'
+// hull in pair_may_touch: a pair it rejects is one pair_near rejects at every lane of the wave,
+// so skipping it adds nothing to any lane's sum (bit-identical), and along a path the 64
+// consecutive waypoints of a wave span a fraction of the candidate's hull.  Every lane of the
+// wave calls it (shuffles); `has`: the lane evaluates a waypoint.
+__device__ __forceinline__ unsigned long long wave_pair_mask(const double* p, bool has, int npairs,
+                                                             cpair_t pairs, cgeom_t geoms) {
+    double lo[3], hi[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        lo[d] = has ? p[d] : INFINITY;
+        hi[d] = has ? p[d] : -INFINITY;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = fmin(lo[d], __shfl_xor(lo[d], off, 64));
+            hi[d] = fmax(hi[d], __shfl_xor(hi[d], off, 64));
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    bool act = false;
+    if (lane < npairs && lo[0] <= hi[0]) {
+        const DPair pr = load_pair(pairs + lane);
+        const DGeom G = load_geom(geoms + pr.gm);
+        act = pair_may_touch(pr, G, lo, hi);
+    }
+    unsigned long long mask = __ballot(act);
+    if (npairs > 64) mask = ~0ull;
+    return mask;
+}
+
 struct BlockBest {
     double cost;
     long long idx;
@@ -1599,6 +1634,7 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
     double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
     BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
+    static_assert(NM == 1, "k_tsp: one yaw-only mover (wave_pair_mask reads its position from q[0..2])");
     constexpr int D = 4, P = 2, P1 = 3;
     const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, cp = a.cp;
     const int slot = tid / lpc, lane = tid - slot * lpc;
@@ -1698,10 +1734,17 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
             aW = aW + (c + fp);
         }
     } else if (valid) {
-        for (int j = lane; j < cp; j += lpc) {
-            const int i = j + 1;
+        // wave-uniform trip count: lpc is a multiple of 64, so a wave holds one candidate
+        for (int j0 = 0; j0 < cp; j0 += lpc) {
+            const int j = j0 + lane;
+            const bool on = j < cp;
+            const int i = (on ? j : cp - 1) + 1;
             double pv[4], pc[4];
             eval_pt<D, P>(myc, tab + i * P1, span[i], pc);
+            // several moving geoms (the gripper's 7, 48 pairs): the wave-level cull pays for its
+            // reductions; a single geom's few pairs are near along most of the path anyway
+            const unsigned long long wmask =
+                ONEGEOM ? ~0ull : wave_pair_mask(pc, on, a.sc.npairs, (cpair_t)T.pairs, (cgeom_t)T.geoms);
             if (one_pass) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pc[d], 1, 64);
@@ -1709,15 +1752,17 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
             } else {
                 eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
             }
-            aL = aL + dist_nd<D>(pv, pc);
-            double c = 0.0;
+            if (on) {
+                aL = aL + dist_nd<D>(pv, pc);
+                double c = 0.0;
 #ifndef SSPP_PROF_NOCOLL  // profiling variant only
-            point_collide<D, NM, 1, true, ONEGEOM, CB, 0, UP>(pc, a.sc, T, mask, &c);
+                point_collide<D, NM, 1, true, ONEGEOM, CB, 0, UP>(pc, a.sc, T, mask & wmask, &c);
 #endif
-            const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
-            const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
-            aC = aC + c;
-            aW = aW + (c + fp);
+                const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
+                const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
+                aC = aC + c;
+                aW = aW + (c + fp);
+            }
         }
     }
     aL = wave_sum(aL);

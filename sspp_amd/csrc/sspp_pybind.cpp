@@ -281,7 +281,9 @@ private:
         if (planner_) return;
         if (!scene_) {
             sspp_scene* s = nullptr;
-            ck(sspp_scene_create(model_.get(), SSPP_MODE_QPOS, N, 0, &s), "scene");
+            // count_static = 1: checkCollision's ncon is the whole scene's (include/sspp.h:143-144,
+            // Q7), static-static contacts included
+            ck(sspp_scene_create(model_.get(), SSPP_MODE_QPOS, N, 1, &s), "scene");
             scene_.reset(s);
         }
         sspp_planner* p = nullptr;

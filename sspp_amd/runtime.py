@@ -136,9 +136,12 @@ class Model:
 
 
 class Scene:
-    """Model bound to its moving set, with device-resident geom/pair tables."""
+    """Model bound to its moving set, with device-resident geom/pair tables.  count_static: the
+    SamplingPathPlanner feasibility counts the scene's static-static contacts too (the
+    reference's whole-scene ncon, include/sspp.h:143-144; Q7); False ignores them.  The
+    TaskSpacePlanner cost always includes them (Collision.h:89-101)."""
 
-    def __init__(self, model, mode, arg, count_static=False):
+    def __init__(self, model, mode, arg, count_static=True):
         if isinstance(arg, str):
             arg = model.body_id(arg)
         h = C.c_void_p()

@@ -194,3 +194,24 @@ def test_plan_sspp_c_abi_cached(cuda):
                 assert best.index == -1
         del scene  # sspp_scene_free drops the cached planner of this scene
     assert nfeas > 0
+
+
+def test_static_contacts_count_like_the_reference(sp):
+    """checkCollision's ncon is the whole scene's (include/sspp.h:143-144): in
+    stacking.xml block2 and block3 rest on the floor (MuJoCo's plane-box collider counts a
+    corner at distance 0), so every candidate of a planner moving block1 is in collision, as in
+    the reference; the robocrane scene has no static contact, so its results do not change."""
+    stacking = os.path.join(SCENES, "stacking.xml")
+    osc = O.Scene(mjcf_ref.load(stacking), 0, 7)
+    q = np.array([0.2, 0.0, 0.4, 1.0, 0.0, 0.0, 0.0])  # block1 lifted clear of everything
+    assert osc.contacts(q)[0] == 0 and osc.contacts(q, count_static=True)[0] == 8
+    planner = sp.SamplingPathPlanner7(stacking)
+    start = q
+    end = np.array([0.0, 0.2, 0.4, 1.0, 0.0, 0.0, 0.0])
+    ok, paths = planner.plan(start, end, 0.01, np.ones(7), sample_count=256, check_points=32,
+                             init_points=10)
+    assert not ok and len(paths) == 0
+    init = sp.Spline7()
+    assert planner.initializePath(start, end, init, 10)
+    arc, feas = O.sspp_score(osc, init.knots(), 3, init.ctrls().T.copy()[None], 32, count_static=True)
+    assert not feas.any()
