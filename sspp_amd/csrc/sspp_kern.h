@@ -187,41 +187,6 @@ __device__ __forceinline__ unsigned long long hull_mask(const double* ctrl, int 
     return mask;
 }
 
-// Wave-level broadphase (k_tsp: one waypoint per lane, a wave holds consecutive waypoints of one
-// candidate, a single mover whose position is q[0..2]).  The AABB of the mover positions the
-// wave's lanes evaluate — the points themselves, exact — takes the place of the control points'
-// hull in pair_may_touch: a pair it rejects is one pair_near rejects at every lane of the wave,
-// so skipping it adds nothing to any lane's sum (bit-identical), and along a path the 64
-// consecutive waypoints of a wave span a fraction of the candidate's hull.  Every lane of the
-// wave calls it (shuffles); `has`: the lane evaluates a waypoint.
-__device__ __forceinline__ unsigned long long wave_pair_mask(const double* p, bool has, int npairs,
-                                                             cpair_t pairs, cgeom_t geoms) {
-    double lo[3], hi[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        lo[d] = has ? p[d] : INFINITY;
-        hi[d] = has ? p[d] : -INFINITY;
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            lo[d] = fmin(lo[d], __shfl_xor(lo[d], off, 64));
-            hi[d] = fmax(hi[d], __shfl_xor(hi[d], off, 64));
-        }
-    }
-    const int lane = threadIdx.x & 63;
-    bool act = false;
-    if (lane < npairs && lo[0] <= hi[0]) {
-        const DPair pr = load_pair(pairs + lane);
-        const DGeom G = load_geom(geoms + pr.gm);
-        act = pair_may_touch(pr, G, lo, hi);
-    }
-    unsigned long long mask = __ballot(act);
-    if (npairs > 64) mask = ~0ull;
-    return mask;
-}
-
 struct BlockBest {
     double cost;
     long long idx;
@@ -974,6 +939,7 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
             have_rot = false;
         }
         int nc = 0;
+        bool nr = false;
         if (live && (k >= 64 || ((mymask >> k) & 1ull))) {
             double op_[3], om_[9];
             const double* op = pr.opos;
@@ -988,8 +954,7 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
                 matmul3(R, pr.omat, om_);
                 op = op_; om = om_;
             }
-            const bool nr = pair_near(pr, G.rbound, gp, op, om);
-            C2F_STAT(2, __popcll(__ballot(nr)));
+            nr = pair_near(pr, G.rbound, gp, op, om);
             if (nr) {
                 if (!ONEGEOM && !have_rot) {
                     const bool second = NM > 1 && G.mover == 1;
@@ -1003,6 +968,8 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
                 if (nc < 0) { dfr = true; nc = 0; }
             }
         }
+        C2F_STAT(2, __popcll(__ballot(nr)));                // lanes past the sphere test (narrowphase)
+        C2F_STAT(flag ? 10 : 9, __ballot(nr) != 0ull);      // wave iterations running a narrowphase
         C2F_STAT(flag ? 4 : 0, 1);                          // wave pair iterations (phase 2 / 1)
         C2F_STAT(flag ? 5 : 1, __popcll(__ballot(live && (k >= 64 || ((mymask >> k) & 1ull)))));
         if (__ballot(nc > 0) & gbits) { ghit = true; live = false; }
@@ -1611,8 +1578,10 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
 
 // CB: the scene has cylinder-box pairs (without them the exact cylinder-box code is compiled
 // out: it costs registers even when it never runs)
-#ifndef SSPP_TSP_WAVES_PER_EU_MG  // several moving geoms (their per-geom poses stay live)
-#define SSPP_TSP_WAVES_PER_EU_MG 2
+// Several moving geoms (the gripper's 7): 3 waves per SIMD, 168 VGPRs with ~50 spilled, beats
+// 2 waves without spills (multi-goal 40.6 against 34.6 M cand/s; 4 waves: 29.8)
+#ifndef SSPP_TSP_WAVES_PER_EU_MG
+#define SSPP_TSP_WAVES_PER_EU_MG 3
 #endif
 // DEF (one waypoint per lane, at most kDefPairs pairs): box-box contact polygons deferred — the
 // waypoint loop records every pair's count / term (REC 3), the workgroup then counts the
@@ -1634,7 +1603,6 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
     double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
     BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    static_assert(NM == 1, "k_tsp: one yaw-only mover (wave_pair_mask reads its position from q[0..2])");
     constexpr int D = 4, P = 2, P1 = 3;
     const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, cp = a.cp;
     const int slot = tid / lpc, lane = tid - slot * lpc;
@@ -1734,17 +1702,10 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
             aW = aW + (c + fp);
         }
     } else if (valid) {
-        // wave-uniform trip count: lpc is a multiple of 64, so a wave holds one candidate
-        for (int j0 = 0; j0 < cp; j0 += lpc) {
-            const int j = j0 + lane;
-            const bool on = j < cp;
-            const int i = (on ? j : cp - 1) + 1;
+        for (int j = lane; j < cp; j += lpc) {
+            const int i = j + 1;
             double pv[4], pc[4];
             eval_pt<D, P>(myc, tab + i * P1, span[i], pc);
-            // several moving geoms (the gripper's 7, 48 pairs): the wave-level cull pays for its
-            // reductions; a single geom's few pairs are near along most of the path anyway
-            const unsigned long long wmask =
-                ONEGEOM ? ~0ull : wave_pair_mask(pc, on, a.sc.npairs, (cpair_t)T.pairs, (cgeom_t)T.geoms);
             if (one_pass) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pc[d], 1, 64);
@@ -1752,17 +1713,15 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
             } else {
                 eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
             }
-            if (on) {
-                aL = aL + dist_nd<D>(pv, pc);
-                double c = 0.0;
+            aL = aL + dist_nd<D>(pv, pc);
+            double c = 0.0;
 #ifndef SSPP_PROF_NOCOLL  // profiling variant only
-                point_collide<D, NM, 1, true, ONEGEOM, CB, 0, UP>(pc, a.sc, T, mask & wmask, &c);
+            point_collide<D, NM, 1, true, ONEGEOM, CB, 0, UP>(pc, a.sc, T, mask, &c);
 #endif
-                const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
-                const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
-                aC = aC + c;
-                aW = aW + (c + fp);
-            }
+            const double deficit = (a.floor_z_min + a.floor_margin) - pc[2];
+            const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
+            aC = aC + c;
+            aW = aW + (c + fp);
         }
     }
     aL = wave_sum(aL);

@@ -58,7 +58,7 @@ def run_sspp(job, B, first=0, with_ctrl=True):
 
 # k_sspp_c2f launch shapes (threads per workgroup, phase-1 lanes per candidate), forced through
 # the job option SSPP_OPT_SHAPE_NT / _G1; (0, 0) = the shape the library picks per launch
-# (256 x 64 below 16384 candidates per launch, 64 x 4 above).  Every shape must give the
+# (256 x 64 below 16384 candidates per launch, 128 x 4 above).  Every shape must give the
 # oracle's results.
 SHAPES = [(0, 0), (128, 4), (64, 4), (64, 3), (64, 8), (64, 16), (64, 64), (256, 64), (256, 16)]
 
