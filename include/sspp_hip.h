@@ -215,8 +215,9 @@ void sspp_job_free(sspp_job* job);
                                    sampled jobs, sigma > 0); setting it rebuilds the tables
                                    (synchronous)                                               */
 #define SSPP_OPT_TSP_FORM 4     /* TaskSpacePlanner: -1 by batch size, 0 k_tsp, 1 k_tsp_pp,
-                                   2 k_tsp_pp2, 3 k_tsp with deferred box-box polygons (where
-                                   they apply); get: the last launch's form                   */
+                                   2 k_tsp_pp2, 3 k_tsp with box-box polygons deferred to the
+                                   workgroup (<= 8 pairs), 4 deferred to the end of each lane's
+                                   pair loop (<= 64 pairs); get: the last launch's form        */
 #define SSPP_OPT_TSP_GENERIC 5  /* TaskSpacePlanner: 1 = generic box-box / cylinder-box code even
                                    where every pair is upright                                 */
 #define SSPP_OPT_SAMPLER 6      /* get: the job's sampler (sspp_sspp_args::sampler)             */

@@ -582,18 +582,21 @@ __device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const doub
 // is counted later by the workgroup over its compacted deferred pairs (bb_clip_count(_up)) —
 // and rec_term[k] its cost term; rec_pose receives the mover pose (position, the five non-zero
 // entries of the yaw rotation) those later counts recompute the geom poses from.
+// REC 4 (k_tsp<..., DEF 2>): the records of REC 3 without the terms — the lane itself sums its
+// records after the pair loop (tsp_lane_sum), recomputing each term from the recorded pose.
 constexpr int kBbPend = 16;
 template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, int CB = 1, int REC = 0, bool UP = false>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                              unsigned long long mask, double* cost, int* stop = nullptr,
                              void* rec_nd = nullptr, double* rec_term = nullptr, double* rec_pose = nullptr) {
-    static_assert(REC != 3 || (DEEP && MODE == 1 && NM == 1), "deferred box-box polygons: yaw-only single mover");
+    static_assert(REC < 3 || (DEEP && MODE == 1 && NM == 1), "deferred box-box polygons: yaw-only single mover");
+    constexpr bool RECD = REC == 3 || REC == 4;  // records with deferred box-box polygons
     static_assert(!ONEGEOM || NM == 1, "single moving geom implies a single mover");
     const cgeom_t geoms = (cgeom_t)T.geoms;
     const cpair_t pairs = (cpair_t)T.pairs;
     double mp[NM][3], mR[NM][9];
     mover_poses<D, NM, MODE>(q, (cmover_t)T.movers, mp, mR);
-    if (REC == 3) {
+    if (RECD) {
         rec_pose[0] = mp[0][0]; rec_pose[1] = mp[0][1]; rec_pose[2] = mp[0][2];
         rec_pose[3] = mR[0][0]; rec_pose[4] = mR[0][1]; rec_pose[5] = mR[0][3]; rec_pose[6] = mR[0][4];
         rec_pose[7] = mR[0][8];
@@ -649,7 +652,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                 have_rot = true;
             }
             const bool gfirst = (G.type < pr.otype) || (G.type == pr.otype && G.orig < pr.oorig);
-            if (REC == 3 && G.type == 6 && pr.otype == 6) {
+            if (RECD && G.type == 6 && pr.otype == 6) {
                 // box-box: the SAT decision now, the contact polygon later (collide's DEEP path
                 // runs box_box_deep_count(_up) unconditionally: margin >= 0 > kDeep)
                 const int c = gfirst ? (UP ? box_box_deep_class_up(gp, gmat, G.size, op, om, pr.osize)
@@ -663,13 +666,13 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                 nc = collide<DEEP, CB, DEEP, false, UP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
             }
         }
-        if (REC == 3) ((unsigned char*)rec_nd)[k] = (unsigned char)nd;
+        if (RECD) ((unsigned char*)rec_nd)[k] = (unsigned char)nd;
         if (!DEEP) {
             // the loop trip is wave-uniform, so every active lane reaches this vote
             if (__ballot(nc > 0) != 0ull) return 1;
             if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
                 return 1;
-        } else if (nd > 0) {
+        } else if (REC != 4 && nd > 0) {
             const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
             const double cd = sqrt(dot3(dc, dc));
             const double term = -1.0 / (cd + 1e-4);
@@ -689,6 +692,53 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
     }
     if (DEEP && REC == 0) *cost = acc + sc.static_cost;
     return 0;
+}
+
+// A deep box-box pair's contact polygon (bb_clip_count(_up), reference face fi) for the moving geom
+// G at the mover pose `ps` (position, the five non-zero entries of the yaw rotation: REC 3/4's
+// record) against the static partner of pair pr; the operand order of collide's box-box call.
+template <bool UP>
+__device__ __forceinline__ int tsp_clip(const double* ps, const DGeom& G, const DPair& pr, int fi) {
+    const double mp0[3] = {ps[0], ps[1], ps[2]};
+    const double mR0[9] = {ps[3], ps[4], 0.0, ps[5], ps[6], 0.0, 0.0, 0.0, ps[7]};
+    double gp[3], gm[9];
+    geom_pos_t<true>(mp0, mR0, G, gp);
+    geom_rot_t<true>(mR0, G, gm);
+    const bool gfirst = G.orig < pr.oorig;  // both boxes
+    return gfirst ? (UP ? bb_clip_count_up(gp, gm, G.size, pr.opos, pr.omat, pr.osize, fi)
+                        : bb_clip_count(gp, gm, G.size, pr.opos, pr.omat, pr.osize, fi))
+                  : (UP ? bb_clip_count_up(pr.opos, pr.omat, pr.osize, gp, gm, G.size, fi)
+                        : bb_clip_count(pr.opos, pr.omat, pr.osize, gp, gm, G.size, fi));
+}
+
+// REC 4's sum, after the pair loop: the lane's records in pair order, each deep pair adding
+// its term -1/(centre distance + 1e-4) nd times — point_collide's additions in its order, so the
+// cost is bit-identical — with a deferred polygon counted here (tsp_clip), where the pair loop's
+// state is dead: the polygon's registers no longer add to the loop's.  The trip over the pairs is
+// wave-uniform; a pair no lane of the wave recorded costs one ballot.
+template <bool UP>
+__device__ __forceinline__ double tsp_lane_sum(bool has, const unsigned char* rn, const double* ps, int np,
+                                               const KScene& sc, const SceneT& T) {
+    const cgeom_t geoms = (cgeom_t)T.geoms;
+    const cpair_t pairs = (cpair_t)T.pairs;
+    double acc = 0.0;
+    for (int k = 0; k < np; ++k) {
+        const int nd0 = has ? rn[k] : 0;
+        if (__ballot(nd0 != 0) == 0ull) continue;
+        const DPair pr = load_pair(pairs + k);
+        const DGeom G = load_geom(geoms + pr.gm);
+        if (nd0 != 0) {
+            const int nd = nd0 >= kBbPend ? tsp_clip<UP>(ps, G, pr, nd0 - kBbPend) : nd0;
+            const double mp0[3] = {ps[0], ps[1], ps[2]};
+            const double mR0[9] = {ps[3], ps[4], 0.0, ps[5], ps[6], 0.0, 0.0, 0.0, ps[7]};
+            double gp[3];
+            geom_pos_t<true>(mp0, mR0, G, gp);
+            const double dc[3] = {pr.opos[0] - gp[0], pr.opos[1] - gp[1], pr.opos[2] - gp[2]};
+            const double term = -1.0 / (sqrt(dot3(dc, dc)) + 1e-4);
+            for (int r = 0; r < nd; ++r) acc = acc + term;
+        }
+    }
+    return acc + sc.static_cost;
 }
 
 // ---------------------------------------------------------------- batch argmin helpers
@@ -1589,9 +1639,10 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
 // wave that happen to hold one), and each lane sums its records in pair order: the same additions
 // in the same order as the inline form, so the costs are bit-identical.
 constexpr int kDefPairs = 8;
-// 5 waves per SIMD (96 VGPRs, ~75 spilled) beat 4 without spills: stacking 101.6 -> 106.0 M cand/s
+// 4 waves per SIMD, no spills.  5 waves (96 VGPRs, ~75 spilled) measured 106.0 against 101.6 M
+// cand/s on stacking, but its spills raised the HBM traffic from 1.4x to 140x the algorithmic bytes
 #ifndef SSPP_TSP_WAVES_PER_EU_DEF
-#define SSPP_TSP_WAVES_PER_EU_DEF 5
+#define SSPP_TSP_WAVES_PER_EU_DEF 4
 #endif
 template <int NM, bool ONEGEOM, int CB, bool UP = false, int DEF = 0>
 __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
@@ -1614,10 +1665,11 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
     double* s_wsum = s_ctrl + cpb * ndof;    // [3][4]
     double* s_best = s_wsum + 3 * (kBlock / 64);
     int* s_stat = (int*)(s_best + 4);        // [cpb]
-    // DEF 1: per-lane records [kBlock][np] (terms, counts), mover poses [kBlock][8], deferred list
-    const int npr = DEF == 1 ? a.sc.npairs : 0;
+    // DEF 1: per-lane records [kBlock][np] (terms, counts), mover poses [kBlock][8], deferred list;
+    // DEF 2: per-lane counts [kBlock][np] and mover poses only
+    const int npr = DEF ? a.sc.npairs : 0;
     double* s_rterm = (double*)(s_stat + ((cpb + 1) & ~1));
-    double* s_rpose = s_rterm + kBlock * npr;
+    double* s_rpose = s_rterm + (DEF == 1 ? kBlock * npr : 0);
     unsigned char* s_rnd = (unsigned char*)(s_rpose + (DEF ? kBlock * 8 : 0));
     int* s_items = (int*)(s_rnd + ((kBlock * npr + 3) & ~3));
     int* s_nitems = s_items + kBlock * npr;
@@ -1699,6 +1751,30 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
                 for (int r = 0; r < nd; ++r) acc = acc + term;
             }
             const double c = acc + a.sc.static_cost;
+            const double deficit = (a.floor_z_min + a.floor_margin) - pz;
+            const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
+            aC = aC + c;
+            aW = aW + (c + fp);
+        }
+    } else if (DEF == 2) {  // host-checked: one waypoint per lane (cp <= lpc), np <= 64, NM == 1
+        unsigned char* rn = s_rnd + tid * npr;
+        double* ps = s_rpose + tid * 8;
+        for (int k = 0; k < npr; ++k) rn[k] = 0;
+        const bool has = valid && lane < cp;
+        double pz = 0.0;
+        if (has) {
+            const int i = lane + 1;
+            double pv[4], pc[4];
+            eval_pt<D, P>(myc, tab + i * P1, span[i], pc);
+#pragma unroll
+            for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pc[d], 1, 64);
+            if ((tid & 63) == 0) eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
+            aL = aL + dist_nd<D>(pv, pc);
+            pz = pc[2];
+            point_collide<D, NM, 1, true, ONEGEOM, CB, 4, UP>(pc, a.sc, T, mask, nullptr, nullptr, rn, nullptr, ps);
+        }
+        const double c = tsp_lane_sum<UP>(has, rn, ps, npr, a.sc, T);  // every lane: wave ballots
+        if (has) {
             const double deficit = (a.floor_z_min + a.floor_margin) - pz;
             const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
             aC = aC + c;
@@ -1975,6 +2051,11 @@ inline size_t tsp_def_lds(int np) {
            sizeof(int) * ((size_t)kBlock * np + 1) + 16;
 }
 
+// extra LDS of k_tsp<..., DEF 2>: per-lane counts and mover poses
+inline size_t tsp_def2_lds(int np) {
+    return sizeof(double) * (size_t)kBlock * 8 + (((size_t)kBlock * np + 7) & ~(size_t)7) + 16;
+}
+
 inline int lanes_for(int items) {
     int l = ((items + 63) / 64) * 64;
     return std::min(std::max(l, 64), kBlock);
@@ -2239,9 +2320,10 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
     const bool og = k.sc.onegeom && k.sc.npairs > 0;
     const int cbm = k.sc.cylbox ? (k.sc.cbup ? 2 : 1) : 0;
     const bool up = k.sc.upright && cbm != 1;
-    // pp == 3: the deferred-polygon form (host-checked: one waypoint per lane, <= kDefPairs pairs)
-    const int def = pp == 3 ? 1 : 0;
-    const size_t lds = def ? j->lds + tsp_def_lds(k.sc.npairs) : j->lds;
+    // pp == 3: the deferred-polygon form (host-checked: one waypoint per lane, <= kDefPairs pairs);
+    // pp == 4: the lane-local deferred polygons (one waypoint per lane, <= 64 pairs)
+    const int def = pp == 3 ? 1 : (pp == 4 ? 2 : 0);
+    const size_t lds = def == 1 ? j->lds + tsp_def_lds(k.sc.npairs) : (def == 2 ? j->lds + tsp_def2_lds(k.sc.npairs) : j->lds);
 #define SSPP_LAUNCH_TSP_ALL(DEFV)                                                                         \
     if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false, DEFV);                                            \
     else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true, DEFV); else SSPP_LAUNCH_TSP(true, 2, false, DEFV); } \
@@ -2252,6 +2334,7 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
     else if (up) SSPP_LAUNCH_TSP(false, 0, true, DEFV);                                                   \
     else SSPP_LAUNCH_TSP(false, 0, false, DEFV);
     if (def == 1) { SSPP_LAUNCH_TSP_ALL(1) }
+    else if (def == 2) { SSPP_LAUNCH_TSP_ALL(2) }
     else { SSPP_LAUNCH_TSP_ALL(0) }
 #undef SSPP_LAUNCH_TSP_ALL
 #undef SSPP_LAUNCH_TSP

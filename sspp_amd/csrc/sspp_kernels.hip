@@ -972,7 +972,7 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
             return set_job_tables(j, j->h_stage.data(), j->sigma, j->h_stage.data() + nd, (int)value, true, nullptr);
         }
         case SSPP_OPT_TSP_FORM:
-            if (j->kind != 1 || value < -1 || value > 3) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_FORM: -1..3");
+            if (j->kind != 1 || value < -1 || value > 4) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_FORM: -1..4");
             j->tsp_form = (int)value;
             return SSPP_OK;
         case SSPP_OPT_TSP_GENERIC:
@@ -1117,6 +1117,11 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     const bool def_ok = j->cp <= j->lpc && k.sc.npairs >= 1 && k.sc.npairs <= kDefPairs && has_bb &&
                         j->lds + tsp_def_lds(k.sc.npairs) <= 64 * 1024;
     if (mode == 0 && def_ok && (pp_opt < 0 || pp_opt == 3)) mode = 3;
+    // the lane-local deferred polygons (mode 4): one waypoint per lane, up to 64 pairs, some of them
+    // box-box; the default where mode 3 does not apply (the gripper's 48 pairs)
+    const bool def2_ok = j->cp <= j->lpc && k.sc.npairs >= 1 && k.sc.npairs <= 64 && has_bb &&
+                         j->lds + tsp_def2_lds(k.sc.npairs) <= 64 * 1024;
+    if (mode == 0 && def2_ok && (pp_opt < 0 || pp_opt == 4)) mode = 4;
     const int nblk = mode == 2 ? (int)B * npg : mode == 1 ? (int)B : (int)((B + j->cpb - 1) / j->cpb);
     j->last_form = mode;
     hipStream_t st = (hipStream_t)stream;

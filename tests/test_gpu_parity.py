@@ -615,9 +615,11 @@ def test_gripper_tsp_matches_oracle(cuda, goal):
                                            ("robocrane.xml", "gripper_collision_with_block/", 300, 64),
                                            ("stacking.xml", "block1", 200, 48)])
 def test_tsp_kernel_forms_identical(cuda, xml, body, B, cp):
-    """k_tsp, the single-workgroup pair split (k_tsp_pp) and the multi-workgroup split (k_tsp_pp2,
-    48 gripper pairs over 6 workgroups per candidate) give bit-identical per-candidate results and
-    argmin records, and match the oracle."""
+    """k_tsp, the single-workgroup pair split (k_tsp_pp), the multi-workgroup split (k_tsp_pp2,
+    48 gripper pairs over 6 workgroups per candidate) and the two deferred-polygon forms of k_tsp
+    (3: compacted per workgroup, <= 8 pairs; 4: summed per lane after its pair loop, the gripper's
+    48 pairs) give bit-identical per-candidate results and argmin records, and match the oracle.
+    A form that does not apply to a scene runs k_tsp (the read-back says which ran)."""
     import torch
     import sspp_amd as S
     path = os.path.join(SCENES, xml)
@@ -636,14 +638,14 @@ def test_tsp_kernel_forms_identical(cuda, xml, body, B, cp):
     job = S.TspJob(scene, start, end, 1, cp, mean=mean, sigma=sigma, lo=np.array(lo), hi=np.array(hi),
                    z_min=0.0, max_batch=B)
     res = {}
-    for mode in ("0", "1", "2", "3"):
+    for mode in ("0", "1", "2", "3", "4"):
         job.set_option(S.OPT_TSP_FORM, int(mode))
         q = job.alloc(B, device="cuda", with_vias=True)
         job.sample_score(0, B, q["L"], q["Cnf"], q["Cwf"], q["status"], q["cost"], q["best"],
                          vias_out=q["vias"])
         torch.cuda.synchronize()
         res[mode] = {k: v.cpu().numpy() for k, v in q.items()}
-    for mode in ("1", "2", "3"):
+    for mode in ("1", "2", "3", "4"):
         for k in ("L", "Cnf", "Cwf", "cost", "status", "vias", "best"):
             np.testing.assert_array_equal(res[mode][k], res["0"][k], err_msg="%s %s" % (mode, k))
     osc = O.Scene(mjcf_ref.load(path), 1, bid)

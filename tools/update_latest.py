@@ -96,6 +96,11 @@ def main(src, prefix):
         occ2 = rows(os.path.join(d, "occ", "p2"), kern)
         if occ2:
             res["mean_occupancy_per_cu"] = per_launch(occ2, {r["Counter_Name"] for r in occ2}).get("MeanOccupancyPerCU")
+        ut = rows(os.path.join(d, "util"), kern)
+        if ut:  # share of the 64 lanes active per VALU instruction (derived VALUUtilization, %)
+            u = per_launch(ut, {r["Counter_Name"] for r in ut})
+            res["valu_utilization_pct"] = u.get("VALUUtilization")
+            res["valu_thread_cycles"] = u.get("SQ_THREAD_CYCLES_VALU")
         json.dump(res, open("%s_%s_pmc.json" % (prefix, cfg), "w"), indent=1, sort_keys=True)
         print(cfg, json.dumps(res, sort_keys=True)[:600])
     json.dump(traffic, open(tf, "w"), indent=1)
