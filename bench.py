@@ -75,10 +75,11 @@ def parse(argv=None):
     ap.add_argument("--shape", default="",
                     help="robocrane: force the k_sspp_c2f launch shape NTxG1 (e.g. 64x4; tuning, "
                          "default: chosen per launch by the library); the line reports it")
-    ap.add_argument("--chunk", type=int, default=64)
-    ap.add_argument("--steps-per-launch", type=int, default=32,
+    ap.add_argument("--chunk", type=int, default=80, help="native mode: steps per executor call")
+    ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="native mode: independent steps (each its own B candidates, outputs and "
-                         "argmin) grouped into one kernel launch")
+                         "argmin) grouped into one kernel launch; 40 x 4096 candidates = 5120 "
+                         "workgroups of 128 x 4 = two resident rounds of the chip")
     a = ap.parse_args(argv)
     if a.steps is None and a.mode == "tsp-anytime":
         a.steps = 10  # trials per budget and mode

@@ -14,8 +14,8 @@ run() { local d=$1 grp=$2; shift 2; mkdir -p $O/$d
     || { echo "PMC $d FAILED"; tail -5 $O/$d.log; exit 1; }; echo "ok $d"; }
 for c in $CFGS; do
   case $c in
-    robocrane) A="--steps 64 --warmup 4 --roofline-launches 20";;
-    robocrane_b32768_w256) A="--batch 32768 --waypoints 256 --steps 64 --warmup 4 --roofline-launches 10";;
+    robocrane) A="--steps 80 --warmup 4 --roofline-launches 20";;
+    robocrane_b32768_w256) A="--batch 32768 --waypoints 256 --steps 80 --warmup 4 --roofline-launches 10";;
     *) A="--config $c --steps 4 --warmup 1 --roofline-launches 20";;
   esac
   run $c/pmc_fetch FETCH_SIZE $A

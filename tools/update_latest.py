@@ -17,12 +17,12 @@ from bench import KERNEL_REV  # noqa: E402  (records of another kernel revision 
 # record keys: the bench config, or config_b<batch>_w<waypoints> off the default shape
 KERNEL = {"robocrane": "k_sspp_c2f", "stacking": "k_tsp", "multigoal": "k_tsp",
           "robocrane_b32768_w256": "k_sspp_c2f"}
-PER_LAUNCH = {"robocrane": 32 * 4096, "stacking": 16384, "multigoal": 4098,
-              "robocrane_b32768_w256": 32 * 32768}
-STEPS = {"robocrane": "--steps 64 --warmup 4 (32 steps x 4096 candidates per launch)",
+PER_LAUNCH = {"robocrane": 40 * 4096, "stacking": 16384, "multigoal": 4098,
+              "robocrane_b32768_w256": 40 * 32768}
+STEPS = {"robocrane": "--steps 80 --warmup 4 (40 steps x 4096 candidates per launch)",
          "stacking": "--config stacking --steps 4 --warmup 1",
          "multigoal": "--config multigoal --steps 4 --warmup 1",
-         "robocrane_b32768_w256": "--batch 32768 --waypoints 256 --steps 64 --warmup 4 (config-4 shard)"}
+         "robocrane_b32768_w256": "--batch 32768 --waypoints 256 --steps 80 --warmup 4 (config-4 shard)"}
 
 
 def rows(path, kern):
