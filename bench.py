@@ -90,6 +90,13 @@ def parse(argv=None):
     return a
 
 
+def roofline_spl(args):
+    """Steps per launch of the roofline launches: the timed loop's launch shape, i.e. the
+    executor's steps per launch, or all the timed steps when they are fewer (the driver's
+    --steps 20 run is one launch of 20 steps)."""
+    return min(args.steps, args.steps_per_launch) if args.mode == "native" else 1
+
+
 def setup_robocrane(args, device):
     import sspp_amd as S
     model = S.Model(os.path.join(S.SCENE_DIR, "robocrane.xml"))
@@ -120,7 +127,7 @@ def setup_robocrane(args, device):
         # one launch exactly as the timed loop issues it: steps_per_launch steps of B
         # candidates (each with its own outputs and argmin record), on the current stream
         import torch
-        spl = args.steps_per_launch if args.mode == "native" else 1
+        spl = roofline_spl(args)
         if spl == 1:
             job.sample_score(first_id, B, bufs[0]["arc"], bufs[0]["feasible"], None)
             return
@@ -148,7 +155,7 @@ def setup_robocrane(args, device):
     ctx = dict(kind="sspp", kernel_name="k_sspp_c2f", effective=job.config,
                job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p,
                make_executor=make_executor,
-               per_launch=B * (args.steps_per_launch if args.mode == "native" else 1))
+               per_launch=B * roofline_spl(args))
     return B, step, kernel_only, bytes_per, flops_per, meta, ctx
 
 
@@ -773,6 +780,8 @@ def main(argv=None):
     # default shape, and used only for launches of the recorded kernel and size
     pmc_key = args.config if (args.waypoints == 128 and not args.batch) else \
         "%s_b%d_w%d" % (args.config, B, args.waypoints)
+    if args.config == "robocrane" and args.mode == "native" and roofline_spl(args) != 40:
+        pmc_key += "_spl%d" % roofline_spl(args)  # records of another launch shape
     traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", "traffic_latest.json")
     if os.path.exists(tf):

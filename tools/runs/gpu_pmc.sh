@@ -5,7 +5,7 @@
 #   gpurun --timeout 1100 -- bash tools/runs/gpu_pmc.sh TAG [configs...]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; TAG=${1:-pmc}; shift; O=$R/gpurun_out/$TAG; mkdir -p $O
-CFGS=${@:-robocrane robocrane_b32768_w256 stacking multigoal}
+CFGS=${@:-robocrane robocrane_spl20 robocrane_b32768_w256 stacking multigoal}
 cd /tmp && export TMPDIR=/tmp
 F64="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY"
 OCC="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE"
@@ -15,6 +15,7 @@ run() { local d=$1 grp=$2; shift 2; mkdir -p $O/$d
 for c in $CFGS; do
   case $c in
     robocrane) A="--steps 80 --warmup 4 --roofline-launches 20";;
+    robocrane_spl20) A="--steps 20 --warmup 5 --roofline-launches 20";;
     robocrane_b32768_w256) A="--batch 32768 --waypoints 256 --steps 80 --warmup 4 --roofline-launches 10";;
     *) A="--config $c --steps 4 --warmup 1 --roofline-launches 20";;
   esac

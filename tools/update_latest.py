@@ -16,13 +16,14 @@ from bench import KERNEL_REV  # noqa: E402  (records of another kernel revision 
 
 # record keys: the bench config, or config_b<batch>_w<waypoints> off the default shape
 KERNEL = {"robocrane": "k_sspp_c2f", "stacking": "k_tsp", "multigoal": "k_tsp",
-          "robocrane_b32768_w256": "k_sspp_c2f"}
+          "robocrane_b32768_w256": "k_sspp_c2f", "robocrane_spl20": "k_sspp_c2f"}
 PER_LAUNCH = {"robocrane": 40 * 4096, "stacking": 16384, "multigoal": 4098,
-              "robocrane_b32768_w256": 40 * 32768}
+              "robocrane_b32768_w256": 40 * 32768, "robocrane_spl20": 20 * 4096}
 STEPS = {"robocrane": "--steps 80 --warmup 4 (40 steps x 4096 candidates per launch)",
          "stacking": "--config stacking --steps 4 --warmup 1",
          "multigoal": "--config multigoal --steps 4 --warmup 1",
-         "robocrane_b32768_w256": "--batch 32768 --waypoints 256 --steps 80 --warmup 4 (config-4 shard)"}
+         "robocrane_b32768_w256": "--batch 32768 --waypoints 256 --steps 80 --warmup 4 (config-4 shard)",
+         "robocrane_spl20": "--steps 20 --warmup 5 (the driver's run: one launch of 20 steps x 4096)"}
 
 
 def rows(path, kern):
