@@ -72,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--tsp-form", type=int, default=None,
                     help="stacking: force the k_tsp form (SSPP_OPT_TSP_FORM 0..3; tuning, every form "
                          "gives bit-identical results)")
+    ap.add_argument("--mg-chunk", type=int, default=1,
+                    help="multigoal: iterations per goal before the next goal's (0: all of a goal's "
+                         "iterations in one call)")
     ap.add_argument("--shape", default="",
                     help="robocrane: force the k_sspp_c2f launch shape NTxG1 (e.g. 64x4; tuning, "
                          "default: chosen per launch by the library); the line reports it")
@@ -230,10 +233,22 @@ def setup_multigoal(args, device, world, rank):
     started = [False] * len(pls)
 
     def run_steps(k):
-        for i, (g, pl) in enumerate(zip(mine, pls)):
-            st, en = MULTIGOAL[g]
-            pl.plan(st, en, iterate=started[i], iterations=k, stream=streams[i])
-            started[i] = True
+        if args.mg_chunk <= 0:  # every goal's k iterations in one call per goal
+            for i, (g, pl) in enumerate(zip(mine, pls)):
+                st, en = MULTIGOAL[g]
+                pl.plan(st, en, iterate=started[i], iterations=k, stream=streams[i])
+                started[i] = True
+            return
+        # the goals take turns, mg_chunk iterations each: every hardware queue then holds work of
+        # several goals, so one goal's small CES kernels overlap another goal's evaluation
+        done = 0
+        while done < k:
+            c = min(args.mg_chunk, k - done)
+            for i, (g, pl) in enumerate(zip(mine, pls)):
+                st, en = MULTIGOAL[g]
+                pl.plan(st, en, iterate=started[i], iterations=c, stream=streams[i])
+                started[i] = True
+            done += c
 
     def kernel_only(first_id):
         pls[0].eval(rank=0, stream=torch.cuda.current_stream())
