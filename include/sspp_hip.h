@@ -340,6 +340,16 @@ int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void* const* str
                             int nsteps, int steps_per_launch, int64_t first_id,
                             int64_t step_stride, double* const* d_arc, uint8_t* const* d_feasible,
                             sspp_best* d_best);
+/* The same executor as a handle (a planning loop's per-call arguments are only the steps):
+ * sspp_steps_create_sspp checks and copies the branches once; sspp_steps_run(ex, nsteps, first_id,
+ * step_stride, d_best) enqueues like sspp_steps_enqueue_sspp; the jobs, streams and buffers must
+ * outlive the handle.                                                                      */
+typedef struct sspp_steps sspp_steps;
+int sspp_steps_create_sspp(sspp_job* const* jobs, int nbranch, void* const* streams, int64_t B,
+                           int steps_per_launch, double* const* d_arc, uint8_t* const* d_feasible,
+                           sspp_steps** out);
+int sspp_steps_run(sspp_steps* ex, int nsteps, int64_t first_id, int64_t step_stride, sspp_best* d_best);
+void sspp_steps_free(sspp_steps* ex);
 
 /* ---- multi-GPU helpers: reduce gathered per-rank results (lowest cost, lowest id) ---- */
 int sspp_best_reduce(const sspp_best* parts, int n, sspp_best* out);          /* host */

@@ -124,6 +124,10 @@ SIGNATURES = {
     "sspp_best_reduce_steps": (C.c_int, [_vp, _i, _i, _vp, _vp]),
     "sspp_steps_enqueue_sspp": (C.c_int, [C.POINTER(_vp), _i, C.POINTER(_vp), _i64, _i, _i,
                                           _i64, _i64, C.POINTER(_vp), C.POINTER(_vp), _vp]),
+    "sspp_steps_create_sspp": (C.c_int, [C.POINTER(_vp), _i, C.POINTER(_vp), _i64, _i, C.POINTER(_vp),
+                                         C.POINTER(_vp), C.POINTER(_vp)]),
+    "sspp_steps_run": (C.c_int, [_vp, _i, _i64, _i64, _vp]),
+    "sspp_steps_free": (None, [_vp]),
     "sspp_plan_sspp": (C.c_int, [_vp, _i, _d, _d, C.c_double, _d, _i, _i, _i, C.c_uint64, _d, _d,
                                  C.POINTER(C.c_uint8), _d, C.POINTER(Best)]),
     "sspp_score_ctrl_host": (C.c_int, [_vp, _d, _i, _d, _i64, _i, _i, _i, _d,

@@ -1246,21 +1246,24 @@ __global__ __launch_bounds__(64) void k_argmin_steps(const BlockBest* __restrict
 }
 }  // namespace
 
-extern "C" int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void* const* streams,
-                                       int64_t B, int nsteps, int steps_per_launch, int64_t first_id,
-                                       int64_t step_stride, double* const* d_arc,
-                                       uint8_t* const* d_feasible, sspp_best* d_best) {
-    sspp::clear_error();
-    if (!jobs || !streams || !d_arc || !d_feasible || nbranch < 1 || nsteps < 0 || B < 1)
-        return sspp::set_error(SSPP_E_INVAL, "sspp_steps_enqueue_sspp: bad argument");
+static int steps_check(sspp_job* const* jobs, int nbranch, void* const* streams, int64_t B, int steps_per_launch,
+                       double* const* d_arc, uint8_t* const* d_feasible) {
+    if (!jobs || !streams || !d_arc || !d_feasible || nbranch < 1 || B < 1)
+        return sspp::set_error(SSPP_E_INVAL, "sspp steps: bad argument");
     for (int b = 0; b < nbranch; ++b) {
         if (!jobs[b] || jobs[b]->kind != 0 || !d_arc[b] || !d_feasible[b])
-            return sspp::set_error(SSPP_E_INVAL, "sspp_steps_enqueue_sspp: bad branch");
+            return sspp::set_error(SSPP_E_INVAL, "sspp steps: bad branch");
         for (int c = 0; c < b; ++c)
             if (jobs[c] == jobs[b]) return sspp::set_error(SSPP_E_INVAL, "branches need distinct jobs");
     }
-    const int S = steps_per_launch;
-    if (S < 1 || S > kMaxSteps) return sspp::set_error(SSPP_E_INVAL, "steps_per_launch must be in [1, 64]");
+    if (steps_per_launch < 1 || steps_per_launch > kMaxSteps)
+        return sspp::set_error(SSPP_E_INVAL, "steps_per_launch must be in [1, 64]");
+    return SSPP_OK;
+}
+
+static int steps_run(sspp_job* const* jobs, int nbranch, void* const* streams, int64_t B, int S, int nsteps,
+                     int64_t first_id, int64_t step_stride, double* const* d_arc, uint8_t* const* d_feasible,
+                     sspp_best* d_best) {
     for (int i = 0, l = 0; i < nsteps; i += S, ++l) {
         const int b = l % nbranch, s = std::min(S, nsteps - i);
         const int rc = run_sspp(jobs[b], nullptr, first_id + (int64_t)i * step_stride, B, d_arc[b],
@@ -1270,6 +1273,58 @@ extern "C" int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void*
     }
     return SSPP_OK;
 }
+
+extern "C" int sspp_steps_enqueue_sspp(sspp_job* const* jobs, int nbranch, void* const* streams,
+                                       int64_t B, int nsteps, int steps_per_launch, int64_t first_id,
+                                       int64_t step_stride, double* const* d_arc,
+                                       uint8_t* const* d_feasible, sspp_best* d_best) {
+    sspp::clear_error();
+    int rc = steps_check(jobs, nbranch, streams, B, steps_per_launch, d_arc, d_feasible);
+    if (rc) return rc;
+    if (nsteps < 0) return sspp::set_error(SSPP_E_INVAL, "sspp_steps_enqueue_sspp: nsteps < 0");
+    return steps_run(jobs, nbranch, streams, B, steps_per_launch, nsteps, first_id, step_stride, d_arc,
+                     d_feasible, d_best);
+}
+
+// the same executor as a handle: its branches checked and copied once, then each call passes only
+// the steps to run (a planning loop's per-call host work: one small argument list)
+struct sspp_steps {
+    std::vector<sspp_job*> jobs;
+    std::vector<void*> streams;
+    std::vector<double*> arc;
+    std::vector<uint8_t*> feas;
+    int64_t B = 0;
+    int spl = 1;
+};
+
+extern "C" int sspp_steps_create_sspp(sspp_job* const* jobs, int nbranch, void* const* streams, int64_t B,
+                                      int steps_per_launch, double* const* d_arc, uint8_t* const* d_feasible,
+                                      sspp_steps** out) {
+    sspp::clear_error();
+    if (!out) return sspp::set_error(SSPP_E_INVAL, "sspp_steps_create_sspp: null output");
+    int rc = steps_check(jobs, nbranch, streams, B, steps_per_launch, d_arc, d_feasible);
+    if (rc) return rc;
+    auto* ex = new sspp_steps();
+    ex->jobs.assign(jobs, jobs + nbranch);
+    ex->streams.assign(streams, streams + nbranch);
+    ex->arc.assign(d_arc, d_arc + nbranch);
+    ex->feas.assign(d_feasible, d_feasible + nbranch);
+    ex->B = B;
+    ex->spl = steps_per_launch;
+    *out = ex;
+    return SSPP_OK;
+}
+
+extern "C" int sspp_steps_run(sspp_steps* ex, int nsteps, int64_t first_id, int64_t step_stride, sspp_best* d_best) {
+    if (!ex || nsteps < 0) {
+        sspp::clear_error();
+        return sspp::set_error(SSPP_E_INVAL, "sspp_steps_run: bad argument");
+    }
+    return steps_run(ex->jobs.data(), (int)ex->jobs.size(), ex->streams.data(), ex->B, ex->spl, nsteps, first_id,
+                     step_stride, ex->arc.data(), ex->feas.data(), d_best);
+}
+
+extern "C" void sspp_steps_free(sspp_steps* ex) { delete ex; }
 
 extern "C" int sspp_best_reduce_steps(const sspp_best* d_parts, int R, int G, sspp_best* d_out,
                                       void* stream) {

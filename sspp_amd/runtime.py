@@ -334,14 +334,26 @@ class SsppSteps:
         self._A = (C.c_void_p * nb)(*[_ptr(a).value for a in arc_bufs])
         self._F = (C.c_void_p * nb)(*[_ptr(f).value for f in feas_bufs])
         self.nb, self.B, self.spl = nb, int(B), int(steps_per_launch)
-        self._fn = lib().sspp_steps_enqueue_sspp
+        h = C.c_void_p()
+        check(lib().sspp_steps_create_sspp(self._J, nb, self._S, self.B, self.spl, self._A, self._F,
+                                           C.byref(h)), "steps create")
+        self._h = h
+        self._run = lib().sspp_steps_run
+        self._free = lib().sspp_steps_free
 
     def enqueue(self, nsteps, first_id, step_stride, best=None):
         """best: None, an (nsteps, 4) int64 device tensor for the per-step argmin records, or
         that tensor's device address as an int (callers in a timed loop cache it)."""
         bp = best if (best is None or isinstance(best, int)) else best.data_ptr()
-        check(self._fn(self._J, self.nb, self._S, self.B, nsteps, self.spl, first_id, step_stride,
-                       self._A, self._F, bp), "steps enqueue")
+        rc = self._run(self._h, nsteps, first_id, step_stride, bp)
+        if rc:
+            check(rc, "steps enqueue")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._free(h)
+            self._h = None
 
 
 class CesPlanner:
