@@ -950,8 +950,10 @@ __device__ __forceinline__ void eval_split_g(const double* sm, int mine, int fix
 
 // Pair loop of one waypoint per lane.  All 64 lanes run the (wave-uniform) loop; `live` lanes
 // test the pairs of their own mask.  gbits = the lanes of this lane's candidate within the
-// wave: when any of them touches, all of them stop (returns true for the group).  flag: the
-// candidate's LDS feasibility flag (phase 2), polled so lanes in other waves stop too.
+// wave: when any of them touches, all of them stop (returns true for the group).  flag: non-null
+// in phase 2 (work counters only).  Lanes of the same survivor in another wave are not stopped
+// inside a pass: polling the survivor's LDS flag at every pair measured slower (1128-1142 against
+// 1143-1152 M cand/s on the 20-step run), and the next round drops the decided survivors anyway.
 // A cylinder-box pair that passes the bounding-sphere test sets dfr (undecided) and counts as
 // no contact here (collide<..., DEFER>); the settle step decides it with the exact test.
 template <int D, int NM, bool ONEGEOM>
@@ -1023,8 +1025,6 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
         C2F_STAT(flag ? 4 : 0, 1);                          // wave pair iterations (phase 2 / 1)
         C2F_STAT(flag ? 5 : 1, __popcll(__ballot(live && (k >= 64 || ((mymask >> k) & 1ull)))));
         if (__ballot(nc > 0) & gbits) { ghit = true; live = false; }
-        if (flag && live && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-            live = false;
         if (__ballot(live) == 0ull) break;
     }
     return ghit;
