@@ -880,8 +880,8 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
 //            candidate's lanes leave the pair loop together at the first pair any of them
 //            touches (ballot over the candidate's lane group);
 //   phase 2  the survivors (few: the feasible ones plus the rare misses) are compacted in LDS
-//            and their remaining waypoints spread over all NT lanes; a lane group that finds
-//            a contact clears the candidate's LDS flag, which stops its other lanes;
+//            and their remaining waypoints spread over all NT lanes in rounds; a contact clears
+//            the candidate's LDS flag and the next round drops the candidate;
 //   settle   cylinder-box pairs the scans left undecided (collide<..., DEFER>) get the exact
 //            test, out of line, for the (rare) candidates that have no other contact;
 //   phase 3  arc length of the collision-free candidates, in the canonical reduction order of
