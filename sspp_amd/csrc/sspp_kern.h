@@ -1282,7 +1282,14 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         // then one (survivor, pair) test per thread (pair_may_touch; exact, see above).  Only
         // survivors: phase 1 stops at the first touching pair anyway, and computing the masks
         // for every candidate cost more than it saved (robocrane: 1.11 vs 1.22 G cand/s)
-        if (ns > 0 && np <= 64) {
+        // with 8 pairs or fewer the masks cull too little to pay for their two barriers and the
+        // hull pass: robocrane (4 pairs) kernel 54.9 -> 53.7 us at 20 steps, 79.9 -> 78.1 us at
+        // 1000 (profiles/r04aa_mask_ab.txt); the scan tests every pair exactly either way
+#ifndef SSPP_P2_MASK_MIN
+#define SSPP_P2_MASK_MIN 9
+#endif
+        const bool hull = np <= 64 && np >= SSPP_P2_MASK_MIN;  // otherwise every pair is scanned
+        if (ns > 0 && hull) {
             for (int e = tid; e < ns * NB; e += NT) {
                 const int si = e / NB, md = e - si * NB, m = md / 3, d = md - m * 3;
                 const int sl = s_surv[si], col = 7 * m + d;
@@ -1313,9 +1320,6 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                     atomicOr(s_mask + sl, 1ull << k);
             }
             __syncthreads();
-        } else if (ns > 0) {
-            if (tid < ns) s_mask[s_surv[tid]] = ~0ull;
-            __syncthreads();
         }
         // Rounds: each round gives every live survivor the next cnt waypoints of the order
         // (cnt = NT / live survivors, so a round is one pass of the workgroup), then drops the
@@ -1338,7 +1342,10 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             if (ns == 0) break;
             const int cnt = min(R - jb, max(1, NT / ns));
             unsigned long long um = 0ull;
-            for (int i = 0; i < ns; ++i) um |= s_mask[s_surv[i]];
+            if (hull)
+                for (int i = 0; i < ns; ++i) um |= s_mask[s_surv[i]];
+            else
+                um = ~0ull;
             const unsigned long long umask =  // workgroup-uniform: scalar registers
                 ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(um >> 32)) << 32) |
                 (unsigned)__builtin_amdgcn_readfirstlane((int)um);
@@ -1381,7 +1388,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                     double q[D];
                     eval_split_g<D, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], q);
                     bool dfr = false;
-                    const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, s_mask[s] & gmask, umask & gmask, gb,
+                    const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, (hull ? s_mask[s] : ~0ull) & gmask, umask & gmask, gb,
                                                               s_feas + s, a.sc, TT, dfr);
                     if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
