@@ -38,7 +38,15 @@ $(OBJDIR)/sspp_inst_d%.o: $(SRC)/sspp_inst.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -DSSPK_D=$* -c $< -o $@
 
-$(LIB): $(OBJDIR)/sspp_kernels.o $(INST) $(OBJDIR)/ces.o $(OBJDIR)/planner.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o
+# the source revision, compiled in as sspp_build_id() (sspp_amd/_stamp.py; checked at load time
+# by sspp_amd/_lib.py): rebuilt whenever any source changes
+SRCS = $(wildcard $(SRC)/*.h $(SRC)/*.hip $(SRC)/*.cpp) include/sspp_hip.h
+$(OBJDIR)/stamp.o: $(SRCS) sspp_amd/_stamp.py
+	@mkdir -p $(OBJDIR)
+	@printf 'extern "C" const char* sspp_build_id() { return "%s"; }\n' `$(PY) sspp_amd/_stamp.py` > $(OBJDIR)/stamp.cpp
+	g++ $(HOSTFLAGS) -c $(OBJDIR)/stamp.cpp -o $@
+
+$(LIB): $(OBJDIR)/sspp_kernels.o $(INST) $(OBJDIR)/ces.o $(OBJDIR)/planner.o $(OBJDIR)/sspp_capi.o $(OBJDIR)/mjcf.o $(OBJDIR)/spline_host.o $(OBJDIR)/sspp_hostapi.o $(OBJDIR)/stamp.o
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 

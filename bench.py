@@ -19,7 +19,7 @@ batches and alternate over --streams (default 2) HIP streams, each with its own 
 batch's argmin tail and launch gap hide under the next batch's scoring.
 
 Printed (rank 0): one JSON line with value = candidates scored per second over all ranks,
-a `roofline` object for the dominant kernel (k_sspp), a `roofline_fp64` object, and a
+a `roofline` object for the dominant kernel (k_sspp_c2f), a `binding_roofline` (FP64 VALU) object, and a
 `cpu_baseline` object (the oracle — test infrastructure, oracle/ — timed on a bounded sample
 of the same workload on the host cores, N=1 only, with a parity check on that sample).
 """
@@ -146,6 +146,25 @@ def setup_robocrane(args, device):
         feas = [torch.empty(spl * B, dtype=torch.uint8, device=device) for _ in js]
         return S.SsppSteps(js, streams[:len(js)], B, arcs, feas, steps_per_launch=spl)
 
+    def isolated_step_us(n=30):
+        # one B-candidate launch alone on the idle current stream, HIP events around each
+        import torch
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ts = []
+        for i in range(n + 5):
+            e0.record(st)
+            job.sample_score((1 << 41) + i * B, B, bufs[0]["arc"], bufs[0]["feasible"], None)
+            e1.record(st)
+            torch.cuda.synchronize()
+            if i >= 5:
+                ts.append(e0.elapsed_time(e1) * 1e3)
+        return float(np.median(ts))
+
+    def set_order(order):
+        for j in jobs:
+            j.set_option(S.OPT_ORDER, order)
+
     n_, D, p = 10, 7, 3
     # SURVEY §8(d) algorithmic work per candidate
     bytes_per = n_ * D * 8 + 8 + 1
@@ -157,7 +176,7 @@ def setup_robocrane(args, device):
     # hit-order pre-pass), read back from the library after the timed region
     ctx = dict(kind="sspp", kernel_name="k_sspp_c2f", effective=job.config,
                job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p,
-               make_executor=make_executor,
+               make_executor=make_executor, isolated_step_us=isolated_step_us, set_order=set_order,
                per_launch=B * roofline_spl(args))
     return B, step, kernel_only, bytes_per, flops_per, meta, ctx
 
@@ -686,6 +705,80 @@ def launch_ranks(args, argv):
     return subprocess.call(rank_launch_cmd(argv, args.gpus, port))
 
 
+def bench_line(args, ctx, meta, world, ns, native, B, elapsed, enqueue_s, kernel_s, bytes_per, flops_per,
+               per_launch, traffic, traffic_src, exec_per, exec_src, cpu, extras):
+    """The JSON line (rank 0).  `roofline` is the metric's HBM figure for the dominant kernel
+    (algorithmic bytes per launch / HIP-event launch time; `traffic` and `traffic_frac` are the
+    PMC-measured HBM bytes per launch and their rate against the peak); `binding_roofline` is
+    the resource that actually bounds it, FP64 VALU (PMC-executed flops per candidate)."""
+    total = args.steps * B * world
+    if ctx["kind"] == "multigoal":
+        # every goal's mean set + samples, whatever the rank count; the forwarded best
+        # (and, before the first success, the padding slot in its place) is not counted
+        total = args.steps * (ctx["samples"] + 1) * len(MULTIGOAL)
+    value = total / elapsed
+    ach_exec = None if exec_per is None else exec_per * per_launch / kernel_s / 1e12
+    ach_gbs = bytes_per * per_launch / kernel_s / 1e9
+    config = dict(meta, streams=ns, launch=("CES iteration chains (sspp_ces_plan), one stream per goal"
+                                            if "run_steps" in ctx else
+                                            "native executor, %d steps/call, %d steps/launch"
+                                            % (args.chunk, args.steps_per_launch)
+                                            if native else "eager"),
+                  parallelism="dp%d (candidate shards, RCCL all-gather argmin)" % world)
+    if "order1_elapsed_s" in extras:
+        # throughput at the hit order (the default) over throughput at order 1, same run
+        config["order_gain"] = extras["order1_elapsed_s"] / elapsed
+    line = {
+        "metric": {"robocrane": "candidate paths scored/sec (7-DoF, 128 waypts) at 1/2/4/8 MI355X; HBM %peak",
+                   "stacking": "candidate paths scored/sec (stacking.xml TSP)",
+                   "multigoal": "candidate paths scored/sec (TSP multi-goal, full CES iterations)"}[args.config],
+        "value": value,
+        "unit": "candidate paths/s",
+        "n_gpus": world,
+        "ranks_joined": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "host_enqueue_ms": enqueue_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong" if ctx["kind"] == "multigoal" else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (on-device Philox candidates around a linear init spline)",
+        "config": config,
+        "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": ach_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
+                     # the measured bytes' rate against the peak (the candidates are generated
+                     # in-kernel, so far below the algorithmic figure above)
+                     "traffic_frac": None if traffic is None else traffic / kernel_s / (HBM_PEAK_GBS * 1e9),
+                     "algorithmic_bytes_per_launch": bytes_per * per_launch,
+                     "kernel": ctx.get("kernel_name", "k_tsp"),
+                     "kernel_us": kernel_s * 1e6, "candidates_per_launch": per_launch,
+                     "bytes_per_candidate": bytes_per,
+                     # the same bytes at the timed loop's rate (launches overlap on streams)
+                     "steady_state_GBps": bytes_per * value / 1e9 / max(1, world)},
+        # what bounds the kernel: FP64 VALU with the flops it EXECUTES (PMC: 64 lanes x F64 wave
+        # instructions, FMA = 2; profiles/fp64_latest.json) over the same launches as
+        # `roofline`.  SURVEY 8(d)'s fixed charge table (every pair at every waypoint, no credit
+        # for early exit / culling) is kept for reference only: it overstates the work ~70x for
+        # the early-exit feasibility path.
+        "binding_roofline": {"bound": "fp64_valu", "achieved": ach_exec, "peak": FP64_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": None if ach_exec is None else ach_exec / FP64_PEAK_TFLOPS,
+                             "flops_per_candidate_executed": exec_per, "source": exec_src,
+                             "flops_per_candidate_charged": flops_per,
+                             # the same executed flops at the timed loop's rate (launches overlap)
+                             "steady_state_TFLOPs": None if exec_per is None else
+                             exec_per * value / 1e12 / max(1, world)},
+        "cpu_baseline": cpu,
+    }
+    if "isolated_step_us" in extras:
+        # one B-candidate batch (a single plan()'s worth) alone on the device
+        line["isolated_step_us"] = extras["isolated_step_us"]
+        line["single_plan_cand_per_s"] = B / (extras["isolated_step_us"] * 1e-6)
+    return line
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
@@ -808,68 +901,31 @@ def main(argv=None):
     lib_path = os.environ.get("SSPP_LIB_PATH")
     if lib_path:  # a variant build (profiling only): say so on the line
         meta["library"] = lib_path
+    extras = {}
+    if rank == 0 and world == 1 and "isolated_step_us" in ctx:
+        # one plan()-sized batch alone on an idle stream (HIP events per launch): the latency
+        # side of the same kernel, beside the fused multi-step throughput above
+        extras["isolated_step_us"] = ctx["isolated_step_us"]()
+    if world == 1 and "set_order" in ctx and args.mode == "native":
+        # what the hit-order pre-pass buys: the same timed run at scan order 1 (mean-path gap
+        # pairs, bisection waypoints; bit-identical results), after the main region
+        ctx["set_order"](1)
+        run_steps(args.warmup)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        run_steps(args.steps)
+        torch.cuda.synchronize()
+        extras["order1_elapsed_s"] = time.perf_counter() - t1
     if rank == 0:
-        total = args.steps * B * world
-        if ctx["kind"] == "multigoal":
-            # every goal's mean set + samples, whatever the rank count; the forwarded best
-            # (and, before the first success, the padding slot in its place) is not counted
-            total = args.steps * (ctx["samples"] + 1) * len(MULTIGOAL)
-        value = total / elapsed
-        exec_per, exec_src, ach_exec = None, None, None
+        exec_per, exec_src = None, None
         ff = os.path.join(ROOT, "profiles", "fp64_latest.json")
         if os.path.exists(ff):
             rec = json.load(open(ff)).get(pmc_key)
             if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and rec.get("rev") == KERNEL_REV and \
                     rec.get("candidates_per_launch", per_launch) == per_launch:
                 exec_per, exec_src = rec["fp64_flops_per_candidate"], rec["source"]
-                ach_exec = exec_per * per_launch / kernel_s / 1e12
-        ach_gbs = bytes_per * per_launch / kernel_s / 1e9
-        line = {
-            "metric": {"robocrane": "candidate paths scored/sec (7-DoF, 128 waypts) at 1/2/4/8 MI355X; HBM %peak",
-                       "stacking": "candidate paths scored/sec (stacking.xml TSP)",
-                       "multigoal": "candidate paths scored/sec (TSP multi-goal, full CES iterations)"}[args.config],
-            "value": value,
-            "unit": "candidate paths/s",
-            "n_gpus": world,
-            "ranks_joined": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "host_enqueue_ms": (t_enq - t0) * 1e3,
-            "higher_is_better": True,
-            "scaling": "strong" if ctx["kind"] == "multigoal" else "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (on-device Philox candidates around a linear init spline)",
-            "config": dict(meta, streams=ns, launch=("CES iteration chains (sspp_ces_plan), one stream per goal"
-                                                     if "run_steps" in ctx else
-                                                     "native executor, %d steps/call, %d steps/launch"
-                                                     % (args.chunk, args.steps_per_launch)
-                                                     if native else "eager"),
-                           parallelism="dp%d (candidate shards, RCCL all-gather argmin)" % world),
-            "roofline": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": bytes_per * per_launch,
-                         "kernel": ctx.get("kernel_name", "k_tsp"),
-                         "kernel_us": kernel_s * 1e6, "candidates_per_launch": per_launch,
-                         "bytes_per_candidate": bytes_per,
-                         # the same bytes at the timed loop's rate (launches overlap on streams)
-                         "steady_state_GBps": bytes_per * value / 1e9 / max(1, world)},
-            # FP64 VALU roofline with the flops the kernel EXECUTES (PMC: 64 lanes x F64 wave
-            # instructions, FMA = 2; profiles/fp64_latest.json) over the same launches as
-            # `roofline`.  SURVEY 8(d)'s fixed charge table (every pair at every waypoint, no
-            # credit for early exit / culling) is kept for reference only: it overstates the
-            # work ~40x for the early-exit feasibility path.
-            "roofline_fp64": {"bound": "fp64_valu", "achieved": ach_exec, "peak": FP64_PEAK_TFLOPS,
-                              "unit": "TFLOP/s", "frac": None if ach_exec is None else ach_exec / FP64_PEAK_TFLOPS,
-                              "flops_per_candidate_executed": exec_per, "source": exec_src,
-                              "flops_per_candidate_charged": flops_per,
-                              # the same executed flops at the timed loop's rate (launches overlap)
-                              "steady_state_TFLOPs": None if exec_per is None else
-                              exec_per * value / 1e12 / max(1, world)},
-            "cpu_baseline": cpu,
-        }
+        line = bench_line(args, ctx, meta, world, ns, native, B, elapsed, t_enq - t0, kernel_s, bytes_per,
+                          flops_per, per_launch, traffic, traffic_src, exec_per, exec_src, cpu, extras)
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -155,6 +155,10 @@ typedef struct sspp_tsp_args {
 
 const char* sspp_last_error(void);
 int sspp_version(void);
+/* Source revision the library was built from (16 hex digits of sspp_amd/_stamp.py's hash of
+ * sspp_amd/csrc/ + this header); the Python layer refuses a profiling variant whose revision
+ * differs from the tree it runs in.  No reference counterpart (build hygiene only). */
+const char* sspp_build_id(void);
 int sspp_device_count(int* n);
 
 /* ---- model ---- */
@@ -209,7 +213,9 @@ void sspp_job_free(sspp_job* job);
  * Nothing here changes a result: every option selects among bit-identical evaluation orders or
  * kernel forms.  sspp_job_get_option also reads back the effective configuration.          */
 #define SSPP_OPT_SHAPE_NT 1     /* k_sspp_c2f threads per workgroup: 64, 128 or 256; 0 = per launch */
-#define SSPP_OPT_SHAPE_G1 2     /* phase-1 lanes per candidate 1..64; 0 = per launch            */
+#define SSPP_OPT_SHAPE_G1 2     /* phase-1 lanes per candidate 1..64; 0 = per launch.  A launch
+                                   whose (NT / 64) * (64 / G1) exceeds 64 candidates per workgroup
+                                   (e.g. 128 x 1, 256 x 2) fails with SSPP_E_INVAL            */
 #define SSPP_OPT_ORDER 3        /* scan order: 0 scene / bisection, 1 mean-path gap (pairs),
                                    2 hit order (waypoints + pairs, host pre-pass; the default of
                                    sampled jobs, sigma > 0); setting it rebuilds the tables

@@ -10,7 +10,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("SSPP_LIB_PATH") or os.path.join(_HERE, "lib", "libsspp_hip.so")
+PRODUCT_LIB_PATH = os.path.join(_HERE, "lib", "libsspp_hip.so")
+# SSPP_LIB_PATH: a profiling variant (tools/build_variant.sh); never set on the product path
+LIB_PATH = os.environ.get("SSPP_LIB_PATH") or PRODUCT_LIB_PATH
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "sspp_hip.h")
 
 SSPP_OK = 0
@@ -96,6 +98,7 @@ _vp, _i64, _d, _i = C.c_void_p, C.c_int64, C.POINTER(C.c_double), C.c_int
 SIGNATURES = {
     "sspp_last_error": (C.c_char_p, []),
     "sspp_version": (C.c_int, []),
+    "sspp_build_id": (C.c_char_p, []),
     "sspp_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "sspp_model_load_mjcf": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
     "sspp_model_view_get": (C.c_int, [_vp, C.POINTER(ModelView)]),
@@ -174,15 +177,41 @@ def declared_symbols(header=HEADER_PATH):
 
 
 _lib = None
+build_warning = None  # set when the product library's revision differs from the tree's
+
+
+def check_revision(L, path, variant):
+    """Compare the library's source stamp (sspp_build_id) with the tree's (sspp_amd/_stamp.py).
+    A profiling variant from other sources is refused (its numbers would describe another
+    revision, and a missing export would surface later as an AttributeError); a product library
+    that differs is reported through `build_warning` (warnings.warn)."""
+    from ._stamp import source_hash
+    tree = source_hash()
+    f = getattr(L, "sspp_build_id", None)
+    built = None
+    if f is not None:
+        f.restype, f.argtypes = C.c_char_p, []
+        built = (f() or b"").decode(errors="replace")
+    if tree is None or built == tree:
+        return None
+    what = ("built from sources %s" % built) if built else "no source stamp (sspp_build_id)"
+    msg = "%s: %s, but the tree's sources are %s" % (path, what, tree)
+    if variant:
+        raise SsppError("stale variant library " + msg +
+                        " (rebuild it: bash tools/build_variant.sh NAME FLAGS)")
+    import warnings
+    warnings.warn("libsspp_hip.so does not match its sources: " + msg + " (run `make`)", RuntimeWarning)
+    return msg
 
 
 def lib():
-    global _lib
+    global _lib, build_warning
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise SsppError("HIP library not built: %s (run `make` or __graft_entry__.build())"
                             % LIB_PATH)
         L = C.CDLL(LIB_PATH)
+        build_warning = check_revision(L, LIB_PATH, os.path.abspath(LIB_PATH) != PRODUCT_LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)  # AttributeError -> missing export: fail loudly
             f.restype = res

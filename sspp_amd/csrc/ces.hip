@@ -779,6 +779,11 @@ int sspp_ces_read(sspp_ces* p, sspp_ces_state* st, double* L, double* Cnf, doubl
     }
     if (e == hipSuccess) e = hipStreamSynchronize(p->last);
     if (e != hipSuccess) return hip_err(e, "sspp_ces_read");
+    // everything enqueued so far has completed: the next operation starts a new record, so a
+    // read's stream differing from the next operation's does not count as mixed (which would
+    // make the next read wait on the whole device, other planners' streams included)
+    p->any_op = false;
+    p->mixed = false;
     CesHdr h;
     std::memcpy(&h, p->h_stage, sizeof h);
     st->n_fixed = h.nfixed;

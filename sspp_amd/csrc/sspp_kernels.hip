@@ -743,6 +743,14 @@ static int set_job_tables(sspp_job* j, const double* init_ctrl, double sigma, co
     return SSPP_OK;
 }
 
+// k_sspp_c2f dynamic LDS bytes for cpb candidates of nrd own doubles each
+static size_t c2f_lds(const sspp_job* j, int cpb, int nrd) {
+    const int nm = j->nm < 1 ? 1 : j->nm;
+    const int rbox = std::max(6 * nm, lanes_for(j->W - 1) / 64 + 1);
+    return sizeof(double) * ((size_t)j->n * j->D + (size_t)cpb * (nrd + rbox) + j->D) +
+           sizeof(unsigned long long) * cpb + sizeof(int) * (3 * cpb + 1);
+}
+
 extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_args* a, int64_t max_batch,
                          sspp_job** out) {
     sspp::clear_error();
@@ -759,10 +767,6 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     if (max_batch < 1) return sspp::set_error(SSPP_E_INVAL, "max_batch must be >= 1");
     if (scene && (scene->mode != SSPP_MODE_QPOS || scene->dof != D))
         return sspp::set_error(SSPP_E_INVAL, "scene was not bound for this dof");
-    // the largest per-candidate footprint (caller splines, n x D doubles) must fit the latency
-    // shape's 4 candidates in 64 KiB of LDS
-    if ((size_t)4 * n * D * sizeof(double) + 4096 > 64 * 1024)
-        return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS (n_ctrl x dof)");
     auto* j = new sspp_job();
     j->kind = 0; j->scene = scene; j->D = D; j->p = p; j->n = n; j->W = W;
     j->nknots = n + p + 1; j->sigma = a->sigma; j->seed = a->seed; j->max_batch = max_batch;
@@ -772,6 +776,13 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     j->nm = scene ? (int)scene->movers.size() : 1;
     if (j->nm < 1) j->nm = 1;
     j->lpc = lanes_for(W - 1);
+    // the worst-case launch footprint (caller splines: n x D doubles per candidate, plus the
+    // shared initial spline, hull boxes and flags) must fit the latency shape's 4 candidates in
+    // 64 KiB of LDS, or a later sspp_job_score_ctrl could not launch
+    if (c2f_lds(j, 4, n * D) > 64 * 1024) {
+        delete j;
+        return sspp::set_error(SSPP_E_UNSUPPORTED, "problem too large for LDS (n_ctrl x dof)");
+    }
     int rc;
     std::vector<double> us;
     for (int i = 0; i <= W; ++i) us.push_back((double)i / W);            // collision grid
@@ -816,12 +827,6 @@ static void c2f_shape(const sspp_job* j, int64_t cands, int* nt, int* g1) {
     *g1 = j->opt_g1 ? j->opt_g1 : (lat ? 64 : kThroughputG1);
 }
 
-static size_t c2f_lds(const sspp_job* j, int cpb, int nrd) {
-    const int nm = j->nm < 1 ? 1 : j->nm;
-    const int rbox = std::max(6 * nm, lanes_for(j->W - 1) / 64 + 1);
-    return sizeof(double) * ((size_t)j->n * j->D + (size_t)cpb * (nrd + rbox) + j->D) +
-           sizeof(unsigned long long) * cpb + sizeof(int) * (3 * cpb + 1);
-}
 
 static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B, double* d_arc,
                     uint8_t* d_feasible, double* d_ctrl_out, sspp_best* d_best, void* stream,
@@ -839,6 +844,11 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     const int r0 = d_ctrl ? 0 : std::min(p, n), r1 = d_ctrl ? n : std::max(r0, n - p);
     const int nrd = (r1 - r0) * D;
     int cpw = 64 / g1, cpb = (nt / 64) * cpw;
+    // k_sspp_c2f compacts survivors, lists phase-3 candidates and reduces the block argmin with
+    // one wave (tid < 64): a forced shape holding more than 64 candidates per workgroup is refused
+    if (cpb > 64)
+        return sspp::set_error(SSPP_E_INVAL, "launch shape " + std::to_string(nt) + "x" + std::to_string(g1) +
+                                                 " holds more than 64 candidates per workgroup");
     size_t lds = c2f_lds(j, cpb, nrd);
     if (lds > 64 * 1024 && !j->opt_nt) {  // large splines: the latency shape's 4 candidates
         nt = 256; g1 = 64; cpw = 1; cpb = 4;

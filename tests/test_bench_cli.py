@@ -51,3 +51,31 @@ def test_world_size_must_match_gpus():
 def test_latency_modes_are_single_gpu():
     r = _run(["--gpus", "2", "--mode", "dropin"])
     assert r.returncode != 0 and "single-GPU" in r.stderr
+
+
+def test_line_reports_what_bounds_the_kernel():
+    """The JSON line's fields, from stubbed measurements (no GPU): the metric's HBM roofline with
+    the PMC traffic's own fraction of the peak, the FP64 VALU binding roofline, the hit-order
+    gain of the same run and the single-plan (one isolated batch) rate."""
+    args = bench.parse(["--steps", "20", "--warmup", "5"])
+    ctx = dict(kind="sspp", kernel_name="k_sspp_c2f")
+    B, kernel_s, per_launch = 4096, 50e-6, 20 * 4096
+    line = bench.bench_line(args, ctx, dict(workload="stub"), 1, 4, True, B, elapsed=70e-6, enqueue_s=5e-6,
+                            kernel_s=kernel_s, bytes_per=569, flops_per=537056, per_launch=per_launch,
+                            traffic=2.4e6, traffic_src="stub", exec_per=7443.0, exec_src="stub", cpu=None,
+                            extras={"isolated_step_us": 25.0, "order1_elapsed_s": 77e-6})
+    assert line["value"] == pytest.approx(20 * B / 70e-6)
+    r = line["roofline"]
+    assert r["bound"] == "hbm" and r["frac"] == pytest.approx(569 * per_launch / kernel_s / 8e12)
+    assert r["traffic_frac"] == pytest.approx(2.4e6 / kernel_s / 8e12)
+    b = line["binding_roofline"]
+    assert b["bound"] == "fp64_valu" and b["frac"] == pytest.approx(7443.0 * per_launch / kernel_s / 78.6e12)
+    assert line["config"]["order_gain"] == pytest.approx(77 / 70)
+    assert line["single_plan_cand_per_s"] == pytest.approx(B / 25e-6)
+    assert line["isolated_step_us"] == 25.0
+    # without PMC records or the extra runs the fields are absent or null, never invented
+    line = bench.bench_line(args, ctx, {}, 2, 4, True, B, 70e-6, 5e-6, kernel_s, 569, 537056, per_launch,
+                            None, None, None, None, None, {})
+    assert line["roofline"]["traffic_frac"] is None and line["binding_roofline"]["frac"] is None
+    assert "order_gain" not in line["config"] and "single_plan_cand_per_s" not in line
+    assert line["n_gpus"] == line["ranks_joined"] == 2

@@ -122,3 +122,77 @@ def test_all_gather_records_gloo_layout():
     wantf = torch.cat([torch.arange(10, dtype=torch.float64) + 0.5 * r for r in range(world)])
     for r in range(world):
         assert res[r][0] == want.tolist() and res[r][1] == wantf.tolist()
+
+
+G_ = 3  # steps per chunk (bench.native_runner gathers a chunk's per-step records at once)
+
+
+def _steps_worker(rank, world, port, q, per):
+    """bench.native_runner's protocol on gloo: G_ steps, step t scoring ids (t*world + rank)*per
+    + [0, per); the chunk's per-step records [G][4] all-gathered once -> [world][G][4]."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    from oracle import oracle as O
+    import sspp_amd as S
+    from sspp_amd.runtime import all_gather_records
+    scene, knots, ctrl0 = _problem()
+    recs = []
+    for t in range(G_):
+        first = (t * world + rank) * per
+        ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), SEED, first, per)
+        arc, feas = O.sspp_score(scene, knots, 3, ctrl, W_, nthreads=1)
+        idx, cost = O.argmin(arc, feas)
+        recs.append([int(np.float64(cost).view(np.int64)), idx + first if idx >= 0 else -1, int(feas.sum()), 0])
+    rec = torch.tensor(recs, dtype=torch.int64)
+    out = torch.empty((world, G_, 4), dtype=torch.int64)
+    all_gather_records(out, rec)
+    steps = []
+    for t in range(G_):  # the per-step reduction reduce_best_steps runs on the device
+        parts = [(float(np.int64(out[r, t, 0].item()).view(np.float64)), int(out[r, t, 1]), int(out[r, t, 2]))
+                 for r in range(world)]
+        steps.append(S.reduce_best(parts))
+    q.put((rank, steps, out.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4])
+def test_chunked_step_records_four_ranks(world):
+    """The 4-rank layout of the driver's SCALE run, rehearsed on gloo: every rank's chunk of
+    per-step records gathers rank-major, and each step's reduced record equals one rank scoring
+    that step's whole batch (world * per candidates, ids t * world * per + [0, world * per))."""
+    from oracle import oracle as O
+    per = 24
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_steps_worker, args=(r, world, port, q, per)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (s, g)) for r, s, g in (q.get(timeout=180) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    scene, knots, ctrl0 = _problem()
+    B = world * per
+    some_mixed = False
+    for t in range(G_):
+        ctrl = O.sample_sspp(ctrl0, 3, 0.12, np.ones(7), SEED, t * B, B)
+        arc, feas = O.sspp_score(scene, knots, 3, ctrl, W_, nthreads=1)
+        idx, cost = O.argmin(arc, feas)
+        some_mixed |= bool(feas.any() and not feas.all())
+        want = (cost, idx + t * B if idx >= 0 else -1, int(feas.sum()))
+        for r in range(world):
+            assert res[r][0][t] == want
+    assert some_mixed
+    for r in range(1, world):  # every rank holds the same gathered records
+        assert res[r][1] == res[0][1]
+
+
+def test_host_reducer_ties_go_to_lowest_id():
+    """Equal costs on several ranks: the lowest global id wins, whatever the rank order."""
+    import sspp_amd as S
+    parts = [(1.5, 900, 2), (1.5, 17, 1), (float("inf"), -1, 0), (2.0, 3, 4)]
+    assert S.reduce_best(parts) == (1.5, 17, 7)
+    assert S.reduce_best(parts[::-1]) == (1.5, 17, 7)
+    assert S.reduce_best([(float("inf"), -1, 0)] * 4) == (float("inf"), -1, 0)

@@ -94,6 +94,19 @@ def test_robocrane_sample_score_matches_oracle(robocrane, nt, g1, B, W, arc_all)
         assert abs(cost - best_o) <= COST_TOL
 
 
+@pytest.mark.parametrize("nt,g1", [(128, 1), (256, 1), (256, 2), (256, 3)])
+def test_oversized_shapes_are_refused(robocrane, nt, g1):
+    """k_sspp_c2f reduces with one wave: a forced shape of more than 64 candidates per
+    workgroup ((NT / 64) * (64 / G1) > 64) must fail loudly, not score a subset."""
+    import sspp_amd as S
+    _, scene, _ = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=4096)
+    set_shape(job, nt, g1)
+    with pytest.raises(S.SsppError, match="more than 64 candidates"):
+        run_sspp(job, 4096, with_ctrl=False)
+
+
 def test_robocrane_config2_is_nontrivial(robocrane):
     """Config 2 must have both feasible and colliding candidates (else parity is vacuous)."""
     import sspp_amd as S

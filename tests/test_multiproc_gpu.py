@@ -1,6 +1,6 @@
 """The real multi-rank exchange in separate processes.
 
-Two processes share cuda:0 and form a gloo group (device records are staged through host
+Two (and, for the step protocol, four) processes share cuda:0 and form a gloo group (device records are staged through host
 memory by sspp_amd.all_gather_records; RCCL itself is exercised only on the driver's 8-GPU
 node).  Everything else is the production path:
 * bench.native_runner: executor launches on two streams, the chunk's per-step argmin records
@@ -45,11 +45,13 @@ def _run(tmp_path, mode, world, batch=0):
 
 
 @pytest.mark.timeout(450)
-def test_bench_step_protocol_two_ranks_equals_one(cuda, tmp_path):
-    two = _run(tmp_path, "steps", 2, batch=2048)
-    one = _run(tmp_path, "steps", 1, batch=4096)  # the union of both shards per step
-    assert two[0]["records"] == two[1]["records"]
-    assert two[0]["records"] == one[0]["records"]
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_step_protocol_ranks_equal_one(cuda, tmp_path, world):
+    many = _run(tmp_path, "steps", world, batch=4096 // world)
+    one = _run(tmp_path, "steps", 1, batch=4096)  # the union of the shards per step
+    for r in range(1, world):
+        assert many[r]["records"] == many[0]["records"]
+    assert many[0]["records"] == one[0]["records"]
     assert sum(len(c) for c in one[0]["records"]) == 30
 
 

@@ -34,6 +34,35 @@ def test_library_exports_every_declared_symbol():
     assert lib.sspp_version() >= 10000
 
 
+def test_library_matches_its_sources():
+    """The product library carries the hash of the sources it was built from (sspp_build_id,
+    sspp_amd/_stamp.py); a library not rebuilt after an edit would fail here."""
+    from sspp_amd import _stamp
+    lib = _lib.lib()
+    assert lib.sspp_build_id().decode() == _stamp.source_hash()
+    assert _lib.build_warning is None
+
+
+@pytest.mark.parametrize("stamp", ["0123456789abcdef", None])
+def test_stale_variant_library_is_refused(tmp_path, stamp):
+    """A profiling variant (SSPP_LIB_PATH) built from other sources — or from before the stamp
+    existed — is refused at load time with a message naming both revisions, not left to fail
+    later on a missing export (a stale libsspp_wgt.so broke a profiling run)."""
+    src = tmp_path / "stub.c"
+    body = 'int sspp_version(void) { return 10000; }\n'
+    if stamp:
+        body += 'const char* sspp_build_id(void) { return "%s"; }\n' % stamp
+    src.write_text(body)
+    so = tmp_path / "libsspp_stub.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)])
+    L = C.CDLL(str(so))
+    with pytest.raises(_lib.SsppError, match="stale variant library") as e:
+        _lib.check_revision(L, str(so), variant=True)
+    assert ("built from sources " + stamp if stamp else "no source stamp") in str(e.value)
+    with pytest.warns(RuntimeWarning, match="does not match its sources"):
+        assert _lib.check_revision(L, str(so), variant=False)
+
+
 def test_pybind_module_links_hip_library():
     import glob
     mods = glob.glob(os.path.join(ROOT, "sspp", "_sspp*.so"))
