@@ -20,9 +20,10 @@ PYMOD2   = sspp/_tsp$(PYEXT)
 PYINC    = $(shell $(PY) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
 PBINC    = $(shell $(PY) -c "import pybind11;print(pybind11.get_include())")
 
-HDRS = include/sspp_hip.h $(SRC)/model.h $(SRC)/sspp_device.h $(SRC)/xml_lite.h $(SRC)/sspp_kern.h
-# kernel instantiations, one translation unit per dof (+ 0: TaskSpacePlanner), compiled in parallel
-INST = $(foreach d,0 1 2 3 4 6 7 9,$(OBJDIR)/sspp_inst_d$(d).o)
+HDRS = include/sspp_hip.h $(SRC)/model.h $(SRC)/sspp_device.h $(SRC)/sspp_filter.h $(SRC)/xml_lite.h $(SRC)/sspp_kern.h
+# kernel instantiations, one translation unit per (dof, degree) (+ d0: TaskSpacePlanner), compiled
+# in parallel (one unit per degree also keeps the register allocation of each kernel its own)
+INST = $(OBJDIR)/sspp_inst_d0.o $(foreach d,1 2 3 4 6 7 9,$(foreach p,2 3,$(OBJDIR)/sspp_inst_d$(d)_p$(p).o))
 
 all: $(LIB) $(PYMOD) $(PYMOD2) oracle
 
@@ -34,9 +35,13 @@ $(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(OBJDIR)/sspp_inst_d0.o: $(SRC)/sspp_inst.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -DSSPK_D=0 -c $< -o $@
+
 $(OBJDIR)/sspp_inst_d%.o: $(SRC)/sspp_inst.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -DSSPK_D=$* -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DSSPK_D=$(firstword $(subst _p, ,$*)) -DSSPK_P=$(lastword $(subst _p, ,$*)) -c $< -o $@
 
 # the source revision, compiled in as sspp_build_id() (sspp_amd/_stamp.py; checked at load time
 # by sspp_amd/_lib.py): rebuilt whenever any source changes

@@ -78,6 +78,9 @@ def parse(argv=None):
     ap.add_argument("--shape", default="",
                     help="robocrane: force the k_sspp_c2f launch shape NTxG1 (e.g. 64x4; tuning, "
                          "default: chosen per launch by the library); the line reports it")
+    ap.add_argument("--scan", default="fp32", choices=["fp32", "fp64"],
+                    help="robocrane: k_sspp_c2f's FP32-filtered scan (default; FP64 decides whatever "
+                         "FP32 cannot certify, results identical) or the all-FP64 scan (A/B)")
     ap.add_argument("--chunk", type=int, default=80, help="native mode: steps per executor call")
     ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="native mode: independent steps (each its own B candidates, outputs and "
@@ -117,6 +120,8 @@ def setup_robocrane(args, device):
         nt, g1 = (int(x) for x in args.shape.lower().split("x"))
         for j in jobs:
             j.set_shape(nt, g1)
+    for j in jobs:
+        j.set_option(S.OPT_F32, 1 if args.scan == "fp32" else 0)
     bufs = [j.alloc(B, device=device) for j in jobs]
     job = jobs[0]
 
@@ -513,6 +518,19 @@ def run_dropin(args):
             lat.append(time.perf_counter() - ta)
             nfeas.append(len(paths))
         total = time.perf_counter() - t0
+        # the cold side: a fresh planner's first plan() (its job is created in that call: tables,
+        # device buffers, pinned outputs; the hit-order pre-pass runs asynchronously beside it)
+        # and its next calls, in this already-initialised process
+        cold = []
+        for _ in range(3):
+            fresh = _sspp.SamplingPathPlanner7(os.path.join(S.SCENE_DIR, "robocrane.xml"))
+            ts = []
+            for _ in range(4):
+                ta = time.perf_counter()
+                fresh.plan(start, end, 0.08, limits, B, W, n)
+                ts.append((time.perf_counter() - ta) * 1e6)
+            cold.append(ts)
+            del fresh
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
@@ -545,6 +563,9 @@ def run_dropin(args):
         "latency_us": {"median": float(np.median(lat_us)), "p10": float(np.percentile(lat_us, 10)),
                        "p90": float(np.percentile(lat_us, 90)), "mean": float(lat_us.mean())},
         "feasible_per_plan": float(np.mean(nfeas)),
+        # a fresh SamplingPathPlanner7: first plan() (job creation included), then calls 2-4
+        "first_call_us": float(np.median([c[0] for c in cold])),
+        "cold_calls_us": [[round(x, 1) for x in c] for c in cold],
         "isolated_step_kernel_us": float(np.median(ks)),
         "dtype": "f64", "data": "synthetic (on-device Philox candidates around a linear init spline)",
         "config": {"workload": "robocrane SamplingPathPlanner7.plan(start, end, 0.08, ones(7), %d, %d, %d)"

@@ -233,6 +233,13 @@ void sspp_job_free(sspp_job* job);
 #define SSPP_OPT_PREPASS_US 10  /* get: host microseconds of the creation's hit-order pre-pass  */
 #define SSPP_OPT_NPAIRS 11      /* get: pairs in the sampled-candidate table                    */
 #define SSPP_OPT_CYLBOX 12      /* get: that table has cylinder-box pairs (k_sspp_c2f settles them) */
+#define SSPP_OPT_F32 13         /* k_sspp_c2f's FP32-filtered scan: 1 (default) on, 0 all-FP64.
+                                   The filter only settles what FP64 settles the same way, so the
+                                   results are identical either way               */
+#define SSPP_OPT_LAST_F32 14    /* get: the last k_sspp_c2f launch ran the filtered scan         */
+#define SSPP_OPT_CREATE_US 15   /* get: host microseconds of the job's creation                  */
+#define SSPP_OPT_PREPASS_STATE 16 /* get: asynchronous hit-order pre-pass (the drop-in planner's
+                                   jobs): 0 none, 1 running, 2 landed, 3 applied / dropped      */
 int sspp_job_set_option(sspp_job* job, int key, int64_t value);
 int sspp_job_get_option(const sspp_job* job, int key, int64_t* value);
 
@@ -332,6 +339,8 @@ int sspp_planner_score(sspp_planner* p, const double* knots, int degree,
                        const double* ctrl /* [B][n][D] */, int64_t B, int n, int W, int with_collision,
                        double* arc_out, uint8_t* feasible_out, sspp_best* best_out);
 void sspp_planner_free(sspp_planner* p);
+/* sspp_job_get_option on the planner's plan() job (its effective configuration; tests) */
+int sspp_planner_get_option(const sspp_planner* p, int key, int64_t* value);
 
 /* ---- step executor: a planning loop's back-to-back batches in one call ----
  * Enqueues nsteps independent SamplingPathPlanner steps (each = one plan() batch of B

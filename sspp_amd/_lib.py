@@ -144,6 +144,7 @@ SIGNATURES = {
     "sspp_planner_score": (C.c_int, [_vp, _d, _i, _d, _i64, _i, _i, _i, _d, C.POINTER(C.c_uint8),
                                      C.POINTER(Best)]),
     "sspp_planner_free": (None, [_vp]),
+    "sspp_planner_get_option": (C.c_int, [_vp, _i, C.POINTER(_i64)]),
     "sspp_ces_create": (C.c_int, [_vp, C.POINTER(CesConfig), _i, C.POINTER(_vp)]),
     "sspp_ces_get_info": (C.c_int, [_vp, C.POINTER(CesInfo)]),
     "sspp_ces_begin": (C.c_int, [_vp, _d, _d, _i, _vp]),
@@ -165,7 +166,7 @@ SIGNATURES = {
 # job options (include/sspp_hip.h SSPP_OPT_*)
 OPT_SHAPE_NT, OPT_SHAPE_G1, OPT_ORDER, OPT_TSP_FORM, OPT_TSP_GENERIC = 1, 2, 3, 4, 5
 OPT_SAMPLER, OPT_LAST_NT, OPT_LAST_G1, OPT_WP_ORDER, OPT_PREPASS_US, OPT_NPAIRS = 6, 7, 8, 9, 10, 11
-OPT_CYLBOX = 12
+OPT_CYLBOX, OPT_F32, OPT_LAST_F32, OPT_CREATE_US, OPT_PREPASS_STATE = 12, 13, 14, 15, 16
 OPT_CES_FUSED = 101
 
 

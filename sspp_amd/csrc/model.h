@@ -52,6 +52,10 @@ struct TspCesEval {
 int tsp_eval_ces(sspp_job* j, const TspCesEval* e, int64_t n, double* d_L, double* d_Cnf,
                  double* d_Cwf, uint8_t* d_status, double* d_cost, double* d_vias_out,
                  void* stream);
+// sspp_job_create_sspp with the hit-order pre-pass off the caller's path: the job starts in gap /
+// bisection order and swaps in the hit order at the first launch after the pre-pass lands (the
+// drop-in planner's first plan(), planner.hip; results are identical in every order)
+int job_create_sspp_async(const sspp_scene* scene, const sspp_sspp_args* a, int64_t max_batch, sspp_job** out);
 // k_sspp_c2f writes ctrl_out rows only for feasible candidates (drop-in planner, planner.hip)
 void job_set_ctrl_feasible_only(sspp_job* j, int on);
 // sspp_plan_sspp's cached planners (planner.hip): dropped when their scene is freed

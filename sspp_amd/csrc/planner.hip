@@ -126,6 +126,13 @@ extern "C" int sspp_planner_create(const sspp_scene* scene, int dof, sspp_planne
 
 extern "C" void sspp_planner_free(sspp_planner* p) { delete p; }
 
+extern "C" int sspp_planner_get_option(const sspp_planner* p, int key, int64_t* value) {
+    sspp::clear_error();
+    if (!p || !value) return sspp::set_error(SSPP_E_INVAL, "sspp_planner_get_option: null argument");
+    if (!p->plan_job.j) return sspp::set_error(SSPP_E_INVAL, "sspp_planner_get_option: no plan() yet");
+    return sspp_job_get_option(p->plan_job.j, key, value);
+}
+
 // plan()'s common front: initializePath on the host, then the job of this shape created (first
 // call / new shape / larger batch) or re-targeted asynchronously, then one scoring launch on the
 // planner's stream.  pinned_out: arc / feasible / best and the feasible candidates' control
@@ -156,7 +163,8 @@ static int plan_enqueue(sspp_planner* p, const double* start, const double* end,
         sspp_sspp_args a{};
         a.knots = knots_out; a.degree = deg; a.init_ctrl = ctrl0.data(); a.n_ctrl = n; a.dof = D;
         a.sigma = sigma; a.limits = limits; a.check_points = check_points; a.seed = seed;
-        if ((rc = sspp_job_create_sspp(p->scene, &a, B, &p->plan_job.j))) return rc;
+        // the hit-order pre-pass runs off this call's path (first plan() latency)
+        if ((rc = sspp::job_create_sspp_async(p->scene, &a, B, &p->plan_job.j))) return rc;
         p->plan_n = n; p->plan_W = check_points; p->plan_cap = B;
         if ((rc = p->d_arc.reserve(B)) || (rc = p->d_feas.reserve(B)) || (rc = p->d_best.reserve(1)) ||
             (rc = p->d_ctrl.reserve(B * nd)) || (rc = p->h_arc.reserve(B)) || (rc = p->h_feas.reserve(B)) ||

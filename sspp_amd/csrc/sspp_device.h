@@ -38,6 +38,8 @@ struct DGeom {
     int32_t mover;   // -1 static
     int32_t orig;    // model geom index (orders same-type pairs like the oracle)
     int32_t relrot;  // moving geoms: 0 when mat is exactly the identity (pose = mover rotation)
+    // FP32 copies for the filtered scan (sspp_filter.h): the doubles above rounded to nearest
+    float fpos[3], fmat[9], fsize[3], frbound;
 };
 
 // One filter-passing pair with the partner's data inlined, so the wave-uniform pair loop
@@ -54,7 +56,22 @@ struct DPair {
     double omat[9];
     double osize[3];
     double orbound;
+    // FP32 copies for the filtered scan (sspp_filter.h): the doubles above rounded to nearest
+    float fmargin, fopos[3], fomat[9], fosize[3], forbound;
 };
+
+// fill the FP32 copies of a geom / pair record from its doubles (host, at table creation)
+inline void fill_f32(DGeom& g) {
+    for (int k = 0; k < 3; ++k) { g.fpos[k] = (float)g.pos[k]; g.fsize[k] = (float)g.size[k]; }
+    for (int k = 0; k < 9; ++k) g.fmat[k] = (float)g.mat[k];
+    g.frbound = (float)g.rbound;
+}
+inline void fill_f32(DPair& p) {
+    p.fmargin = (float)p.margin;
+    for (int k = 0; k < 3; ++k) { p.fopos[k] = (float)p.opos[k]; p.fosize[k] = (float)p.osize[k]; }
+    for (int k = 0; k < 9; ++k) p.fomat[k] = (float)p.omat[k];
+    p.forbound = (float)p.orbound;
+}
 
 struct DMover {
     int32_t qpos_adr;
@@ -1138,6 +1155,43 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
         return *nd;
     }
     return sat_box_box(p1, m1, s1, p2, m2, s2, margin) ? 1 : 0;
+}
+
+// rounding allowance of the culls (pair_near, the hull masks): the spline evaluation's |error| ~ 1e-15
+constexpr double kHullPad = 1e-9;
+
+// Per-waypoint broadphase of one pair (exact: it only rejects pairs whose narrowphase cannot
+// report dist < margin).  Two spheres: MuJoCo's bounding-sphere test.  Plane vs a bounded
+// geom: every point of the geom lies within rbound of its centre, so a centre height over the
+// plane above rbound + margin (+ kHullPad for rounding) rules out a contact — the plane-box
+// corners satisfy t >= h - sum_j |n.a_j| e_j >= h - |e| = h - rbound (Cauchy-Schwarz).
+// A box partner that passes the sphere test is tested once more against the moving geom's
+// bounding sphere (centre in the box frame, distance to the box): a geom whose sphere stays
+// farther than rbound + margin (+ kHullPad) from the box cannot touch it.  This rejects, for a
+// few dozen flops, the near-but-apart pairs (a block above a large table) before the 15-axis SAT.
+SSPP_HD bool pair_near(const DPair& pr, double rg, const double* gp,
+                                          const double* op, const double* om) {
+    const double ro = pr.orbound;
+    if (rg > 0.0 && ro > 0.0) {
+        const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
+        const double thr = rg + ro + pr.margin;
+        if (dot3(dc, dc) > thr * thr) return false;
+        if (pr.otype == 6) {
+            const double lx = fma(om[6], dc[2], fma(om[3], dc[1], om[0] * dc[0]));
+            const double ly = fma(om[7], dc[2], fma(om[4], dc[1], om[1] * dc[0]));
+            const double lz = fma(om[8], dc[2], fma(om[5], dc[1], om[2] * dc[0]));
+            const double ex = fmax(fabs(lx) - pr.osize[0], 0.0), ey = fmax(fabs(ly) - pr.osize[1], 0.0),
+                         ez = fmax(fabs(lz) - pr.osize[2], 0.0);
+            const double lim = rg + pr.margin + kHullPad;
+            return !(fma(ez, ez, fma(ey, ey, ex * ex)) > lim * lim);
+        }
+        return true;
+    }
+    if (pr.otype == 0 && rg > 0.0) {
+        const double h = (gp[0] - op[0]) * om[2] + (gp[1] - op[1]) * om[5] + (gp[2] - op[2]) * om[8];
+        return !(h - rg > pr.margin + kHullPad);
+    }
+    return true;
 }
 
 SSPP_HD double geom_rbound(int type, const double* s) {

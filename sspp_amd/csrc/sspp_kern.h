@@ -22,10 +22,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "model.h"
@@ -41,6 +43,7 @@ __device__ unsigned long long g_wg_ph[8 << 16];  // per workgroup: shader clock 
 #define WG_PH(k) do { } while (0)
 #endif
 #include "sspp_device.h"
+#include "sspp_filter.h"
 
 using namespace sspd;
 
@@ -124,8 +127,7 @@ __device__ __forceinline__ DPair load_pair(cpair_t p) {
 // position columns.  A pair whose partner cannot come within rbound + margin of that box
 // (expanded by the moving geom's reach) for ANY waypoint is culled for the whole candidate:
 // exactly the pairs the per-waypoint bounding-sphere test would reject at every waypoint.
-// kHullPad absorbs the rounding of the spline evaluation (|error| ~ 1e-15).
-constexpr double kHullPad = 1e-9;
+// kHullPad (sspp_device.h) absorbs the rounding of the spline evaluation (|error| ~ 1e-15).
 
 __host__ __device__ __forceinline__ bool pair_may_touch(const DPair& pr, const DGeom& G, const double* lo,
                                                const double* hi) {
@@ -374,22 +376,34 @@ __device__ __forceinline__ double uniform01(unsigned long long seed, unsigned lo
 __device__ __forceinline__ int sample_items(int sampler, int npert) {
     return sampler ? (npert + 3) >> 2 : (npert + 1) >> 1;
 }
+// c32 (optional): the FP32 copy of the same values (k_sspp_c2f's filtered scan)
 __device__ __forceinline__ void sample_item_to(int sampler, unsigned long long seed, unsigned long long g,
                                                int m, int npert, int D, double sigma,
-                                               const double* limits, const double* base, double* c) {
+                                               const double* limits, const double* base, double* c,
+                                               float* c32 = nullptr) {
     if (sampler == 0) {
         double z0, z1;
         normal_pair(seed, g, (unsigned)m, 0u, &z0, &z1);
         const int k = 2 * m;
-        c[k] = base[k] + (sigma * z0) * limits[k % D];
-        if (k + 1 < npert) c[k + 1] = base[k + 1] + (sigma * z1) * limits[(k + 1) % D];
+        const double v0 = base[k] + (sigma * z0) * limits[k % D];
+        c[k] = v0;
+        if (c32) c32[k] = (float)v0;
+        if (k + 1 < npert) {
+            const double v1 = base[k + 1] + (sigma * z1) * limits[(k + 1) % D];
+            c[k + 1] = v1;
+            if (c32) c32[k + 1] = (float)v1;
+        }
     } else {
         double z[4];
         normal_quad(seed, g, (unsigned)m, 0u, z);
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
             const int k = 4 * m + h;
-            if (k < npert) c[k] = base[k] + (sigma * z[h]) * limits[k % D];
+            if (k < npert) {
+                const double v = base[k] + (sigma * z[h]) * limits[k % D];
+                c[k] = v;
+                if (c32) c32[k] = (float)v;
+            }
         }
     }
 }
@@ -530,40 +544,6 @@ __device__ __forceinline__ void geom_rot_t(const double* R, const DGeom& G, doub
         gm[3 + j] = fma(R[4], G.mat[3 + j], R[3] * G.mat[j]);
         gm[6 + j] = R[8] * G.mat[6 + j];
     }
-}
-
-// Per-waypoint broadphase of one pair (exact: it only rejects pairs whose narrowphase cannot
-// report dist < margin).  Two spheres: MuJoCo's bounding-sphere test.  Plane vs a bounded
-// geom: every point of the geom lies within rbound of its centre, so a centre height over the
-// plane above rbound + margin (+ kHullPad for rounding) rules out a contact — the plane-box
-// corners satisfy t >= h - sum_j |n.a_j| e_j >= h - |e| = h - rbound (Cauchy-Schwarz).
-// A box partner that passes the sphere test is tested once more against the moving geom's
-// bounding sphere (centre in the box frame, distance to the box): a geom whose sphere stays
-// farther than rbound + margin (+ kHullPad) from the box cannot touch it.  This rejects, for a
-// few dozen flops, the near-but-apart pairs (a block above a large table) before the 15-axis SAT.
-__device__ __forceinline__ bool pair_near(const DPair& pr, double rg, const double* gp,
-                                          const double* op, const double* om) {
-    const double ro = pr.orbound;
-    if (rg > 0.0 && ro > 0.0) {
-        const double dc[3] = {op[0] - gp[0], op[1] - gp[1], op[2] - gp[2]};
-        const double thr = rg + ro + pr.margin;
-        if (dot3(dc, dc) > thr * thr) return false;
-        if (pr.otype == 6) {
-            const double lx = fma(om[6], dc[2], fma(om[3], dc[1], om[0] * dc[0]));
-            const double ly = fma(om[7], dc[2], fma(om[4], dc[1], om[1] * dc[0]));
-            const double lz = fma(om[8], dc[2], fma(om[5], dc[1], om[2] * dc[0]));
-            const double ex = fmax(fabs(lx) - pr.osize[0], 0.0), ey = fmax(fabs(ly) - pr.osize[1], 0.0),
-                         ez = fmax(fabs(lz) - pr.osize[2], 0.0);
-            const double lim = rg + pr.margin + kHullPad;
-            return !(fma(ez, ez, fma(ey, ey, ex * ex)) > lim * lim);
-        }
-        return true;
-    }
-    if (pr.otype == 0 && rg > 0.0) {
-        const double h = (gp[0] - op[0]) * om[2] + (gp[1] - op[1]) * om[5] + (gp[2] - op[2]) * om[8];
-        return !(h - rg > pr.margin + kHullPad);
-    }
-    return true;
 }
 
 // DEEP=false: checkCollision's ncon > 0 for one candidate.  Every active lane of the wave
@@ -910,6 +890,10 @@ struct SsppC2F {
     int nt;        // launch shape (host side): threads per workgroup, dynamic LDS bytes
     int lds;
     int ctrl_feas; // ctrl_out rows only for candidates with no contact
+    // FP32-filtered scan (sspp_filter.h): on when f32 != 0; feps = the certified margin (m),
+    // fplim = the largest |mover root coordinate| it is certified for
+    int f32;
+    float feps, fplim;
 };
 
 #ifdef SSPP_C2F_STATS
@@ -1030,6 +1014,165 @@ __device__ __forceinline__ bool scan_pairs(const double* q, bool live, unsigned 
     return ghit;
 }
 
+// ---------------------------------------------------------------- FP32-filtered scan (sspp_filter.h)
+// eval_split on the FP32 copies of the control points (LDS, written beside the doubles)
+template <int D, int P>
+__device__ __forceinline__ void eval_split32(const float* sm, int mine, int fix, int r0, int r1,
+                                             const float (&Nr)[P + 1], int span, float* q) {
+    int o[P + 1];
+#pragma unroll
+    for (int r = 0; r <= P; ++r) o[r] = crow(mine, fix, r0, r1, span - P + r, D);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        float acc = Nr[0] * sm[o[0] + d];
+#pragma unroll
+        for (int r = 1; r <= P; ++r) acc = fmaf(Nr[r], sm[o[r] + d], acc);
+        q[d] = acc;
+    }
+}
+
+// mover_poses<D, NM, 0> in FP32: false when a quaternion is left to FP64 (sspf::quat_rot32) or
+// a root position lies outside the range eps is certified for (|x| <= plim)
+template <int D, int NM>
+__device__ __forceinline__ bool mover_poses32(const float* q, cmover_t movers, float (&mp)[NM][3],
+                                              float (&mR)[NM][9], float plim) {
+    bool ok = true;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        float qp[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+            qp[k] = (7 * m + k < D) ? q[(7 * m + k < D) ? 7 * m + k : 0] : (float)movers[m].qpos0[k];
+        ok = ok && sspf::quat_rot32(qp + 3, mR[m]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            mp[m][k] = qp[k];
+            ok = ok && fabsf(qp[k]) <= plim;
+        }
+    }
+    return ok;
+}
+
+// scan_pairs in FP32 (same wave-uniform loop, masks and group semantics): returns true for the
+// lanes of a group in which some lane has a CERTAIN contact; `amb` receives, per lane, the pairs
+// (bits k < 64) the filter left to FP64.  A group with a certain contact needs no FP64 pass.
+template <int D, int NM, bool ONEGEOM>
+__device__ __forceinline__ bool scan_pairs32(const float* q, bool live, unsigned long long mymask,
+                                             unsigned long long umask, unsigned long long gbits,
+                                             const KScene& sc, const SceneT& T, float eps, float plim,
+                                             unsigned long long& amb) {
+    const cgeom_t geoms = (cgeom_t)T.geoms;
+    const cpair_t pairs = (cpair_t)T.pairs;
+    const int np = sc.npairs;
+    amb = 0ull;
+    float mp[NM][3], mR[NM][9];
+    if (!mover_poses32<D, NM>(q, (cmover_t)T.movers, mp, mR, plim)) {
+        if (live) amb = mymask & (np >= 64 ? ~0ull : ((1ull << np) - 1ull));
+        live = false;
+    }
+    int cur = -1, gtype = 0, gmover = 0, grelrot = 0;
+    float gp[3], gmat[9], gsize[3], grb = 0.0f;
+    bool have_rot = true;
+    // the moving geom's pose (geom_pose in FP32); its rotation only where a pair needs it
+#define SSPF_LOAD_GEOM(IDX, P, R)                                                        \
+    do {                                                                                 \
+        const SSPP_CONST DGeom* g_ = geoms + (IDX);                                      \
+        gtype = g_->type; gmover = g_->mover; grelrot = g_->relrot; grb = g_->frbound;   \
+        gsize[0] = g_->fsize[0]; gsize[1] = g_->fsize[1]; gsize[2] = g_->fsize[2];       \
+        const float pos_[3] = {g_->fpos[0], g_->fpos[1], g_->fpos[2]};                   \
+        float t_[3];                                                                     \
+        sspf::matvec3f((R), pos_, t_);                                                   \
+        gp[0] = (P)[0] + t_[0]; gp[1] = (P)[1] + t_[1]; gp[2] = (P)[2] + t_[2];          \
+    } while (0)
+#define SSPF_GEOM_ROT(IDX, R)                                                            \
+    do {                                                                                 \
+        if (grelrot) {                                                                   \
+            const SSPP_CONST DGeom* g_ = geoms + (IDX);                                  \
+            float gm_[9];                                                                \
+            for (int e_ = 0; e_ < 9; ++e_) gm_[e_] = g_->fmat[e_];                       \
+            sspf::matmul3f((R), gm_, gmat);                                              \
+        } else {                                                                         \
+            for (int e_ = 0; e_ < 9; ++e_) gmat[e_] = (R)[e_];                           \
+        }                                                                                \
+    } while (0)
+    if (ONEGEOM) {
+        cur = pairs[0].gm;
+        SSPF_LOAD_GEOM(cur, mp[0], mR[0]);
+        SSPF_GEOM_ROT(cur, mR[0]);
+    }
+    bool ghit = false;
+    const float pad = (float)kHullPad;
+    for (int k = 0; k < np; ++k) {
+        if (k < 64) {
+            const unsigned long long rest = umask >> k;
+            if (rest == 0ull) break;
+            k += __builtin_ctzll(rest);
+            if (k >= np) break;
+        }
+        const SSPP_CONST DPair* pr = pairs + k;
+        if (!ONEGEOM && pr->gm != cur) {
+            cur = pr->gm;
+            const bool second = NM > 1 && geoms[cur].mover == 1;
+            SSPF_LOAD_GEOM(cur, second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0]);
+            have_rot = false;
+        }
+        int r = sspf::kNo;
+        if (live && (k >= 64 || ((mymask >> k) & 1ull))) {
+            float op[3], om[9], os[3];
+            const int otype = pr->otype;
+#pragma unroll
+            for (int e = 0; e < 3; ++e) { op[e] = pr->fopos[e]; os[e] = pr->fosize[e]; }
+#pragma unroll
+            for (int e = 0; e < 9; ++e) om[e] = pr->fomat[e];
+            if (NM > 1 && pr->omover >= 0) {
+                const bool second = pr->omover == 1;
+                const float* R = second ? mR[NM - 1] : mR[0];
+                const float* P = second ? mp[NM - 1] : mp[0];
+                float t[3], om2[9];
+                sspf::matvec3f(R, op, t);
+                op[0] = P[0] + t[0]; op[1] = P[1] + t[1]; op[2] = P[2] + t[2];
+                sspf::matmul3f(R, om, om2);
+#pragma unroll
+                for (int e = 0; e < 9; ++e) om[e] = om2[e];
+            }
+            const float margin = pr->fmargin;
+            const int nr = sspf::pair_near32(pr->forbound, otype, margin, os, grb, gp, op, om, eps, pad);
+            if (nr != sspf::kNo) {
+                if (!ONEGEOM && !have_rot) {
+                    const bool second = NM > 1 && gmover == 1;
+                    SSPF_GEOM_ROT(cur, second ? mR[NM - 1] : mR[0]);
+                    have_rot = true;
+                }
+                const bool gfirst = (gtype < otype) || (gtype == otype && geoms[cur].orig < pr->oorig);
+                r = gfirst ? sspf::collide32(gtype, gp, gmat, gsize, otype, op, om, os, margin, eps)
+                           : sspf::collide32(otype, op, om, os, gtype, gp, gmat, gsize, margin, eps);
+                if (r == sspf::kHit && nr == sspf::kAmb) r = sspf::kAmb;  // FP64 might cull it
+                if (r == sspf::kAmb && k < 64) amb |= 1ull << k;
+            }
+        }
+        C2F_STAT(13, 1);                                   // FP32 wave pair iterations
+        C2F_STAT(3, __popcll(__ballot(r != sspf::kNo)));   // FP32 lanes past the culls
+        if (__ballot(r == sspf::kHit) & gbits) { ghit = true; live = false; }
+        if (__ballot(live) == 0ull) break;
+    }
+#undef SSPF_LOAD_GEOM
+#undef SSPF_GEOM_ROT
+    return ghit;
+}
+
+// OR of a per-lane 64-bit mask over the wave, in scalar registers (the FP64 pass's pair loop
+// bound: only the pairs some lane left ambiguous)
+__device__ __forceinline__ unsigned long long wave_or64(unsigned long long m) {
+    unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        lo |= (unsigned)__shfl_xor((int)lo, off, 64);
+        hi |= (unsigned)__shfl_xor((int)hi, off, 64);
+    }
+    return ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)hi) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((int)lo);
+}
+
 // ================================================================ hit census (job creation)
 // The waypoint order of k_sspp_c2f's phase 1 is chosen from where sampled candidates of the
 // job's own distribution touch the scene: one workgroup per census candidate draws it
@@ -1141,7 +1284,8 @@ template <int D, int NM, int P, bool ONEGEOM, int NT, bool CBX>
 #define SSPP_C2F_GP_NT 256
 #endif
 __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F_WAVES_PER_EU : SSPP_C2F_WAVES_PER_EU_WIDE) void k_sspp_c2f(
-    SsppC2F a, SceneT T, const double* __restrict__ otab, const int* __restrict__ ospan,
+    SsppC2F a, SceneT T, const double* __restrict__ otab, const float* __restrict__ otab32,
+    const int* __restrict__ ospan,
     const double* __restrict__ atab, const int* __restrict__ aspan,
     const double* __restrict__ init_ctrl, const double* __restrict__ limits,
     const double* __restrict__ ctrl_in, double* __restrict__ ctrl_out, double* __restrict__ arc,
@@ -1183,6 +1327,8 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     int* s_feas = (int*)(s_mask + cpb);                       // [cpb]
     int* s_surv = s_feas + cpb;                               // [cpb + 1] (last = count)
     int* s_defer = s_surv + cpb + 1;                          // [cpb] undecided cylinder-box pair
+    // FP32 copies of the control points (filtered scan), at the same offsets as the doubles
+    float* s_f32 = (float*)(s_defer + cpb);                   // [ndof + cpb * nrd]
 
     // ---- per-lane layout: wave w holds candidates [w cpw, (w + 1) cpw), g1 lanes each
     const int wv = tid >> 6, ln = tid & 63;
@@ -1195,18 +1341,26 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     // spline, the limits, this lane's phase-1 basis row) is issued here, so their L2 round trips
     // overlap instead of following one another.
     const int row_p1 = l < a.npts ? l : 0;
-    double N_p1[P1];
+    const bool f32 = a.f32 != 0;
+    // the filtered scan's row in FP32 (the FP64 passes read their row when they need it)
+    float N32_p1[P1];
 #pragma unroll
-    for (int r = 0; r < P1; ++r) N_p1[r] = otab[row_p1 * P1 + r];
+    for (int r = 0; r < P1; ++r) N32_p1[r] = otab32[row_p1 * P1 + r];
     const int span_p1 = ospan[row_p1];
-    for (int rr = tid; rr < ndof; rr += NT) smem[o_fix + rr] = init_ctrl[rr];
+    for (int rr = tid; rr < ndof; rr += NT) {
+        const double v = init_ctrl[rr];
+        smem[o_fix + rr] = v;
+        if (f32) s_f32[o_fix + rr] = (float)v;
+    }
     if (tid < D) s_lim[tid] = limits[tid];
     if (ctrl_in) {  // element e = sl * ndof + r walked with add-with-carry
         const int dsl = NT / ndof, dr = NT - dsl * ndof;
         int sl = tid / ndof, r = tid - sl * ndof;
         const double* src = ctrl_in + cand0 * ndof;
         for (; sl < nvalid; sl += dsl) {
-            smem[o_own + sl * ndof + r] = src[sl * ndof + r];
+            const double v = src[sl * ndof + r];
+            smem[o_own + sl * ndof + r] = v;
+            if (f32) s_f32[o_own + sl * ndof + r] = (float)v;
             r += dr;
             if (r >= ndof) { r -= ndof; ++sl; }
         }
@@ -1223,14 +1377,15 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         int sl = tid / nq, m = tid - sl * nq;
         for (int t = tid; t < nvalid * nq; t += NT) {
             double* dst = smem + o_own + sl * nrd;
+            float* dst32 = f32 ? s_f32 + o_own + sl * nrd : nullptr;
             if (!(ABL & 1)) {
                 sample_item_to(a.sampler, a.seed, (unsigned long long)(first_id + cand0 + sl), m, nrd, D, a.sigma,
-                               s_lim, base, dst);
+                               s_lim, base, dst, dst32);
             } else {
                 const int per = a.sampler ? 4 : 2;
                 for (int h = 0; h < per; ++h) {
                     const int k = per * m + h;
-                    if (k < nrd) dst[k] = base[k];
+                    if (k < nrd) { dst[k] = base[k]; if (dst32) dst32[k] = (float)base[k]; }
                 }
             }
             sl += dsl;
@@ -1250,9 +1405,27 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         bool ghit = false, dfr = false;
         if (collide_on) {
             const bool live = valid && l < a.n1 && !a.sc.static_block && !(ABL & 16);
-            double q[D];
-            eval_split<D, P>(smem, o_own + (valid ? g : 0) * nrd, o_fix, r0, r1, N_p1, span_p1, q);
-            ghit = scan_pairs<D, NM, ONEGEOM>(q, live, ~0ull, ~0ull, gbits, nullptr, a.sc, TT, dfr);
+            const int own = o_own + (valid ? g : 0) * nrd;
+            if (f32) {
+                // FP32 first; FP64 only for the pairs it leaves ambiguous, in groups with no
+                // certain contact (sspp_filter.h)
+                float q32[D];
+                eval_split32<D, P>(s_f32, own, o_fix, r0, r1, N32_p1, span_p1, q32);
+                unsigned long long amb;
+                ghit = scan_pairs32<D, NM, ONEGEOM>(q32, live, ~0ull, ~0ull, gbits, a.sc, TT, a.feps, a.fplim, amb);
+                const bool need = live && !ghit && amb != 0ull;
+                C2F_STAT(11, __popcll(__ballot(need)));
+                if (__ballot(need) != 0ull) {
+                    double q[D];
+                    eval_split_g<D, P>(smem, own, o_fix, r0, r1, otab + row_p1 * P1, span_p1, q);
+                    ghit = scan_pairs<D, NM, ONEGEOM>(q, need, amb, wave_or64(need ? amb : 0ull), gbits, nullptr,
+                                                      a.sc, TT, dfr) || ghit;
+                }
+            } else {
+                double q[D];
+                eval_split_g<D, P>(smem, own, o_fix, r0, r1, otab + row_p1 * P1, span_p1, q);
+                ghit = scan_pairs<D, NM, ONEGEOM>(q, live, ~0ull, ~0ull, gbits, nullptr, a.sc, TT, dfr);
+            }
         }
         const bool gdef = (__ballot(dfr) & gbits) != 0ull;
         if (in_grp && l == 0 && g < cpb) {
@@ -1385,11 +1558,28 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                         if (si == q) gb = m;
                     }
                     if (it >= items) gb = 0ull;
-                    double q[D];
-                    eval_split_g<D, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], q);
-                    bool dfr = false;
-                    const bool h = scan_pairs<D, NM, ONEGEOM>(q, live, (hull ? s_mask[s] : ~0ull) & gmask, umask & gmask, gb,
-                                                              s_feas + s, a.sc, TT, dfr);
+                    bool dfr = false, h;
+                    const unsigned long long mym = (hull ? s_mask[s] : ~0ull) & gmask;
+                    if (f32) {
+                        float q32[D], N32[P1];
+#pragma unroll
+                        for (int r = 0; r < P1; ++r) N32[r] = otab32[j * P1 + r];
+                        eval_split32<D, P>(s_f32, o_own + s * nrd, o_fix, r0, r1, N32, ospan[j], q32);
+                        unsigned long long amb;
+                        h = scan_pairs32<D, NM, ONEGEOM>(q32, live, mym, umask & gmask, gb, a.sc, TT, a.feps, a.fplim, amb);
+                        const bool need = live && !h && amb != 0ull;
+                        C2F_STAT(12, __popcll(__ballot(need)));
+                        if (__ballot(need) != 0ull) {
+                            double q[D];
+                            eval_split_g<D, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], q);
+                            h = scan_pairs<D, NM, ONEGEOM>(q, need, amb, wave_or64(need ? amb : 0ull), gb, s_feas + s,
+                                                           a.sc, TT, dfr) || h;
+                        }
+                    } else {
+                        double q[D];
+                        eval_split_g<D, P>(smem, o_own + s * nrd, o_fix, r0, r1, otab + j * P1, ospan[j], q);
+                        h = scan_pairs<D, NM, ONEGEOM>(q, live, mym, umask & gmask, gb, s_feas + s, a.sc, TT, dfr);
+                    }
                     if (h) __hip_atomic_store(s_feas + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (dfr) __hip_atomic_store(s_defer + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
@@ -2114,8 +2304,11 @@ struct sspp_job {
     int last_nt = 0, last_g1 = 0;
     int pair_order = 0;        // effective pair order of the tables (SSPP_ORDER_*)
     int wp_order = 0;          // effective collision-waypoint order (SSPP_ORDER_*)
+    int f32 = 1;               // k_sspp_c2f's FP32-filtered scan (SSPP_OPT_F32; results identical)
+    int last_f32 = 0;          // whether the last launch ran it
     double prepass_ms = 0.0;   // host time of the hit-order pre-pass at creation
     double* d_otab = nullptr;  // collision rows in the job's waypoint order
+    float* d_otab32 = nullptr; // the same rows in FP32 (k_sspp_c2f's filtered scan)
     int* d_ospan = nullptr;
     std::vector<int> h_wps;    // that order
     DPair* d_pairs = nullptr;  // this job's pair table (ordered)
@@ -2139,6 +2332,23 @@ struct sspp_job {
     bool upd_pending = false;
     double start[4], end[4], lo[4], hi[4];
     double z_min = 0, w_col = 1, floor_z_min = 0, floor_margin = 0.01, floor_scale = 10;
+    // asynchronous hit-order pre-pass (the drop-in planner's first plan(): DESIGN.md §5): the
+    // census runs on its own stream and a host thread orders the tables; the next launch after
+    // it lands swaps them in.  Until then the job scans in gap / bisection order (identical results).
+    std::thread prepass_thread;
+    std::atomic<int> prepass_state{0};  // 0 none, 1 running, 2 result ready, 3 applied or dropped
+    std::vector<int> pre_wps;           // the thread's result: waypoint order,
+    std::vector<DPair> pre_pairs, pre_pairs_s;  // pair tables (hit order) for the creation's values
+    double pre_ms = 0.0;                // census + host ordering, wall time
+    int pre_gen = 0;                    // tables_gen the result was computed for
+    int tables_gen = 0;                 // bumped by every update that re-derives the pair tables
+    hipStream_t pre_stream = nullptr;
+    hipEvent_t pre_ev = nullptr;
+    unsigned long long* d_hits = nullptr;
+    unsigned long long* h_hits = nullptr;  // pinned
+    DPair* d_census_pairs = nullptr;    // the census's own copy of the sampled table
+    std::vector<void*> retired;         // device tables replaced while kernels may still read them
+    double create_ms = 0.0;             // host time of sspp_job_create_sspp
 };
 
 
@@ -2212,7 +2422,7 @@ hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o,
     const SceneT T = scene_t_job(j, !o.ctrl_in);
 #define SSPP_LAUNCH_C2F(NMV, OGV, CBV)                                                                    \
     hipLaunchKernelGGL((k_sspp_c2f<D, NMV, P, OGV, NT, CBV>), dim3(nblk), dim3(NT), k.lds, st, k, T, j->d_otab, \
-                       j->d_ospan, atab, aspan, j->d_init, j->d_limits, o.ctrl_in, o.ctrl_out, o.arc,      \
+                       j->d_otab32, j->d_ospan, atab, aspan, j->d_init, j->d_limits, o.ctrl_in, o.ctrl_out, o.arc,      \
                        o.feasible, j->d_part, j->d_sync, o.best)
     const bool og = NM == 1 && k.sc.onegeom && k.sc.npairs > 0;
     if (og && k.sc.cylbox) SSPP_LAUNCH_C2F(1, true, true);
@@ -2235,26 +2445,13 @@ hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, in
 // ---- per-dof entry points, instantiated one dof per translation unit (sspp_inst.hip, built
 // with -DSSPK_D=1..9) so the kernels compile in parallel; the host code (sspp_kernels.hip)
 // switches on the job's dof
-template <int D>
-hipError_t entry_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
-    if (j->nm == 2) {
-        if constexpr (D == 9) return j->p == 3 ? launch_c2f<9, 2, 3>(k, j, o, nblk, st) : launch_c2f<9, 2, 2>(k, j, o, nblk, st);
-        return hipErrorInvalidValue;
-    }
-#ifdef SSPP_DEV_ONLY  // variant builds for experiments: degree 3 only (fast compile)
-    if (j->p != 3) return hipErrorInvalidValue;
-    return launch_c2f<D, 1, 3>(k, j, o, nblk, st);
-#else
-    return j->p == 3 ? launch_c2f<D, 1, 3>(k, j, o, nblk, st) : launch_c2f<D, 1, 2>(k, j, o, nblk, st);
-#endif
-}
-
 // the hit census of a sampled job (k_sspp_census): M candidates, every collision waypoint
 template <int D, int NM, int P>
 hipError_t launch_census(const sspp_job* j, int M, unsigned long long seed, unsigned long long* d_hits,
-                         hipStream_t st) {
+                         const DPair* pairs, hipStream_t st) {
     const KScene sc = kscene_job(j, true);
-    const SceneT T = scene_t_job(j, true);
+    SceneT T = scene_t_job(j, true);
+    if (pairs) T.pairs = pairs;  // the asynchronous pre-pass's own copy of the sampled table
     const int r0 = std::min(P, j->n), r1 = std::max(r0, j->n - P);
     const size_t lds = sizeof(double) * ((size_t)j->n * D + (size_t)(r1 - r0) * D + D);
     if (NM == 1 && sc.onegeom && sc.npairs > 0)
@@ -2265,18 +2462,44 @@ hipError_t launch_census(const sspp_job* j, int M, unsigned long long seed, unsi
                            j->W, j->sampler, j->sigma, seed, j->d_tab, j->d_span, j->d_init, j->d_limits, d_hits);
     return hipGetLastError();
 }
-template <int D>
-hipError_t entry_census(const sspp_job* j, int M, unsigned long long seed, unsigned long long* d_hits, hipStream_t st) {
+
+// one (dof, degree) per translation unit: sharing a unit with the other degree's kernels changed
+// the register allocation of the robocrane kernel (0 -> 275 spilled VGPRs at the same source)
+template <int D, int P>
+hipError_t entry_c2f_p(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
     if (j->nm == 2) {
-        if constexpr (D == 9) return j->p == 3 ? launch_census<9, 2, 3>(j, M, seed, d_hits, st)
-                                               : launch_census<9, 2, 2>(j, M, seed, d_hits, st);
+        if constexpr (D == 9) return launch_c2f<9, 2, P>(k, j, o, nblk, st);
         return hipErrorInvalidValue;
     }
+    return launch_c2f<D, 1, P>(k, j, o, nblk, st);
+}
+template <int D, int P>
+hipError_t entry_census_p(const sspp_job* j, int M, unsigned long long seed, unsigned long long* d_hits,
+                          const DPair* pairs, hipStream_t st) {
+    if (j->nm == 2) {
+        if constexpr (D == 9) return launch_census<9, 2, P>(j, M, seed, d_hits, pairs, st);
+        return hipErrorInvalidValue;
+    }
+    return launch_census<D, 1, P>(j, M, seed, d_hits, pairs, st);
+}
+template <int D>
+hipError_t entry_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
+#ifdef SSPP_DEV_ONLY  // variant builds for experiments: degree 3 only (fast compile)
+    if (j->p != 3) return hipErrorInvalidValue;
+    return entry_c2f_p<D, 3>(k, j, o, nblk, st);
+#else
+    return j->p == 3 ? entry_c2f_p<D, 3>(k, j, o, nblk, st) : entry_c2f_p<D, 2>(k, j, o, nblk, st);
+#endif
+}
+template <int D>
+hipError_t entry_census(const sspp_job* j, int M, unsigned long long seed, unsigned long long* d_hits,
+                        const DPair* pairs, hipStream_t st) {
 #ifdef SSPP_DEV_ONLY
     if (j->p != 3) return hipErrorInvalidValue;
-    return launch_census<D, 1, 3>(j, M, seed, d_hits, st);
+    return entry_census_p<D, 3>(j, M, seed, d_hits, pairs, st);
 #else
-    return j->p == 3 ? launch_census<D, 1, 3>(j, M, seed, d_hits, st) : launch_census<D, 1, 2>(j, M, seed, d_hits, st);
+    return j->p == 3 ? entry_census_p<D, 3>(j, M, seed, d_hits, pairs, st)
+                     : entry_census_p<D, 2>(j, M, seed, d_hits, pairs, st);
 #endif
 }
 
@@ -2348,9 +2571,10 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
     return hipGetLastError();
 }
 
-#define SSPK_ENTRY_DECL(X, D)                                                                             \
-    X template hipError_t entry_c2f<D>(const SsppC2F&, const sspp_job*, const SsppPtrs&, int, hipStream_t); \
-    X template hipError_t entry_census<D>(const sspp_job*, int, unsigned long long, unsigned long long*, hipStream_t);
+#define SSPK_ENTRY_DECL(X, D, P)                                                                          \
+    X template hipError_t entry_c2f_p<D, P>(const SsppC2F&, const sspp_job*, const SsppPtrs&, int, hipStream_t); \
+    X template hipError_t entry_census_p<D, P>(const sspp_job*, int, unsigned long long, unsigned long long*,   \
+                                               const DPair*, hipStream_t);
 #define SSPK_TSP_DECL(X)                                                                                  \
     X template hipError_t entry_tsp<0>(const TspK&, const sspp_job*, int, const double*, const double*,    \
                                        const double*, double*, double*, double*, double*, double*, uint8_t*, \

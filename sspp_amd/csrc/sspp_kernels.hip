@@ -10,13 +10,20 @@ using namespace sspk;
 
 #ifndef SSPP_SINGLE_TU
 namespace sspk {
-SSPK_ENTRY_DECL(extern, 1)
-SSPK_ENTRY_DECL(extern, 2)
-SSPK_ENTRY_DECL(extern, 3)
-SSPK_ENTRY_DECL(extern, 4)
-SSPK_ENTRY_DECL(extern, 6)
-SSPK_ENTRY_DECL(extern, 7)
-SSPK_ENTRY_DECL(extern, 9)
+SSPK_ENTRY_DECL(extern, 1, 2)
+SSPK_ENTRY_DECL(extern, 1, 3)
+SSPK_ENTRY_DECL(extern, 2, 2)
+SSPK_ENTRY_DECL(extern, 2, 3)
+SSPK_ENTRY_DECL(extern, 3, 2)
+SSPK_ENTRY_DECL(extern, 3, 3)
+SSPK_ENTRY_DECL(extern, 4, 2)
+SSPK_ENTRY_DECL(extern, 4, 3)
+SSPK_ENTRY_DECL(extern, 6, 2)
+SSPK_ENTRY_DECL(extern, 6, 3)
+SSPK_ENTRY_DECL(extern, 7, 2)
+SSPK_ENTRY_DECL(extern, 7, 3)
+SSPK_ENTRY_DECL(extern, 9, 2)
+SSPK_ENTRY_DECL(extern, 9, 3)
 SSPK_TSP_DECL(extern)
 }  // namespace sspk
 #endif
@@ -195,6 +202,7 @@ int sspp_scene_create(const sspp_model* m, int mode, int arg, int count_static, 
         for (int k = 0; k < 9; ++k) dg.relrot |= dg.mat[k] != ((k % 4 == 0) ? 1.0 : 0.0);
         dg.reach = mv ? std::sqrt(dg.pos[0] * dg.pos[0] + dg.pos[1] * dg.pos[1] + dg.pos[2] * dg.pos[2]) * (1.0 + 1e-12)
                       : 0.0;
+        fill_f32(dg);
         table_index[g] = (int)s->geoms.size();
         s->geoms.push_back(dg);
         if (m->geom_contype[g] || m->geom_conaffinity[g]) {
@@ -285,6 +293,7 @@ int sspp_scene_create(const sspp_model* m, int mode, int arg, int count_static, 
         for (int k = 0; k < 9; ++k) dp.omat[k] = O.mat[k];
         for (int k = 0; k < 3; ++k) dp.osize[k] = O.size[k];
         dp.orbound = O.rbound;
+        fill_f32(dp);
         s->pairs.push_back(dp);
     }
     for (size_t i = 0; i < mover_bodies.size(); ++i) {
@@ -632,8 +641,9 @@ static void table_flags(const sspp_scene* sc, const std::vector<DPair>& t, int* 
 }
 
 // Basis rows for a list of parameters (same A2.1/A2.2 code as the device header).
+// d_tab32 (optional): the same rows rounded to FP32 (k_sspp_c2f's filtered scan)
 static int upload_basis(const std::vector<double>& us, int p, const double* knots, int nknots,
-                        double** d_tab, int** d_span) {
+                        double** d_tab, int** d_span, float** d_tab32 = nullptr) {
     std::vector<double> tab(us.size() * (p + 1));
     std::vector<int> sp(us.size());
     for (size_t i = 0; i < us.size(); ++i) {
@@ -642,6 +652,10 @@ static int upload_basis(const std::vector<double>& us, int p, const double* knot
     }
     int rc = upload(d_tab, tab.data(), tab.size());
     if (rc) return rc;
+    if (d_tab32) {
+        std::vector<float> t32(tab.begin(), tab.end());
+        if ((rc = upload(d_tab32, t32.data(), t32.size()))) return rc;
+    }
     return upload(d_span, sp.data(), sp.size());
 }
 
@@ -661,30 +675,40 @@ static int upload_pairs_sync(sspp_job* j) {
     return SSPP_OK;
 }
 
-// the hit census (k_sspp_census) of M candidates: hit bits [M][ceil((W + 1) / 64)] to the host
+// the hit census (k_sspp_census) of M candidates into d (hit bits [M][ceil((W + 1) / 64)]), on
+// stream st; pairs: the sampled table to scan (nullptr: the job's)
+static hipError_t launch_census_d(sspp_job* j, int M, unsigned long long* d, const DPair* pairs, hipStream_t st) {
+    const unsigned long long seed = j->seed ^ 0xC3A5C85C97CB3127ull;  // independent of the job's candidates
+    switch (j->D) {
+#ifndef SSPP_DEV_ONLY
+        case 1: return entry_census<1>(j, M, seed, d, pairs, st);
+        case 2: return entry_census<2>(j, M, seed, d, pairs, st);
+        case 3: return entry_census<3>(j, M, seed, d, pairs, st);
+        case 4: return entry_census<4>(j, M, seed, d, pairs, st);
+        case 6: return entry_census<6>(j, M, seed, d, pairs, st);
+        case 9: return entry_census<9>(j, M, seed, d, pairs, st);
+#endif
+        case 7: return entry_census<7>(j, M, seed, d, pairs, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+// the census, synchronously: hit bits to the host
 static int run_census(sspp_job* j, int M, std::vector<uint64_t>& hits) {
     const int nw = (j->W + 64) >> 6;
     unsigned long long* d = nullptr;
     HIPCHK(hipMalloc((void**)&d, sizeof(unsigned long long) * (size_t)M * nw));
-    const unsigned long long seed = j->seed ^ 0xC3A5C85C97CB3127ull;  // independent of the job's candidates
-    hipError_t e = hipErrorInvalidValue;
-    switch (j->D) {
-#ifndef SSPP_DEV_ONLY
-        case 1: e = entry_census<1>(j, M, seed, d, nullptr); break;
-        case 2: e = entry_census<2>(j, M, seed, d, nullptr); break;
-        case 3: e = entry_census<3>(j, M, seed, d, nullptr); break;
-        case 4: e = entry_census<4>(j, M, seed, d, nullptr); break;
-        case 6: e = entry_census<6>(j, M, seed, d, nullptr); break;
-        case 9: e = entry_census<9>(j, M, seed, d, nullptr); break;
-#endif
-        case 7: e = entry_census<7>(j, M, seed, d, nullptr); break;
-    }
+    hipError_t e = launch_census_d(j, M, d, nullptr, nullptr);
     hits.assign((size_t)M * nw, 0ull);
     if (e == hipSuccess) e = hipMemcpy(hits.data(), d, sizeof(uint64_t) * hits.size(), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return hip_fail(e, "k_sspp_census");
     return SSPP_OK;
 }
+
+// The census scans every collision waypoint of kCensus candidates: above this many waypoints the
+// pre-pass would cost more than it saves, and the job keeps the gap / bisection order
+constexpr int kCensusMaxPts = 4097;
 
 // The job's scan orders for its initial spline / sigma / limits: the pair table ordered by the
 // mean-path gap (pairs_for_job), refined with the collision-waypoint order by the hit-order
@@ -701,7 +725,7 @@ static int set_job_tables(sspp_job* j, const double* init_ctrl, double sigma, co
         j->h_pairs_s = reachable_pairs(sc, j->h_pairs, init_ctrl, j->n, j->D, j->p, sigma, limits, j->sampler);
         table_flags(sc, j->h_pairs, &j->np_full, &j->cb_full, &j->og_full);
         table_flags(sc, j->h_pairs_s, &j->np_samp, &j->cb_samp, &j->og_samp);
-        if (order == 2 && create && !j->h_pairs_s.empty()) {
+        if (order == 2 && create && !j->h_pairs_s.empty() && j->W + 1 <= kCensusMaxPts) {
             // the census scans the sampled table in gap order; then both orders, and the
             // sampled table again (reachable_pairs keeps the order it is given)
             const auto t0 = std::chrono::steady_clock::now();
@@ -726,8 +750,9 @@ static int set_job_tables(sspp_job* j, const double* init_ctrl, double sigma, co
         std::vector<double> uo;
         for (int i : wps) uo.push_back((double)i / j->W);
         if (j->d_otab) { (void)hipFree(j->d_otab); j->d_otab = nullptr; }
+        if (j->d_otab32) { (void)hipFree(j->d_otab32); j->d_otab32 = nullptr; }
         if (j->d_ospan) { (void)hipFree(j->d_ospan); j->d_ospan = nullptr; }
-        int rc = upload_basis(uo, j->p, j->h_knots.data(), j->nknots, &j->d_otab, &j->d_ospan);
+        int rc = upload_basis(uo, j->p, j->h_knots.data(), j->nknots, &j->d_otab, &j->d_ospan, &j->d_otab32);
         if (rc) return rc;
     }
     if (!sc || sc->pairs.empty()) return SSPP_OK;
@@ -748,12 +773,146 @@ static size_t c2f_lds(const sspp_job* j, int cpb, int nrd) {
     const int nm = j->nm < 1 ? 1 : j->nm;
     const int rbox = std::max(6 * nm, lanes_for(j->W - 1) / 64 + 1);
     return sizeof(double) * ((size_t)j->n * j->D + (size_t)cpb * (nrd + rbox) + j->D) +
-           sizeof(unsigned long long) * cpb + sizeof(int) * (3 * cpb + 1);
+           sizeof(unsigned long long) * cpb + sizeof(int) * (3 * cpb + 1) +
+           sizeof(float) * ((size_t)j->n * j->D + (size_t)cpb * nrd);  // the FP32 copies
 }
+
+// The FP32 filter's certified margin for a pair table (sspp_filter.h): FP32's error
+// on a separation grows with the pair's extent (centre distance and box extents are bounded by
+// the two bounding radii plus the margin for every pair that passes the sphere test), about 6e-5 m
+// per metre of extent; eps = 2e-4 m per metre, at least 2e-4.  0 (filter off) past 64 pairs or
+// for pairs larger than 8 m, where the certified range would not be worth it.
+constexpr double kF32EpsPerMetre = 2e-4;
+constexpr float kF32PosLimit = 8.0f;
+static double f32_eps(const sspp_scene* sc, const std::vector<DPair>& t) {
+    if (!sc || t.empty() || t.size() > 64) return 0.0;
+    double S = 1.0;
+    for (const DPair& pr : t) {
+        const DGeom& G = sc->geoms[pr.gm];
+        const double ext = G.rbound + pr.orbound + pr.margin;
+        double far = 0.0;
+        for (int k = 0; k < 3; ++k) far = std::max(far, std::fabs(pr.opos[k]));
+        if (!(ext <= 8.0) || !(far <= 2.0 * kF32PosLimit) || G.rbound <= 0.0) return 0.0;
+        S = std::max(S, ext);
+    }
+    return kF32EpsPerMetre * S;
+}
+
+// The asynchronous pre-pass (sspp::job_create_sspp_async): the census on the job's own stream
+// (scanning its own copy of the sampled table), its hit bits into pinned memory, then a host
+// thread orders the waypoints and pairs exactly as the synchronous creation does.  The thread
+// touches only its copies and the job's pre_* result fields, published by prepass_state = 2.
+static int prepass_start(sspp_job* j, const double* init_ctrl, double sigma, const double* limits) {
+    const sspp_scene* sc = j->scene;
+    if (!sc || j->h_pairs_s.empty() || j->W + 1 > kCensusMaxPts) return SSPP_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int M = kCensus, nw = (j->W + 64) >> 6;
+    const size_t nh = (size_t)M * nw;
+    HIPCHK(hipStreamCreateWithFlags(&j->pre_stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&j->pre_ev, hipEventDisableTiming));
+    HIPCHK(hipMalloc((void**)&j->d_hits, sizeof(unsigned long long) * nh));
+    HIPCHK(hipHostMalloc((void**)&j->h_hits, sizeof(unsigned long long) * nh, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&j->d_census_pairs, sizeof(DPair) * j->h_pairs_s.size()));
+    HIPCHK(hipMemcpy(j->d_census_pairs, j->h_pairs_s.data(), sizeof(DPair) * j->h_pairs_s.size(), hipMemcpyHostToDevice));
+    hipError_t e = launch_census_d(j, M, j->d_hits, j->d_census_pairs, j->pre_stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(j->h_hits, j->d_hits, sizeof(unsigned long long) * nh, hipMemcpyDeviceToHost, j->pre_stream);
+    if (e == hipSuccess) e = hipEventRecord(j->pre_ev, j->pre_stream);
+    if (e != hipSuccess) return hip_fail(e, "k_sspp_census (asynchronous pre-pass)");
+    struct Copies {
+        std::vector<double> knots, init, limits;
+        std::vector<DPair> pairs;
+        double sigma;
+        int gen;
+    };
+    Copies c{j->h_knots, std::vector<double>(init_ctrl, init_ctrl + (size_t)j->n * j->D),
+             std::vector<double>(limits, limits + j->D), j->h_pairs, sigma, j->tables_gen};
+    j->prepass_state.store(1, std::memory_order_relaxed);
+    j->prepass_thread = std::thread([j, sc, c = std::move(c), t0, M, nh]() mutable {
+        if (hipEventSynchronize(j->pre_ev) != hipSuccess) {
+            j->prepass_state.store(3, std::memory_order_release);
+            return;
+        }
+        std::vector<uint64_t> hits(j->h_hits, j->h_hits + nh);
+        std::vector<int> wps = c2f_order(j->W);
+        waypoints_from_census(hits, M, j->W, kThroughputG1, wps);
+        const std::vector<int> pick(wps.begin(), wps.begin() + std::min<size_t>(wps.size(), kThroughputG1));
+        pairs_by_hits(sc, c.pairs, c.knots.data(), j->nknots, j->p, c.init.data(), j->D, c.sigma, c.limits.data(), j->W,
+                      pick);
+        j->pre_pairs_s = reachable_pairs(sc, c.pairs, c.init.data(), j->n, j->D, j->p, c.sigma, c.limits.data(), j->sampler);
+        j->pre_pairs = std::move(c.pairs);
+        j->pre_wps = std::move(wps);
+        j->pre_gen = c.gen;
+        j->pre_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        j->prepass_state.store(2, std::memory_order_release);
+    });
+    return SSPP_OK;
+}
+
+// Swap in the pre-pass's orders, once it has landed (called before each launch; never waits).  The
+// waypoint order suits any values; the pair tables are the creation's reachable subset, so they are
+// taken only when no update has re-derived the tables since.  Replaced device tables are retired,
+// not freed: launches on other streams may still read them.
+static void prepass_apply(sspp_job* j) {
+    if (j->prepass_state.load(std::memory_order_acquire) != 2) return;
+    j->prepass_thread.join();
+    j->prepass_state.store(3, std::memory_order_relaxed);
+    std::vector<double> uo;
+    for (int i : j->pre_wps) uo.push_back((double)i / j->W);
+    double* ot = nullptr;
+    float* ot32 = nullptr;
+    int* os = nullptr;
+    if (upload_basis(uo, j->p, j->h_knots.data(), j->nknots, &ot, &os, &ot32) == SSPP_OK) {
+        j->retired.insert(j->retired.end(), {(void*)j->d_otab, (void*)j->d_otab32, (void*)j->d_ospan});
+        j->d_otab = ot; j->d_otab32 = ot32; j->d_ospan = os;
+        j->h_wps = j->pre_wps;
+        j->wp_order = 2;
+    } else {
+        sspp::clear_error();
+        for (void* q : {(void*)ot, (void*)ot32, (void*)os}) if (q) (void)hipFree(q);
+    }
+    if (j->pre_gen == j->tables_gen && j->scene) {
+        const size_t cap = sizeof(DPair) * std::max<size_t>(1, j->scene->pairs.size());
+        DPair *dp = nullptr, *dps = nullptr;
+        if (hipMalloc((void**)&dp, cap) == hipSuccess && hipMalloc((void**)&dps, cap) == hipSuccess &&
+            hipMemcpy(dp, j->pre_pairs.data(), sizeof(DPair) * j->pre_pairs.size(), hipMemcpyHostToDevice) == hipSuccess &&
+            (j->pre_pairs_s.empty() ||
+             hipMemcpy(dps, j->pre_pairs_s.data(), sizeof(DPair) * j->pre_pairs_s.size(), hipMemcpyHostToDevice) == hipSuccess)) {
+            j->retired.insert(j->retired.end(), {(void*)j->d_pairs, (void*)j->d_pairs_s});
+            j->d_pairs = dp; j->d_pairs_s = dps;
+            j->h_pairs = j->pre_pairs; j->h_pairs_s = j->pre_pairs_s;
+            table_flags(j->scene, j->h_pairs, &j->np_full, &j->cb_full, &j->og_full);
+            table_flags(j->scene, j->h_pairs_s, &j->np_samp, &j->cb_samp, &j->og_samp);
+            j->pair_order = 2;
+        } else {
+            if (dp) (void)hipFree(dp);
+            if (dps) (void)hipFree(dps);
+        }
+    }
+    j->prepass_ms = j->pre_ms;
+}
+
+// wait for a running pre-pass and drop its result (option changes, job free)
+static void prepass_drop(sspp_job* j) {
+    if (j->prepass_thread.joinable()) j->prepass_thread.join();
+    j->prepass_state.store(3, std::memory_order_relaxed);
+}
+
+static int job_create_sspp_impl(const sspp_scene* scene, const sspp_sspp_args* a, int64_t max_batch,
+                                sspp_job** out, bool async_prepass);
 
 extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_args* a, int64_t max_batch,
                          sspp_job** out) {
+    return job_create_sspp_impl(scene, a, max_batch, out, false);
+}
+
+int sspp::job_create_sspp_async(const sspp_scene* scene, const sspp_sspp_args* a, int64_t max_batch, sspp_job** out) {
+    return job_create_sspp_impl(scene, a, max_batch, out, true);
+}
+
+static int job_create_sspp_impl(const sspp_scene* scene, const sspp_sspp_args* a, int64_t max_batch,
+                                sspp_job** out, bool async_prepass) {
     sspp::clear_error();
+    const auto t_create = std::chrono::steady_clock::now();
     if (!a || !out || !a->knots || !a->init_ctrl || !a->limits)
         return sspp::set_error(SSPP_E_INVAL, "sspp_job_create_sspp: null argument");
     const int D = a->dof, p = a->degree, n = a->n_ctrl, W = a->check_points;
@@ -798,7 +957,8 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
     j->h_stage.insert(j->h_stage.end(), a->limits, a->limits + D);
     // hit order only for jobs that sample (sigma > 0): a scoring job's candidates are the caller's
     const int order = a->sigma != 0.0 ? 2 : 1;
-    if ((rc = set_job_tables(j, a->init_ctrl, a->sigma, a->limits, order, true, nullptr))) {
+    if ((rc = set_job_tables(j, a->init_ctrl, a->sigma, a->limits, async_prepass ? 1 : order, true, nullptr)) ||
+        (async_prepass && order == 2 && (rc = prepass_start(j, a->init_ctrl, a->sigma, a->limits)))) {
         sspp_job_free(j);
         return rc;
     }
@@ -811,6 +971,7 @@ extern "C" int sspp_job_create_sspp(const sspp_scene* scene, const sspp_sspp_arg
         sspp_job_free(j);
         return sspp::set_error(SSPP_E_NOMEM, "hipMalloc block partials");
     }
+    j->create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_create).count();
     *out = j;
     return SSPP_OK;
 }
@@ -838,6 +999,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     if (steps < 1 || steps > kMaxSteps || (steps > 1 && d_ctrl))
         return sspp::set_error(SSPP_E_INVAL, "steps per launch: 1..64 (sampled candidates)");
     hipStream_t st = (hipStream_t)stream;
+    if (j->prepass_state.load(std::memory_order_relaxed) == 2) prepass_apply(j);
     int nt, g1;
     c2f_shape(j, (int64_t)steps * B, &nt, &g1);
     const int n = j->n, D = j->D, p = j->p;
@@ -879,7 +1041,11 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     c.r0 = r0; c.r1 = r1;
     c.nt = nt; c.lds = (int)lds;
     c.ctrl_feas = j->ctrl_feas;
-    j->last_nt = nt; j->last_g1 = g1;
+    const double feps = j->f32 && c.has_scene ? f32_eps(j->scene, d_ctrl ? j->h_pairs : j->h_pairs_s) : 0.0;
+    c.f32 = feps > 0.0 ? 1 : 0;
+    c.feps = (float)feps;
+    c.fplim = kF32PosLimit;
+    j->last_nt = nt; j->last_g1 = g1; j->last_f32 = c.f32;
     SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
     const int nb = nblk * steps;
     hipError_t e = hipErrorInvalidValue;
@@ -946,6 +1112,7 @@ extern "C" int sspp_job_update_sspp(sspp_job* j, const double* init_ctrl, double
     HIPCHK(hipMemcpyAsync(j->d_init, pv, sizeof(double) * nd, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(j->d_limits, pv + nd, sizeof(double) * j->D, hipMemcpyHostToDevice, st));
     if (pairs) {
+        ++j->tables_gen;  // a pre-pass still running ordered the previous values' tables
         const int rc = set_job_tables(j, init_ctrl, sigma, limits, j->pair_order == 0 ? 0 : 1, false, stream, vbytes);
         if (rc) return rc;
     }
@@ -977,6 +1144,7 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
             return SSPP_OK;
         case SSPP_OPT_ORDER: {
             if (j->kind != 0 || value < 0 || value > 2) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_ORDER: 0, 1 or 2");
+            prepass_drop(j);
             HIPCHK(hipDeviceSynchronize());  // earlier launches may still read the tables
             const size_t nd = (size_t)j->n * j->D;
             return set_job_tables(j, j->h_stage.data(), j->sigma, j->h_stage.data() + nd, (int)value, true, nullptr);
@@ -988,6 +1156,10 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
         case SSPP_OPT_TSP_GENERIC:
             if (j->kind != 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_GENERIC: TaskSpacePlanner jobs only");
             j->tsp_generic = value ? 1 : 0;
+            return SSPP_OK;
+        case SSPP_OPT_F32:
+            if (j->kind != 0 || value < 0 || value > 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_F32: 0 or 1");
+            j->f32 = (int)value;
             return SSPP_OK;
     }
     return sspp::set_error(SSPP_E_INVAL, "unknown or read-only option");
@@ -1008,6 +1180,10 @@ extern "C" int sspp_job_get_option(const sspp_job* j, int key, int64_t* value) {
         case SSPP_OPT_PREPASS_US: *value = (int64_t)(j->prepass_ms * 1e3); return SSPP_OK;
         case SSPP_OPT_NPAIRS: *value = j->np_samp; return SSPP_OK;
         case SSPP_OPT_CYLBOX: *value = j->cb_samp; return SSPP_OK;
+        case SSPP_OPT_F32: *value = j->f32; return SSPP_OK;
+        case SSPP_OPT_LAST_F32: *value = j->last_f32; return SSPP_OK;
+        case SSPP_OPT_CREATE_US: *value = (int64_t)(j->create_ms * 1e3); return SSPP_OK;
+        case SSPP_OPT_PREPASS_STATE: *value = j->prepass_state.load(std::memory_order_acquire); return SSPP_OK;
     }
     return sspp::set_error(SSPP_E_INVAL, "unknown option");
 }
@@ -1191,10 +1367,18 @@ extern "C" int sspp_job_info(const sspp_job* j, int* lpc, int* cpb_out, int* thr
 
 extern "C" void sspp_job_free(sspp_job* j) {
     if (!j) return;
+    prepass_drop(j);
+    if (j->pre_stream) (void)hipStreamSynchronize(j->pre_stream);
+    for (void* q : j->retired) if (q) (void)hipFree(q);
+    for (void* q : {(void*)j->d_hits, (void*)j->d_census_pairs}) if (q) (void)hipFree(q);
+    if (j->h_hits) (void)hipHostFree(j->h_hits);
+    if (j->pre_ev) (void)hipEventDestroy(j->pre_ev);
+    if (j->pre_stream) (void)hipStreamDestroy(j->pre_stream);
     for (double* p : {j->d_knots, j->d_tab, j->d_init, j->d_limits, j->d_Minv, j->d_mean, j->d_sigma})
         if (p) (void)hipFree(p);
     if (j->d_span) (void)hipFree(j->d_span);
     if (j->d_otab) (void)hipFree(j->d_otab);
+    if (j->d_otab32) (void)hipFree(j->d_otab32);
     if (j->d_pairs) (void)hipFree(j->d_pairs);
     if (j->d_pairs_s) (void)hipFree(j->d_pairs_s);
     if (j->d_ospan) (void)hipFree(j->d_ospan);

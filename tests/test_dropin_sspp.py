@@ -215,3 +215,92 @@ def test_static_contacts_count_like_the_reference(sp):
     assert planner.initializePath(start, end, init, 10)
     arc, feas = O.sspp_score(osc, init.knots(), 3, init.ctrls().T.copy()[None], 32, count_static=True)
     assert not feas.any()
+
+
+def _planner_plan(L, pl, start, end, sigma, B, W, n, seed):
+    """sspp_planner_plan through the C ABI: (feasible ids, their arcs, their control points, best)."""
+    import ctypes as C
+    from sspp_amd import _lib
+    d = C.POINTER(C.c_double)
+    st, en, lim = (np.ascontiguousarray(x, dtype=np.float64) for x in (start, end, np.ones(7)))
+    knots = np.zeros(n + 4)
+    nf = C.c_int64()
+    ids = np.zeros(B, dtype=np.int64)
+    arcs = np.zeros(B)
+    ctrl = np.zeros((B, n, 7))
+    best = _lib.Best()
+    _lib.check(L.sspp_planner_plan(pl, st.ctypes.data_as(d), en.ctypes.data_as(d), sigma, lim.ctypes.data_as(d),
+                                   B, W, n, seed, 0, knots.ctypes.data_as(d), C.byref(nf),
+                                   ids.ctypes.data_as(C.POINTER(C.c_int64)), arcs.ctypes.data_as(d),
+                                   ctrl.ctypes.data_as(d), C.byref(best)), "sspp_planner_plan")
+    k = nf.value
+    return ids[:k], arcs[:k], ctrl[:k], knots, (best.cost, best.index, best.count)
+
+
+def _prepass_state(L, pl):
+    import ctypes as C
+    from sspp_amd import _lib
+    v = C.c_int64()
+    _lib.check(L.sspp_planner_get_option(pl, _lib.OPT_PREPASS_STATE, C.byref(v)), "get_option")
+    return v.value
+
+
+def _check_plan(osc, res, start, end, sigma, B, W, n, seed):
+    import sspp_amd as S
+    ids, arcs, ctrl, knots, best = res
+    u = np.array([i / (n - 1) for i in range(n)])
+    k2, ctrl0 = S.interpolate(np.array([(1 - t) * start + t * end for t in u]), 3, u)
+    np.testing.assert_array_equal(knots, k2)
+    cand = O.sample_sspp(ctrl0, 3, sigma, np.ones(7), seed, 0, B)
+    arc, feas = O.sspp_score(osc, knots, 3, cand, W)
+    fid = np.nonzero(feas)[0]
+    assert list(ids) == list(fid)
+    np.testing.assert_array_equal(ctrl, cand[fid])
+    assert np.abs(arcs - arc[fid]).max(initial=0.0) <= 1e-12
+    idx, bc = O.argmin(arc, feas)
+    assert best[1] == idx and best[2] == len(fid)
+
+
+def test_first_plan_prepass_runs_asynchronously(cuda):
+    """The drop-in planner's first plan() creates its job with the hit-order pre-pass off the
+    call's path: the call scans in gap / bisection order, the census lands on its own stream,
+    and a later launch swaps the hit order in.  Every call equals the oracle, including a call
+    that re-targets the job (new start / end) after the pre-pass landed but before it was
+    applied — that call may take only the waypoint order, since the pre-pass's pair tables are
+    the creation's reachable subset."""
+    import time
+    import sspp_amd as S
+    from sspp_amd import _lib
+    import ctypes as C
+    L = _lib.lib()
+    model = S.Model(ROBOCRANE)
+    scene = S.Scene(model, 0, 7)
+    osc = O.Scene(mjcf_ref.load(ROBOCRANE), 0, 7)
+    s0 = np.array([0.5, 0.15, 0.136, 0.707, 0, 0, 0.707])
+    e0 = np.array([0.5, -0.05, 0.136, 0.707, 0, 0, 0.707])
+    s1 = s0 + np.array([0, 0, 0.05, 0, 0, 0, 0])
+    for retarget in (False, True):
+        pl = C.c_void_p()
+        _lib.check(L.sspp_planner_create(scene.handle, 7, C.byref(pl)), "planner create")
+        try:
+            B, W, n = 4096, 128, 10
+            r = _planner_plan(L, pl, s0, e0, 0.08, B, W, n, 11)
+            assert _prepass_state(L, pl) in (1, 2)  # running or landed, not applied yet
+            _check_plan(osc, r, s0, e0, 0.08, B, W, n, 11)
+            t0 = time.time()
+            while _prepass_state(L, pl) != 2 and time.time() - t0 < 30:
+                time.sleep(0.01)
+            assert _prepass_state(L, pl) == 2
+            st = s1 if retarget else s0
+            r = _planner_plan(L, pl, st, e0, 0.08, B, W, n, 12)
+            assert _prepass_state(L, pl) == 3  # applied at this call's launch
+            _check_plan(osc, r, st, e0, 0.08, B, W, n, 12)
+            v = C.c_int64()
+            _lib.check(L.sspp_planner_get_option(pl, _lib.OPT_WP_ORDER, C.byref(v)), "wp order")
+            assert v.value == 2
+            _lib.check(L.sspp_planner_get_option(pl, _lib.OPT_ORDER, C.byref(v)), "pair order")
+            assert v.value == (1 if retarget else 2)
+            r = _planner_plan(L, pl, s0, e0, 0.1, B, W, n, 13)
+            _check_plan(osc, r, s0, e0, 0.1, B, W, n, 13)
+        finally:
+            L.sspp_planner_free(pl)

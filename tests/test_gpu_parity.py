@@ -139,6 +139,40 @@ def test_score_ctrl_mode_matches_oracle(robocrane, nt, g1):
     assert S.decode_best(out["best"])[1] == O.argmin(arc_o, feas_o)[0]
 
 
+@pytest.mark.parametrize("nt,g1", [(0, 0), (128, 4), (64, 4), (256, 64)])
+@pytest.mark.parametrize("sigma,B,W", [(0.08, 4096, 128), (0.2, 4096, 128), (0.08, 2048, 256)])
+def test_fp32_filter_is_invisible(robocrane, nt, g1, sigma, B, W):
+    """The FP32-filtered scan (SSPP_OPT_F32, default on; sspp_filter.h) against the all-FP64 scan
+    on the same candidates: arcs, feasibility and the argmin record bit-identical, in sample mode
+    and for caller splines (endpoints perturbed: positions and quaternions everywhere).  sigma 0.2
+    puts many more candidates near contact than the bench's 0.08."""
+    import sspp_amd as S
+    import torch
+    _, scene, _ = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    res = {}
+    for f32 in (1, 0):
+        job = S.SsppJob(scene, knots, 3, ctrl0, sigma, np.ones(7), W, seed=0x5EED, max_batch=B)
+        set_shape(job, nt, g1)
+        job.set_option(S.OPT_F32, f32)
+        r = run_sspp(job, B, first=3000)
+        assert job.get_option(S._lib.OPT_LAST_F32) == f32  # the filter ran (or not)
+        ctrl = ctrl0[None] + np.random.default_rng(11).normal(0, sigma, size=(B, 10, 7))
+        out = job.alloc(B)
+        job.score_ctrl(torch.from_numpy(ctrl).cuda(), 0, out["arc"], out["feasible"], out["best"])
+        torch.cuda.synchronize()
+        res[f32] = (r, _np(out["arc"]), _np(out["feasible"]), S.decode_best(out["best"]))
+    (a, aarc, afeas, abest), (b, barc, bfeas, bbest) = res[1], res[0]
+    np.testing.assert_array_equal(a["ctrl"], b["ctrl"])
+    np.testing.assert_array_equal(a["feasible"], b["feasible"])
+    np.testing.assert_array_equal(a["arc"], b["arc"])
+    assert a["best"] == b["best"]
+    np.testing.assert_array_equal(afeas, bfeas)
+    np.testing.assert_array_equal(aarc, barc)
+    assert abest == bbest
+    assert 0 < int(a["feasible"].sum()) < B and 0 < int(afeas.sum()) < B  # both outcomes occur
+
+
 def test_config1_bsplines_golden(cuda, golden):
     """Config 1: 2-DoF, 64 x 50, no collision, knots/ctrl from the reference's BSplines.py."""
     import sspp_amd as S

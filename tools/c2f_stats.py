@@ -34,6 +34,7 @@ v = list(buf)
 n = v[7]
 names = {0: "p1_wave_pair_iters", 1: "p1_lane_pair_tests", 2: "near_lane_tests(all)", 4: "p2_wave_pair_iters",
          5: "p2_lane_pair_tests", 6: "p1_survivors", 7: "candidates", 9: "p1_wave_narrowphase_iters",
-         10: "p2_wave_narrowphase_iters"}
+         10: "p2_wave_narrowphase_iters", 13: "f32_wave_pair_iters", 3: "f32_lanes_past_culls",
+         11: "p1_f64_fallback_lanes", 12: "p2_f64_fallback_lanes"}
 print(json.dumps({names[i]: (v[i] / n if i != 7 else n) for i in names}, indent=1))
 print("per candidate; feasible:", float(out["feasible"].float().mean()))
