@@ -39,7 +39,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 # kernel revision: PMC records (profiles/*_latest.json) measured on another revision of the
 # kernels are not attached to a line (tools/update_latest.py stamps them)
-KERNEL_REV = "r04"
+KERNEL_REV = "r05"
 FP64_PEAK_TFLOPS = 78.6    # FP64 vector (VALU) spec
 
 
@@ -81,6 +81,10 @@ def parse(argv=None):
     ap.add_argument("--scan", default="fp32", choices=["fp32", "fp64"],
                     help="robocrane: k_sspp_c2f's FP32-filtered scan (default; FP64 decides whatever "
                          "FP32 cannot certify, results identical) or the all-FP64 scan (A/B)")
+    ap.add_argument("--split", type=int, default=1, choices=[0, 1],
+                    help="robocrane: split multi-step launches (k_sspp_c2f's workgroups queue their "
+                         "phase-1 survivors and finish queued survivors; default) or each workgroup "
+                         "finishes its own (A/B; results identical)")
     ap.add_argument("--chunk", type=int, default=80, help="native mode: steps per executor call")
     ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="native mode: independent steps (each its own B candidates, outputs and "
@@ -122,6 +126,7 @@ def setup_robocrane(args, device):
             j.set_shape(nt, g1)
     for j in jobs:
         j.set_option(S.OPT_F32, 1 if args.scan == "fp32" else 0)
+        j.set_option(S.OPT_SPLIT, args.split)
     bufs = [j.alloc(B, device=device) for j in jobs]
     job = jobs[0]
 

@@ -240,6 +240,12 @@ void sspp_job_free(sspp_job* job);
 #define SSPP_OPT_CREATE_US 15   /* get: host microseconds of the job's creation                  */
 #define SSPP_OPT_PREPASS_STATE 16 /* get: asynchronous hit-order pre-pass (the drop-in planner's
                                    jobs): 0 none, 1 running, 2 landed, 3 applied / dropped      */
+#define SSPP_OPT_SPLIT 17       /* multi-step launches of >= 16384 sampled candidates that fit one
+                                   resident round (single-geom movers, no cylinder-box pairs): 1
+                                   (default) k_sspp_c2f's workgroups queue their phase-1 survivors
+                                   and finish queued survivors, whoever sampled them; 0 each
+                                   workgroup finishes its own.  Results identical either way      */
+#define SSPP_OPT_LAST_SPLIT 18  /* get: the last launch was split                                */
 int sspp_job_set_option(sspp_job* job, int key, int64_t value);
 int sspp_job_get_option(const sspp_job* job, int key, int64_t* value);
 

@@ -11,7 +11,7 @@ import os
 
 SCENE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scenes")
 
-from ._lib import (OPT_CES_FUSED, OPT_F32, OPT_ORDER, OPT_SHAPE_G1, OPT_SHAPE_NT, OPT_TSP_FORM,  # noqa: E402
+from ._lib import (OPT_CES_FUSED, OPT_F32, OPT_ORDER, OPT_SPLIT, OPT_SHAPE_G1, OPT_SHAPE_NT, OPT_TSP_FORM,  # noqa: E402
                    OPT_TSP_GENERIC, SsppError)
 from .runtime import (DEFAULT_SEED, SAMPLER_FP32, SAMPLER_FP64, CesPlanner, Model, Scene, SsppJob, SsppSteps, TspJob,  # noqa: E402
                       all_gather_records, best_tensor, decode_best, device_count, interpolate,

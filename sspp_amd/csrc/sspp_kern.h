@@ -39,6 +39,8 @@ __device__ unsigned long long g_c2f_stats[16];
 __device__ unsigned long long g_wg_t[1 << 18];
 __device__ unsigned long long g_wg_ph[8 << 16];  // per workgroup: shader clock after each phase
 #define WG_PH(k) do { if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_wg_ph[8 * blockIdx.x + (k)] = clock64(); } while (0)
+__device__ unsigned long long g_p2_t[8 << 12];  // split launch: [4095] the last arriver's epilogue (start, end, grid)
+__device__ unsigned long long g_p2_w[8 << 13];  // split launch per queue slot: start, end (wall), passes, FP64 passes, feasible, p2/p3 clocks, wave
 #else
 #define WG_PH(k) do { } while (0)
 #endif
@@ -867,6 +869,71 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
 //   phase 3  arc length of the collision-free candidates, in the canonical reduction order of
 //            oracle/sspp_oracle.c::or_canon_sum;
 //   phase 4  block argmin + the fused batch argmin (finish_batch).
+//   split    (multi-step throughput launches) survivors go through the launch's survivor queue.
+// ---------------------------------------------------------------- split launch: the survivor queue
+// A split k_sspp_c2f launch (multi-step throughput launches) does not finish its
+// phase-1 survivors in the workgroup that sampled them: each workgroup appends its survivors to
+// a job-owned queue (rows written through to the coherent level, then a ready word per slot),
+// writes the final outputs of the others, and then every workgroup of the launch pops survivors,
+// one at a time, until the queue is empty (surv_finish: phase 2 in passes of NT waypoints, phase
+// 3, the outputs).  A survivor therefore runs on whichever workgroup is free, in parallel with
+// the others, instead of in sequence behind its workgroup's other survivors (the one-round tail
+// of a 20-step launch).  The queue is sharded (workgroup b produces into and consumes from
+// shard b % 64).  A workgroup pops with a ticket (one fetch-add on the shard's taken counter: a
+// compare-and-swap pop serialises a shard's consumers on the atomic's round trip, 93 vs 61 us) and
+// waits until its slot is reserved, or leaves once every producer of the shard has pushed and
+// the ticket is past the final count.  Waiting is deadlock-free because the launch is one
+// resident round (c2f_one_round: every producer runs to its push whatever the consumers do);
+// kLingerTicks only guards against a hang if that ever failed, counting the abandoned tickets.
+// A reserved slot's producer is resident (it reserved the slot) and sets the ready word shortly.
+// Each step's argmin: a feasible survivor takes part in an agent-scope atomicMin on its arc's bits
+// (non-negative doubles order like their bits) and the feasible count; one whose arc was not
+// above the minimum it saw is listed; the last workgroup to finish (sharded arrival counters, as
+// finish_batch) picks the lowest global id at each step's minimum from that list, writes the
+// records and re-arms the queue for the next launch on the job's stream.
+constexpr unsigned long long kLingerTicks = 1000000;  // 10 ms of the 100 MHz wall clock (a hang guard)
+#ifndef SSPP_QUEUE_WAITERS  // tickets per shard that may wait for slots not reserved yet
+#define SSPP_QUEUE_WAITERS 4
+#endif
+#ifndef SSPP_LINGER_SLEEP  // s_sleep between a waiting wave's polls (x 64 clocks)
+#define SSPP_LINGER_SLEEP 16
+#endif
+constexpr int kSurvShards = 64;      // queue shards: workgroup b produces into and consumes from b % 64
+struct SurvShard {
+    unsigned count;                    // slots reserved by the shard's producers
+    unsigned taken;                    // slots popped by its consumers
+    unsigned pushed;                   // producers whose slots are all ready
+    unsigned pad[29];                  // own 128-byte line
+};
+struct SurvQ {
+    SurvShard shard[kSurvShards];
+    unsigned nlist;                    // entries of the argmin list (SurvPtrs::res)
+    unsigned lost;                     // tickets abandoned by the hang guard (0 on a resident launch)
+    unsigned pad2[30];
+    unsigned arrive_sh[8][32];         // arrival counters (8 shards, own cache lines)
+    unsigned arrive_top[32];
+    unsigned long long bestbits[kMaxSteps];  // per step: min arc of a feasible survivor (bits)
+    unsigned count_feas[kMaxSteps];    // per step: feasible survivors
+};
+// a slot's ready word: bit 63 ready, bit 62 undecided cylinder-box pair, bits 32..39 the step of
+// the launch, bits 0..31 the candidate within the step (0: not ready; re-armed by its consumer)
+__host__ __device__ inline unsigned long long surv_word(int step, long long lc, bool defer) {
+    return (1ull << 63) | ((unsigned long long)defer << 62) | ((unsigned long long)(unsigned)step << 32) |
+           (unsigned long long)(unsigned)lc;
+}
+struct SurvBest {                      // the argmin list: a feasible arc not above the minimum it saw
+    unsigned long long bits, id, step, pad;
+};
+struct SurvPtrs {
+    SurvQ* hdr;
+    unsigned long long* rec;  // [cap] ready words
+    double* ctrl;      // [cap][nrd]  the survivors' own control-point rows
+    float* ctrl32;     // [cap][nrd]  their FP32 copies
+    SurvBest* res;     // [cap]       the argmin list (SurvQ::nlist entries)
+    long long cap;
+    int shard_cap;     // slots per shard: shard s owns [s * shard_cap, (s + 1) * shard_cap)
+};
+
 struct SsppC2F {
     KScene sc;
     int has_scene;
@@ -894,6 +961,8 @@ struct SsppC2F {
     // fplim = the largest |mover root coordinate| it is certified for
     int f32;
     float feps, fplim;
+    int split;     // the survivor queue (SurvQ) instead of phases 2-4 in the workgroup
+    int nsteps;    // steps in this launch
 };
 
 #ifdef SSPP_C2F_STATS
@@ -1257,6 +1326,123 @@ __device__ SSPP_CB_INLINE bool c2f_cb_exact(const double* sm, int mine, int fix,
     return false;
 }
 
+// One queued survivor, finished by the whole workgroup (the split launch's consumers, see SurvQ):
+// phase 2 over waypoints j0 .. npts-1 of the job's order in passes of NT (a colliding survivor
+// usually stops after its first pass; 124 remaining waypoints are one pass of the 128-thread
+// shape), phase 3 in k_sspp_c2f's canonical order (each wave its 64-lane groups), the outputs and
+// the step's argmin candidates.  Its rows are at o_own of smem / s_f32; s_ctl holds [feasible,
+// defer], s_vsum the group sums.  Every thread calls it (it synchronises).
+template <int D, int NM, int P, bool ONEGEOM, int NT>
+__device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, const double* __restrict__ otab,
+                                            const float* __restrict__ otab32, const int* __restrict__ ospan,
+                                            const double* __restrict__ atab, const int* __restrict__ aspan,
+                                            const double* smem, const float* s_f32, int o_fix, int o_own, int* s_ctl,
+                                            double* s_vsum, unsigned long long word, unsigned slot,
+                                            double* __restrict__ arc, unsigned char* __restrict__ feasible,
+                                            bool with_best, const SurvPtrs& q) {
+    constexpr int P1 = P + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int r0 = a.r0, r1 = a.r1, nch = a.W - 1;
+    const int step = (int)((word >> 32) & 0xFFu), lc = (int)(unsigned)word;
+    const int j0 = a.n1, R = a.npts - j0;
+#ifdef SSPP_WG_TIMING
+    const unsigned long long w_t0 = wall_clock64(), c0 = clock64();
+    unsigned w_np = 0, w_nf = 0;
+#endif
+    for (int jb = 0; jb < R; jb += NT) {  // workgroup-uniform
+        // a uniform exit once a pass has found a contact (every thread's read precedes the barrier)
+        if (jb > 0 && !__syncthreads_or(__hip_atomic_load(s_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+            break;
+        const int jj = jb + tid;
+        const bool live = jj < R;
+        const int j = j0 + (live ? jj : 0);
+        if (__ballot(live) == 0ull) continue;
+        bool h;
+        if (a.f32) {
+            float q32[D], N32[P1];
+#pragma unroll
+            for (int r = 0; r < P1; ++r) N32[r] = otab32[j * P1 + r];
+            eval_split32<D, P>(s_f32, o_own, o_fix, r0, r1, N32, ospan[j], q32);
+            unsigned long long amb;
+            h = scan_pairs32<D, NM, ONEGEOM>(q32, live, ~0ull, ~0ull, ~0ull, a.sc, TT, a.feps, a.fplim, amb);
+            const bool need = live && !h && amb != 0ull;
+            if (__ballot(need) != 0ull && __ballot(h) == 0ull) {  // one contact decides the survivor
+#ifdef SSPP_WG_TIMING
+                ++w_nf;
+#endif
+                double qd[D];
+                bool dfr = false;
+                eval_split_g<D, P>(smem, o_own, o_fix, r0, r1, otab + j * P1, ospan[j], qd);
+                h = scan_pairs<D, NM, ONEGEOM>(qd, need, amb, wave_or64(need ? amb : 0ull), ~0ull, nullptr, a.sc,
+                                               TT, dfr) || h;
+            }
+        } else {
+            double qd[D];
+            bool dfr = false;
+            eval_split_g<D, P>(smem, o_own, o_fix, r0, r1, otab + j * P1, ospan[j], qd);
+            h = scan_pairs<D, NM, ONEGEOM>(qd, live, ~0ull, ~0ull, ~0ull, nullptr, a.sc, TT, dfr);
+        }
+        if (__ballot(h) != 0ull && lane == 0) __hip_atomic_store(s_ctl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef SSPP_WG_TIMING
+        ++w_np;
+#endif
+    }
+    __syncthreads();
+    const bool feas = s_ctl[0] != 0;
+#ifdef SSPP_WG_TIMING
+    const unsigned long long c1 = clock64();
+#endif
+    double total = INFINITY;
+    if (feas) {
+        // phase 3: lane partials over lpc lanes, xor butterfly per 64-lane group, groups in order
+        const int lpc = a.lpc, nvw = lpc >> 6;
+        for (int vw = wv; vw < nvw; vw += NT / 64) {  // wave-uniform
+            double acc = 0.0;
+            for (int base = vw * 64; base < nch; base += lpc) {
+                const int jc = base + lane, jj = jc < nch ? jc : nch - 1;
+                double qa[D], qb[D];
+                eval_split_g<D, P>(smem, o_own, o_fix, r0, r1, atab + (jj + 1) * P1, aspan[jj + 1], qb);
+#pragma unroll
+                for (int d = 0; d < D; ++d) qa[d] = __shfl_up(qb[d], 1, 64);
+                if (lane == 0) eval_split_g<D, P>(smem, o_own, o_fix, r0, r1, atab + jj * P1, aspan[jj], qa);
+                if (jc < nch) acc = acc + dist_nd<D>(qa, qb);
+            }
+            acc = wave_sum(acc);
+            if (lane == 0) s_vsum[vw] = acc;
+        }
+        __syncthreads();
+        total = s_vsum[0];
+        for (int w = 1; w < nvw; ++w) total = total + s_vsum[w];
+    }
+    if (tid == 0) {
+        const long long c = (long long)step * a.B + lc;
+        arc[c] = total;
+        feasible[c] = (unsigned char)feas;
+        if (with_best) {
+            if (feas && total < INFINITY) {
+                const unsigned long long bits = (unsigned long long)__double_as_longlong(total);
+                const unsigned long long seen =
+                    __hip_atomic_fetch_min(q.hdr->bestbits + step, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (bits <= seen) {  // may be the step's minimum: listed for the last arriver
+                    const unsigned k = __hip_atomic_fetch_add(&q.hdr->nlist, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&q.res[k].bits, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&q.res[k].id, (unsigned long long)(a.first_id + step * a.step_stride + lc),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&q.res[k].step, (unsigned long long)step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (feas) __hip_atomic_fetch_add(q.hdr->count_feas + step, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#ifdef SSPP_WG_TIMING
+        unsigned long long* t = g_p2_w + 8 * (slot & ((8u << 10) - 1u));
+        t[0] = w_t0; t[1] = wall_clock64(); t[2] = w_np; t[3] = w_nf; t[4] = feas;
+        t[5] = c1 - c0; t[6] = clock64() - c1; t[7] = blockIdx.x;
+#endif
+    }
+    (void)slot;
+    __syncthreads();  // the next survivor may overwrite the rows and the flags
+}
+
 // Occupancy per shape: one-wave workgroups of a single-geom mover at 5 waves per SIMD (96 VGPRs,
 // no spill: 20 workgroups per CU, so a 20-step launch of 4096-candidate steps is one resident
 // round); 4-wave workgroups and multi-geom movers at 4 (128 VGPRs; at 5 they spill).
@@ -1276,7 +1462,10 @@ __device__ SSPP_CB_INLINE bool c2f_cb_exact(const double* sm, int mine, int fix,
 #endif
 // CBX: the pair table has cylinder-box pairs, so the kernel carries the settle step (its
 // out-of-line exact test costs the whole kernel registers: 96 -> 128 VGPRs and scratch)
-template <int D, int NM, int P, bool ONEGEOM, int NT, bool CBX>
+// SPLIT: the split launch's instance (single-geom movers without cylinder-box pairs): phase 1,
+// then the survivor queue; the in-workgroup phases 2-4 are unreachable there and compiled out, so
+// the queue costs the unsplit instances no registers
+template <int D, int NM, int P, bool ONEGEOM, int NT, bool CBX, bool SPLIT = false>
 #ifndef SSPP_C2F_FIVE_MAX  // profiling builds: the largest workgroup at SSPP_C2F_WAVES_PER_EU
 #define SSPP_C2F_FIVE_MAX 128
 #endif
@@ -1289,7 +1478,8 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     const double* __restrict__ atab, const int* __restrict__ aspan,
     const double* __restrict__ init_ctrl, const double* __restrict__ limits,
     const double* __restrict__ ctrl_in, double* __restrict__ ctrl_out, double* __restrict__ arc,
-    unsigned char* __restrict__ feasible, BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    unsigned char* __restrict__ feasible, BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best,
+    SurvPtrs q) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int P1 = P + 1;
     constexpr int NB = 3 * NM;  // AABB extents per candidate (x, y, z per mover)
@@ -1307,6 +1497,9 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     int wg_ns = -1;
 #endif
     WG_PH(0);
+    double* const arc_base = arc;  // the split launch's consumers write any step's outputs
+    unsigned char* const feas_base = feasible;
+    sspp_best* const best_base = best;
     if (step) {
         arc += step * a.B;
         feasible += step * a.B;
@@ -1435,6 +1628,191 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     }
     __syncthreads();
     WG_PH(3);
+    if constexpr (SPLIT) {
+        static_assert(NM == 1 && ONEGEOM && !CBX, "split launches: single-geom movers without cylinder-box pairs");
+        // ---- producer: one queue reservation per workgroup (survivors in candidate order), the
+        // survivors' rows written through to the coherent level, then each slot's ready word; the
+        // other candidates' outputs are final here
+        if (tid < 64) {
+            const bool f = tid < nvalid && s_feas[tid] != 0;
+            const unsigned long long m = __ballot(f);
+            unsigned base = 0;
+            if (tid == 0 && m)
+                base = __hip_atomic_fetch_add(&q.hdr->shard[blockIdx.x % kSurvShards].count, (unsigned)__popcll(m),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            base = (unsigned)__shfl((int)base, 0, 64) + (unsigned)((blockIdx.x % kSurvShards) * q.shard_cap);
+            if (tid < cpb) s_surv[tid] = f ? (int)(base + __popcll(m & ((1ull << tid) - 1ull))) : -1;
+        }
+        __syncthreads();
+        for (int e = tid; e < nvalid * nrd; e += NT) {
+            const int sl = e / nrd, r = e - sl * nrd, slot = s_surv[sl];
+            if (slot >= 0) {
+                const long long o = (long long)slot * nrd + r;
+                __hip_atomic_store((unsigned long long*)q.ctrl + o,
+                                   (unsigned long long)__double_as_longlong(smem[o_own + sl * nrd + r]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned*)q.ctrl32 + o, __float_as_uint(s_f32[o_own + sl * nrd + r]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's row stores are done
+        __syncthreads();                                   // ... and every other thread's
+        if (tid < nvalid) {
+            const int slot = s_surv[tid];
+            if (slot >= 0) {
+                __hip_atomic_store(q.rec + slot, surv_word(step, cand0 + tid, s_defer[tid] != 0), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                arc[tid + cand0] = INFINITY;
+                feasible[tid + cand0] = 0;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ready words are stored
+        __syncthreads();  // the rows in LDS are free: each wave finishes survivors in its own slot
+        if (tid == 0)
+            __hip_atomic_fetch_add(&q.hdr->shard[blockIdx.x % kSurvShards].pushed, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        // ---- consumers: every workgroup pops survivors until the queue is empty
+        {
+            const unsigned nb_all = gridDim.x, shs = blockIdx.x % kSurvShards;
+            const unsigned nwg_s = (nb_all - shs + kSurvShards - 1) / kSurvShards;  // producers of the shard
+            SurvShard* const sh = q.hdr->shard + shs;
+            int* s_ctl = s_surv;  // [0] feasible, [1] slot, [2..3] the ready word
+            for (;;) {  // workgroup-uniform
+                if (tid == 0) {
+                    // a ticket: the shard's next slot in reservation order, reserved now or later —
+                    // unless SSPP_QUEUE_WAITERS tickets already wait for slots not reserved yet:
+                    // then this workgroup leaves (those waiters, and every producer after its
+                    // push, serve the slots still to come; a waiter leaves once the shard is done)
+                    unsigned t = ~0u;
+                    const unsigned tk0 = __hip_atomic_load(&sh->taken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned ct0 = __hip_atomic_load(&sh->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((int)(tk0 - ct0) < SSPP_QUEUE_WAITERS) {
+                        t = __hip_atomic_fetch_add(&sh->taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const unsigned long long w0 = wall_clock64();
+                        for (;;) {
+                            if (t < __hip_atomic_load(&sh->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                            // every producer has pushed (its count is then final), the ticket past it
+                            if (__hip_atomic_load(&sh->pushed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nwg_s &&
+                                __hip_atomic_load(&sh->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= t) {
+                                t = ~0u;
+                                break;
+                            }
+                            if (wall_clock64() - w0 > kLingerTicks) {  // never on a resident launch
+                                __hip_atomic_fetch_add(&q.hdr->lost, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                t = ~0u;
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(SSPP_LINGER_SLEEP);
+                        }
+                    }
+                    unsigned long long w = 0ull;
+                    if (t != ~0u) {  // the producer is resident (it reserved the slot): its word lands shortly
+                        t += shs * (unsigned)q.shard_cap;
+                        while ((w = __hip_atomic_load(q.rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0ull)
+                            __builtin_amdgcn_s_sleep(1);
+                        __hip_atomic_store(q.rec + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+                    }
+                    s_ctl[0] = 1;
+                    s_ctl[1] = (int)t;
+                    s_ctl[2] = (int)(unsigned)(w >> 32);
+                    s_ctl[3] = (int)(unsigned)w;
+                }
+                __syncthreads();
+                const unsigned t = (unsigned)s_ctl[1];
+                if (t == ~0u) break;
+                const unsigned long long w = ((unsigned long long)(unsigned)s_ctl[2] << 32) | (unsigned)s_ctl[3];
+                for (int e = tid; e < nrd; e += NT) {
+                    const long long o = (long long)t * nrd + e;
+                    smem[o_own + e] = __longlong_as_double((long long)__hip_atomic_load(
+                        (unsigned long long*)q.ctrl + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    s_f32[o_own + e] = __uint_as_float(
+                        __hip_atomic_load((unsigned*)q.ctrl32 + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                }
+                __syncthreads();
+                surv_finish<D, NM, P, ONEGEOM, NT>(a, TT, otab, otab32, ospan, atab, aspan, smem, s_f32, o_fix, o_own,
+                                                   s_ctl, s_vsum, w, t, arc_base, feas_base, best_base != nullptr, q);
+            }
+        }
+#ifdef SSPP_WG_TIMING
+        if (tid == 0 && blockIdx.x < (1 << 16)) {
+            g_wg_t[4 * blockIdx.x] = wg_t0;
+            g_wg_t[4 * blockIdx.x + 1] = wall_clock64();
+            g_wg_t[4 * blockIdx.x + 2] = __smid();
+            g_wg_t[4 * blockIdx.x + 3] = 0ull;
+        }
+#endif
+        // ---- completion: sharded arrival, then the last workgroup finishes every step's argmin
+        __syncthreads();
+        const unsigned nblk = gridDim.x;
+        const int sh = blockIdx.x & 7, nsh = nblk < 8 ? (int)nblk : 8;
+        int* s_last = s_surv + cpb;
+        if (tid == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned shard_n = (nblk - sh + 7) >> 3;
+            const unsigned prev = __hip_atomic_fetch_add(&q.hdr->arrive_sh[sh][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int last = 0;
+            if (prev == shard_n - 1) {
+                const unsigned pt = __hip_atomic_fetch_add(&q.hdr->arrive_top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = pt == (unsigned)nsh - 1;
+            }
+            s_last[0] = last;
+        }
+        __syncthreads();
+        if (!s_last[0]) return;
+#ifdef SSPP_WG_TIMING
+        const unsigned long long t_ep = wall_clock64();
+#endif
+        // LDS is free: the per-step minimum bits, ids and feasible counts
+        unsigned long long* s_bits = (unsigned long long*)smem;
+        unsigned long long* s_id = s_bits + kMaxSteps;
+        unsigned* s_cnt = (unsigned*)(s_id + kMaxSteps);
+        const int nsteps = a.nsteps;
+        for (int e = tid; e < nsteps; e += NT) {
+            s_bits[e] = __hip_atomic_load(q.hdr->bestbits + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_cnt[e] = __hip_atomic_load(q.hdr->count_feas + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_id[e] = ~0ull;
+        }
+        __syncthreads();
+        if (best_base) {
+            const unsigned nl = __hip_atomic_load(&q.hdr->nlist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (unsigned i = tid; i < nl; i += NT) {
+                const unsigned long long bits = __hip_atomic_load(&q.res[i].bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long id = __hip_atomic_load(&q.res[i].id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int st = (int)__hip_atomic_load(&q.res[i].step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (bits == s_bits[st]) atomicMin(s_id + st, id);
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < nsteps; e += NT) {
+            if (best_base) {
+                const bool has = s_id[e] != ~0ull;
+                best_base[e].cost = has ? __longlong_as_double((long long)s_bits[e]) : INFINITY;
+                best_base[e].index = has ? (long long)s_id[e] : -1;
+                best_base[e].count = s_cnt[e];
+                best_base[e].reserved = __hip_atomic_load(&q.hdr->lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __hip_atomic_store(q.hdr->bestbits + e, 0x7FF0000000000000ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(q.hdr->count_feas + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (int e = tid; e < kSurvShards; e += NT) {
+            __hip_atomic_store(&q.hdr->shard[e].count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q.hdr->shard[e].taken, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q.hdr->shard[e].pushed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (tid == 0) {
+            for (int k = 0; k < 8; ++k) __hip_atomic_store(&q.hdr->arrive_sh[k][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q.hdr->arrive_top[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q.hdr->nlist, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q.hdr->lost, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef SSPP_WG_TIMING
+            g_p2_t[8 * 4095] = t_ep;
+            g_p2_t[8 * 4095 + 1] = wall_clock64();
+            g_p2_t[8 * 4095 + 2] = gridDim.x;
+#endif
+        }
+        return;
+    }
     // ---- phase 2: survivors' remaining waypoints over the whole workgroup
     const int j0 = a.n1;
     const int R = a.npts - j0;
@@ -2349,6 +2727,16 @@ struct sspp_job {
     DPair* d_census_pairs = nullptr;    // the census's own copy of the sampled table
     std::vector<void*> retired;         // device tables replaced while kernels may still read them
     double create_ms = 0.0;             // host time of sspp_job_create_sspp
+    // split launches: the survivor queue (SurvQ), grown on demand
+    int opt_split = 1;                  // SSPP_OPT_SPLIT
+    int last_split = 0;
+    SurvQ* d_sq_hdr = nullptr;
+    unsigned long long* d_sq_rec = nullptr;
+    double* d_sq_ctrl = nullptr;
+    float* d_sq_ctrl32 = nullptr;
+    SurvBest* d_sq_res = nullptr;
+    long long sq_cap = 0;               // survivors the buffers hold (x sq_nrd doubles each)
+    int sq_nrd = 0;
 };
 
 
@@ -2397,6 +2785,8 @@ struct SsppPtrs {
     double* arc;
     unsigned char* feasible;
     sspp_best* best;
+    SurvPtrs q;  // the split launch's survivor queue (k.split)
+    int* split_used = nullptr;  // out: whether the launch was split (one resident round only)
 };
 
 // the job's pair table: sampled candidates use the reachable subset, caller splines the full one
@@ -2415,20 +2805,46 @@ inline KScene kscene_job(const sspp_job* j, bool sampled) {
     return k;
 }
 
+// the split launch's second kernel: a persistent grid of the chip's resident capacity
+// whether a launch of nblk workgroups is one resident round (the split launch's waiting waves
+// need every producer resident); the occupancy query is cached per (kernel, LDS)
+inline bool c2f_one_round(const sspp_job* j, const void* fn, int nt, int lds, int nblk) {
+    static thread_local const void* c_fn = nullptr;
+    static thread_local int c_lds = -1, c_wgs = 0;
+    if (fn != c_fn || lds != c_lds) {
+        int per_cu = 0, dev = 0, ncu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, (size_t)lds) != hipSuccess ||
+            hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            per_cu = ncu = 0;
+        c_fn = fn; c_lds = lds; c_wgs = per_cu * ncu;
+    }
+    (void)j;
+    return nblk <= c_wgs;
+}
+
 template <int D, int NM, int P, int NT>
-hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
+hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st,
+                         const SurvPtrs& q) {
     const double* atab = j->d_tab + (size_t)(j->W + 1) * (P + 1);
     const int* aspan = j->d_span + (j->W + 1);
     const SceneT T = scene_t_job(j, !o.ctrl_in);
-#define SSPP_LAUNCH_C2F(NMV, OGV, CBV)                                                                    \
-    hipLaunchKernelGGL((k_sspp_c2f<D, NMV, P, OGV, NT, CBV>), dim3(nblk), dim3(NT), k.lds, st, k, T, j->d_otab, \
-                       j->d_otab32, j->d_ospan, atab, aspan, j->d_init, j->d_limits, o.ctrl_in, o.ctrl_out, o.arc,      \
-                       o.feasible, j->d_part, j->d_sync, o.best)
+#define SSPP_LAUNCH_C2F(NMV, OGV, CBV, SPV)                                                               \
+    do {                                                                                                  \
+        SsppC2F kk = k;                                                                                   \
+        kk.split = SPV;                                                                                   \
+        if (o.split_used) *o.split_used = SPV;                                                            \
+        hipLaunchKernelGGL((k_sspp_c2f<D, NMV, P, OGV, NT, CBV, SPV>), dim3(nblk), dim3(NT), kk.lds, st, kk, T, \
+                           j->d_otab, j->d_otab32, j->d_ospan, atab, aspan, j->d_init, j->d_limits, o.ctrl_in,   \
+                           o.ctrl_out, o.arc, o.feasible, j->d_part, j->d_sync, o.best, q);              \
+    } while (0)
     const bool og = NM == 1 && k.sc.onegeom && k.sc.npairs > 0;
-    if (og && k.sc.cylbox) SSPP_LAUNCH_C2F(1, true, true);
-    else if (og) SSPP_LAUNCH_C2F(1, true, false);
-    else if (k.sc.cylbox) SSPP_LAUNCH_C2F(NM, false, true);
-    else SSPP_LAUNCH_C2F(NM, false, false);
+    if (og && k.sc.cylbox) SSPP_LAUNCH_C2F(1, true, true, false);
+    else if (og && k.split && c2f_one_round(j, (const void*)k_sspp_c2f<D, 1, P, true, NT, false, true>, NT, k.lds, nblk))
+        SSPP_LAUNCH_C2F(1, true, false, true);
+    else if (og) SSPP_LAUNCH_C2F(1, true, false, false);
+    else if (k.sc.cylbox) SSPP_LAUNCH_C2F(NM, false, true, false);
+    else SSPP_LAUNCH_C2F(NM, false, false, false);
 #undef SSPP_LAUNCH_C2F
     return hipGetLastError();
 }
@@ -2437,9 +2853,10 @@ hipError_t launch_c2f_nt(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o,
 // (a single plan() batch, latency shape); DESIGN.md §5
 template <int D, int NM, int P>
 hipError_t launch_c2f(const SsppC2F& k, const sspp_job* j, const SsppPtrs& o, int nblk, hipStream_t st) {
-    if (k.nt == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st);
-    if (k.nt == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st);
-    return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st);
+    const SurvPtrs q = o.q;
+    if (k.nt == 64) return launch_c2f_nt<D, NM, P, 64>(k, j, o, nblk, st, q);
+    if (k.nt == 128) return launch_c2f_nt<D, NM, P, 128>(k, j, o, nblk, st, q);
+    return launch_c2f_nt<D, NM, P, 256>(k, j, o, nblk, st, q);
 }
 
 // ---- per-dof entry points, instantiated one dof per translation unit (sspp_inst.hip, built

@@ -989,6 +989,37 @@ static void c2f_shape(const sspp_job* j, int64_t cands, int* nt, int* g1) {
 }
 
 
+// Split launches from this many candidates per launch (the throughput shape's range): below it
+// a launch is one plan() batch, whose workgroups are few enough to finish their own survivors
+constexpr int64_t kSplitMinCands = 16384;
+
+// the survivor queue of split launches: header (counters re-armed by each launch's last
+// workgroup), ready words, the survivors' rows and the argmin list, for `cands` slots of `nrd`
+// own doubles each
+static int survq_reserve(sspp_job* j, int64_t cands, int nrd) {
+    if (!j->d_sq_hdr) {
+        SurvQ h{};
+        for (int s = 0; s < kMaxSteps; ++s) h.bestbits[s] = 0x7FF0000000000000ull;  // +inf
+        HIPCHK(hipMalloc((void**)&j->d_sq_hdr, sizeof(SurvQ)));
+        HIPCHK(hipMemcpy(j->d_sq_hdr, &h, sizeof(SurvQ), hipMemcpyHostToDevice));
+    }
+    if (cands <= j->sq_cap && nrd == j->sq_nrd) return SSPP_OK;
+    HIPCHK(hipDeviceSynchronize());  // earlier launches may still use the old buffers
+    for (void* p : {(void*)j->d_sq_rec, (void*)j->d_sq_ctrl, (void*)j->d_sq_ctrl32, (void*)j->d_sq_res})
+        if (p) (void)hipFree(p);
+    j->d_sq_rec = nullptr; j->d_sq_ctrl = nullptr; j->d_sq_ctrl32 = nullptr; j->d_sq_res = nullptr;
+    j->sq_cap = 0;
+    const size_t n = (size_t)cands, nr = (size_t)std::max(1, nrd);
+    HIPCHK(hipMalloc((void**)&j->d_sq_rec, sizeof(unsigned long long) * n));
+    HIPCHK(hipMemset(j->d_sq_rec, 0, sizeof(unsigned long long) * n));  // ready words: not ready
+    HIPCHK(hipMalloc((void**)&j->d_sq_ctrl, sizeof(double) * n * nr));
+    HIPCHK(hipMalloc((void**)&j->d_sq_ctrl32, sizeof(float) * n * nr));
+    HIPCHK(hipMalloc((void**)&j->d_sq_res, sizeof(SurvBest) * n));
+    j->sq_cap = cands;
+    j->sq_nrd = nrd;
+    return SSPP_OK;
+}
+
 static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t B, double* d_arc,
                     uint8_t* d_feasible, double* d_ctrl_out, sspp_best* d_best, void* stream,
                     int steps = 1, int64_t step_stride = 0) {
@@ -1046,7 +1077,24 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     c.feps = (float)feps;
     c.fplim = kF32PosLimit;
     j->last_nt = nt; j->last_g1 = g1; j->last_f32 = c.f32;
-    SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best};
+    // split launch (the survivor queue, SurvQ): multi-step throughput launches of sampled
+    // candidates with collision, one output row per candidate; launch_c2f_nt
+    // splits only a launch that is one resident round (c2f_one_round)
+    c.nsteps = steps;
+    c.split = j->opt_split && (int64_t)steps * B >= kSplitMinCands && !d_ctrl && !d_ctrl_out && !j->arc_all &&
+              c.has_scene && c.sc.npairs > 0 && !c.sc.static_block && j->nm == 1 && c.sc.onegeom && !c.sc.cylbox &&
+              cpb >= 3;  // the consumers' control words live in s_surv (cpb + 1 ints)
+    SurvPtrs q{};
+    int split_used = 0;
+    if (c.split) {
+        // shard s holds the survivors of workgroups b = s (mod kSurvShards), cpb at most each
+        const int nb_all = nblk * steps;
+        const int shard_cap = ((nb_all + kSurvShards - 1) / kSurvShards) * cpb;
+        int rc = survq_reserve(j, (int64_t)shard_cap * kSurvShards, nrd);
+        if (rc) return rc;
+        q = SurvPtrs{j->d_sq_hdr, j->d_sq_rec, j->d_sq_ctrl, j->d_sq_ctrl32, j->d_sq_res, j->sq_cap, shard_cap};
+    }
+    SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best, q, &split_used};
     const int nb = nblk * steps;
     hipError_t e = hipErrorInvalidValue;
     switch (j->D) {
@@ -1060,6 +1108,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
 #endif
         case 7: e = entry_c2f<7>(c, j, o, nb, st); break;
     }
+    j->last_split = split_used;
     if (e != hipSuccess) return hip_fail(e, "k_sspp_c2f launch");
     return SSPP_OK;
 }
@@ -1161,6 +1210,10 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
             if (j->kind != 0 || value < 0 || value > 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_F32: 0 or 1");
             j->f32 = (int)value;
             return SSPP_OK;
+        case SSPP_OPT_SPLIT:
+            if (j->kind != 0 || value < 0 || value > 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SPLIT: 0 or 1");
+            j->opt_split = (int)value;
+            return SSPP_OK;
     }
     return sspp::set_error(SSPP_E_INVAL, "unknown or read-only option");
 }
@@ -1183,6 +1236,8 @@ extern "C" int sspp_job_get_option(const sspp_job* j, int key, int64_t* value) {
         case SSPP_OPT_F32: *value = j->f32; return SSPP_OK;
         case SSPP_OPT_LAST_F32: *value = j->last_f32; return SSPP_OK;
         case SSPP_OPT_CREATE_US: *value = (int64_t)(j->create_ms * 1e3); return SSPP_OK;
+        case SSPP_OPT_SPLIT: *value = j->opt_split; return SSPP_OK;
+        case SSPP_OPT_LAST_SPLIT: *value = j->last_split; return SSPP_OK;
         case SSPP_OPT_PREPASS_STATE: *value = j->prepass_state.load(std::memory_order_acquire); return SSPP_OK;
     }
     return sspp::set_error(SSPP_E_INVAL, "unknown option");
@@ -1369,6 +1424,9 @@ extern "C" void sspp_job_free(sspp_job* j) {
     if (!j) return;
     prepass_drop(j);
     if (j->pre_stream) (void)hipStreamSynchronize(j->pre_stream);
+    for (void* q : {(void*)j->d_sq_hdr, (void*)j->d_sq_rec, (void*)j->d_sq_ctrl, (void*)j->d_sq_ctrl32,
+                    (void*)j->d_sq_res})
+        if (q) (void)hipFree(q);
     for (void* q : j->retired) if (q) (void)hipFree(q);
     for (void* q : {(void*)j->d_hits, (void*)j->d_census_pairs}) if (q) (void)hipFree(q);
     if (j->h_hits) (void)hipHostFree(j->h_hits);
@@ -1552,6 +1610,16 @@ extern "C" int sspp_debug_wg_times(unsigned long long* out, int n) {
 extern "C" int sspp_debug_wg_phases(unsigned long long* out, int n) {  // 8 per workgroup
     hipDeviceSynchronize();
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wg_ph), sizeof(unsigned long long) * (size_t)n);
+    return 0;
+}
+extern "C" int sspp_debug_p2_times(unsigned long long* out, int n) {  // [8 * 4095]: the split epilogue
+    hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p2_t), sizeof(unsigned long long) * (size_t)n);
+    return 0;
+}
+extern "C" int sspp_debug_p2_waves(unsigned long long* out, int n) {  // 8 per split-queue slot
+    hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p2_w), sizeof(unsigned long long) * (size_t)n);
     return 0;
 }
 #endif

@@ -273,7 +273,8 @@ class SsppJob(_Job):
                     waypoint_order={0: "bisection", 2: "hit"}[g(_lib.OPT_WP_ORDER)],
                     prepass_ms=g(_lib.OPT_PREPASS_US) / 1e3, sampled_pairs=g(_lib.OPT_NPAIRS),
                     cylinder_box=bool(g(_lib.OPT_CYLBOX)),
-                    scan="fp32-filtered" if g(_lib.OPT_LAST_F32) else "fp64")
+                    scan="fp32-filtered" if g(_lib.OPT_LAST_F32) else "fp64",
+                    split=bool(g(_lib.OPT_LAST_SPLIT)))
 
 
 class TspJob(_Job):

@@ -700,3 +700,41 @@ def test_tsp_kernel_forms_identical(cuda, xml, body, B, cp):
     np.testing.assert_array_equal(res["0"]["status"], st)
     fin = np.isfinite(cost)
     assert (np.abs(res["0"]["cost"][fin] - cost[fin]) <= 1e-12 * np.maximum(1.0, np.abs(cost[fin]))).all()
+
+
+@pytest.mark.parametrize("sigma,spl,B", [(0.08, 20, 4096), (0.02, 16, 4096), (0.12, 4, 8192), (0.3, 40, 1024)])
+def test_split_launch_is_invisible(robocrane, sigma, spl, B):
+    """Split launches (SSPP_OPT_SPLIT, default: every workgroup of k_sspp_c2f queues its phase-1
+    survivors and every wave finishes queued survivors) against unsplit launches of the same
+    steps: every output bit-identical — arcs, feasibility and each step's argmin record — over
+    three launches back to back on two streams (the queue re-armed by each launch's last
+    workgroup).  sigma 0.02 leaves most candidates surviving phase 1, 0.3 almost none; at 0.3
+    the sampled pair table reaches more than one geom, which run_sspp never splits."""
+    import sspp_amd as S
+    import torch
+    _, scene, _ = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    G, stride, first = 3 * spl, B, 11 * B
+    out = {}
+    for split in (1, 0):
+        jobs = [S.SsppJob(scene, knots, 3, ctrl0, sigma, np.ones(7), 128, max_batch=B) for _ in range(2)]
+        for j in jobs:
+            j.set_option(S.OPT_SPLIT, split)
+        arcs = [torch.empty(spl * B, dtype=torch.float64, device="cuda") for _ in jobs]
+        feas = [torch.empty(spl * B, dtype=torch.uint8, device="cuda") for _ in jobs]
+        streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+        ex = S.SsppSteps(jobs, streams, B, arcs, feas, steps_per_launch=spl)
+        best = torch.zeros((G, 4), dtype=torch.int64, device="cuda")
+        ex.enqueue(G, first, stride, best)
+        torch.cuda.synchronize()
+        assert jobs[0].get_option(S._lib.OPT_LAST_SPLIT) == (split if sigma <= 0.12 else 0)
+        # the last launch of each branch left its outputs in that branch's buffers
+        out[split] = (best.cpu().numpy(), [a.cpu().numpy() for a in arcs], [f.cpu().numpy() for f in feas])
+    (b1, a1, f1), (b0, a0, f0) = out[1], out[0]
+    np.testing.assert_array_equal(b1, b0)
+    for x, y in zip(a1, a0):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(f1, f0):
+        np.testing.assert_array_equal(x, y)
+    if sigma >= 0.08:  # (sigma 0.02 stays near the infeasible straight path: nothing feasible)
+        assert (b1[:, 2] > 0).any()
