@@ -798,6 +798,16 @@ def bench_line(args, ctx, meta, world, ns, native, B, elapsed, enqueue_s, kernel
                              exec_per * value / 1e12 / max(1, world)},
         "cpu_baseline": cpu,
     }
+    vi = extras.get("valu_issue")
+    if vi:
+        # the FP32-filtered scan moved most of the arithmetic off FP64: the binding resource is
+        # VALU issue (PMC: ~4 cycles per wave instruction per SIMD over the dispatch's cycles) at
+        # the measured occupancy; the FP64 figure stays beside it
+        fp64 = line["binding_roofline"]
+        line["binding_roofline"] = {"bound": "valu_issue", "achieved": vi["per_simd"], "peak": 1.0,
+                                    "unit": "VALU issue-slot fraction per SIMD (PMC)", "frac": vi["per_simd"],
+                                    "mean_occupancy_waves_per_cu": vi.get("occupancy"), "source": vi.get("source"),
+                                    "fp64_valu": fp64}
     if "isolated_step_us" in extras:
         # one B-candidate batch (a single plan()'s worth) alone on the device
         line["isolated_step_us"] = extras["isolated_step_us"]
@@ -950,6 +960,9 @@ def main(argv=None):
             if rec and rec.get("kernel") == ctx.get("kernel_name", "k_tsp") and rec.get("rev") == KERNEL_REV and \
                     rec.get("candidates_per_launch", per_launch) == per_launch:
                 exec_per, exec_src = rec["fp64_flops_per_candidate"], rec["source"]
+                if rec.get("valu_issue_per_simd") is not None:
+                    extras["valu_issue"] = {"per_simd": rec["valu_issue_per_simd"],
+                                            "occupancy": rec.get("mean_occupancy_per_cu"), "source": rec["source"]}
         line = bench_line(args, ctx, meta, world, ns, native, B, elapsed, t_enq - t0, kernel_s, bytes_per,
                           flops_per, per_launch, traffic, traffic_src, exec_per, exec_src, cpu, extras)
         print(json.dumps(line))

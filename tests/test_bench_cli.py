@@ -73,6 +73,13 @@ def test_line_reports_what_bounds_the_kernel():
     assert line["config"]["order_gain"] == pytest.approx(77 / 70)
     assert line["single_plan_cand_per_s"] == pytest.approx(B / 25e-6)
     assert line["isolated_step_us"] == 25.0
+    # with the PMC issue record the binding resource is VALU issue, the FP64 figure beside it
+    line = bench.bench_line(args, ctx, dict(workload="stub"), 1, 4, True, B, 70e-6, 5e-6, kernel_s, 569, 537056,
+                            per_launch, 2.4e6, "stub", 1786.0, "stub", None,
+                            {"valu_issue": {"per_simd": 0.49, "occupancy": 10.1, "source": "stub"}})
+    b = line["binding_roofline"]
+    assert b["bound"] == "valu_issue" and b["frac"] == 0.49 and b["mean_occupancy_waves_per_cu"] == 10.1
+    assert b["fp64_valu"]["frac"] == pytest.approx(1786.0 * per_launch / kernel_s / 78.6e12)
     # without PMC records or the extra runs the fields are absent or null, never invented
     line = bench.bench_line(args, ctx, {}, 2, 4, True, B, 70e-6, 5e-6, kernel_s, 569, 537056, per_launch,
                             None, None, None, None, None, {})

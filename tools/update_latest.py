@@ -1,7 +1,7 @@
 """Fold a PMC evidence run (tools/runs/gpu_pmc.sh) into profiles/traffic_latest.json and
 profiles/fp64_latest.json, which bench.py reads for roofline.traffic / roofline_fp64.
     python tools/update_latest.py gpurun_out/TAG profiles/PREFIX
-Per config: the dominant kernel's launches of the roofline shape (the most frequent grid),
+Per config: the dominant kernel's launches of the roofline shape (GRID, else the most frequent grid),
 mean FETCH_SIZE / WRITE_SIZE per launch (KiB; HBM bytes = 1024 * (2 * FETCH + WRITE), the
 gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md) and the executed FP64 flops (64 lanes x
 (ADD + MUL + TRANS + 2 FMA) F64 wave instructions).  Also writes PREFIX_<config>_pmc.json."""
@@ -33,9 +33,16 @@ def rows(path, kern):
     return [r for r in csv.DictReader(open(f)) if kern in r["Kernel_Name"]]
 
 
-def per_launch(rs, counters):
-    """{counter: mean per launch} over the launches of the most frequent grid size."""
-    grid = collections.Counter(r["Grid_Size"] for r in rs).most_common(1)[0][0]
+# the timed launch's grid (threads) where other launches of the same kernel share the run: the
+# 128 x 4 shape holds 32 candidates per 128-thread workgroup (4 threads per candidate)
+GRID = {"robocrane": 4 * 40 * 4096, "robocrane_spl20": 4 * 20 * 4096}
+
+
+def per_launch(rs, counters, grid=None):
+    """{counter: mean per launch} over the launches of `grid`, else of the most frequent grid."""
+    if grid is None or not any(int(r["Grid_Size"]) == grid for r in rs):
+        grid = collections.Counter(r["Grid_Size"] for r in rs).most_common(1)[0][0]
+    grid = str(grid)
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in rs:
         if r["Grid_Size"] == grid and r["Counter_Name"] in counters:
@@ -59,7 +66,8 @@ def main(src, prefix):
         res = {"kernel": kern, "candidates_per_launch": PER_LAUNCH[cfg], "command": STEPS[cfg]}
         fr, wr = rows(os.path.join(d, "pmc_fetch"), kern), rows(os.path.join(d, "pmc_write"), kern)
         if fr and wr:
-            f, w = per_launch(fr, {"FETCH_SIZE"}), per_launch(wr, {"WRITE_SIZE"})
+            g = GRID.get(cfg)
+            f, w = per_launch(fr, {"FETCH_SIZE"}, g), per_launch(wr, {"WRITE_SIZE"}, g)
             res.update(FETCH_SIZE_KiB=f["FETCH_SIZE"], WRITE_SIZE_KiB=w["WRITE_SIZE"], launches=f["launches"],
                        grid=f["grid"], vgpr=f["VGPR_Count"], sgpr=f["SGPR_Count"],
                        scratch_per_lane=f["Scratch_Size"], lds=f["LDS_Block_Size"])
@@ -70,7 +78,7 @@ def main(src, prefix):
                                       "FETCH x2 gfx950 correction; %s)" % (prefix, cfg, STEPS[cfg])}
         pr = rows(os.path.join(d, "p1"), kern)
         if pr:
-            m = per_launch(pr, {r["Counter_Name"] for r in pr})
+            m = per_launch(pr, {r["Counter_Name"] for r in pr}, GRID.get(cfg))
             res["mix"] = m
             fl = 64.0 * (m["SQ_INSTS_VALU_ADD_F64"] + m["SQ_INSTS_VALU_MUL_F64"] +
                          m["SQ_INSTS_VALU_TRANS_F64"] + 2 * m["SQ_INSTS_VALU_FMA_F64"])
@@ -82,7 +90,7 @@ def main(src, prefix):
                                    "launch / %d candidates" % (prefix, cfg, PER_LAUNCH[cfg])}
         occ = rows(os.path.join(d, "occ", "p1"), kern)
         if occ:
-            o = per_launch(occ, {r["Counter_Name"] for r in occ})
+            o = per_launch(occ, {r["Counter_Name"] for r in occ}, GRID.get(cfg))
             res["occupancy"] = o
             if o.get("GRBM_GUI_ACTIVE"):
                 # GRBM_GUI_ACTIVE is summed over the 8 XCDs (each counts the dispatch's busy
@@ -96,12 +104,15 @@ def main(src, prefix):
                 res["waves_per_cu_from_wave_cycles"] = 4.0 * o["SQ_WAVE_CYCLES"] / (cyc * 256)
         occ2 = rows(os.path.join(d, "occ", "p2"), kern)
         if occ2:
-            res["mean_occupancy_per_cu"] = per_launch(occ2, {r["Counter_Name"] for r in occ2}).get("MeanOccupancyPerCU")
+            res["mean_occupancy_per_cu"] = per_launch(occ2, {r["Counter_Name"] for r in occ2}, GRID.get(cfg)).get("MeanOccupancyPerCU")
         ut = rows(os.path.join(d, "util"), kern)
         if ut:  # share of the 64 lanes active per VALU instruction (derived VALUUtilization, %)
-            u = per_launch(ut, {r["Counter_Name"] for r in ut})
+            u = per_launch(ut, {r["Counter_Name"] for r in ut}, GRID.get(cfg))
             res["valu_utilization_pct"] = u.get("VALUUtilization")
             res["valu_thread_cycles"] = u.get("SQ_THREAD_CYCLES_VALU")
+        if cfg in fp64 and fp64[cfg].get("rev") == KERNEL_REV and "valu_issue_per_simd" in res:
+            fp64[cfg]["valu_issue_per_simd"] = res["valu_issue_per_simd"]
+            fp64[cfg]["mean_occupancy_per_cu"] = res.get("mean_occupancy_per_cu")
         json.dump(res, open("%s_%s_pmc.json" % (prefix, cfg), "w"), indent=1, sort_keys=True)
         print(cfg, json.dumps(res, sort_keys=True)[:600])
     json.dump(traffic, open(tf, "w"), indent=1)
