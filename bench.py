@@ -72,6 +72,10 @@ def parse(argv=None):
     ap.add_argument("--tsp-form", type=int, default=None,
                     help="stacking: force the k_tsp form (SSPP_OPT_TSP_FORM 0..3; tuning, every form "
                          "gives bit-identical results)")
+    ap.add_argument("--mg-group", type=int, default=1, choices=[0, 1],
+                    help="multigoal: this rank's goals as one chain of batched launches per "
+                         "iteration (sspp_ces_plan_group, one k_tsp_group over every goal; default) "
+                         "or one planner per stream (A/B; results identical)")
     ap.add_argument("--mg-chunk", type=int, default=1,
                     help="multigoal: iterations per goal before the next goal's (0: all of a goal's "
                          "iterations in one call)")
@@ -261,7 +265,14 @@ def setup_multigoal(args, device, world, rank):
     streams = [torch.cuda.Stream(device) for _ in pls]
     started = [False] * len(pls)
 
+    st_mine = np.array([MULTIGOAL[g][0] for g in mine], dtype=np.float64)
+    en_mine = np.array([MULTIGOAL[g][1] for g in mine], dtype=np.float64)
+
     def run_steps(k):
+        if args.mg_group and pls:  # every goal's iteration in the same batched launches
+            S.CesPlanner.plan_group(pls, st_mine, en_mine, iterate=started[0], iterations=k, stream=streams[0])
+            started[0] = True
+            return
         if args.mg_chunk <= 0:  # every goal's k iterations in one call per goal
             for i, (g, pl) in enumerate(zip(mine, pls)):
                 st, en = MULTIGOAL[g]
@@ -280,7 +291,11 @@ def setup_multigoal(args, device, world, rank):
             done += c
 
     def kernel_only(first_id):
-        pls[0].eval(rank=0, stream=torch.cuda.current_stream())
+        if args.mg_group:  # one group iteration: k_ces_begin_group, k_tsp_group, the update
+            S.CesPlanner.plan_group(pls, st_mine, en_mine, iterate=True, iterations=1,
+                                    stream=torch.cuda.current_stream())
+        else:
+            pls[0].eval(rank=0, stream=torch.cuda.current_stream())
 
     bytes_per = 3 * 4 * 8 + 8 + 1
     flops_per = (2 * cp + 1) * 2 * 3 * 4 + cp * (3 * 4 + 1) + cp * (40 + 7 * 42 + 48 + 8 * 450)
@@ -288,7 +303,9 @@ def setup_multigoal(args, device, world, rank):
                          "full CES iterations (eval + elites + distribution update)" % len(MULTIGOAL),
                 goals=len(MULTIGOAL), goals_this_rank=len(mine), samples_per_goal=samples,
                 candidates_per_goal=samples + 2, waypoints=cp, vias=1, degree=2, dof=4)
-    ctx = dict(kind="multigoal", kernel_name="k_tsp", run_steps=run_steps, planners=pls, mine=mine,
+    meta["launch_form"] = "k_tsp_group (all goals per iteration)" if args.mg_group else "k_tsp per goal"
+    ctx = dict(kind="multigoal", kernel_name="k_tsp_group" if args.mg_group else "k_tsp", run_steps=run_steps,
+               planners=pls, mine=mine,
                scene_path=model.path, body=body, cp=cp, samples=samples)
     # candidates per step over ALL ranks: every goal's list (mean set + best + samples)
     return (samples + 2) * len(MULTIGOAL) // max(1, world), None, kernel_only, bytes_per, \
@@ -919,7 +936,8 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, ctx, B, device)
 
-    per_launch = ctx["samples"] + 2 if ctx["kind"] == "multigoal" else ctx.get("per_launch", B)
+    per_launch = ((ctx["samples"] + 2) * (len(ctx["mine"]) if args.mg_group else 1) if ctx["kind"] == "multigoal"
+                  else ctx.get("per_launch", B))
     # PMC records (tools/update_latest.py) are keyed by config, or config_b<B>_w<W> off the
     # default shape, and used only for launches of the recorded kernel and size
     pmc_key = args.config if (args.waypoints == 128 and not args.batch) else \

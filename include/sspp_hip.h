@@ -298,6 +298,13 @@ int sspp_ces_eval(sspp_ces* ces, int rank, void* stream);  /* this rank's slots 
 int sspp_ces_update(sspp_ces* ces, void* stream);           /* needs every slot's results */
 int sspp_ces_plan(sspp_ces* ces, const double* start, const double* end, int iterate,
                   int iterations, void* stream);            /* world == 1 */
+/* multi-goal: iterations x sspp_ces_plan of G <= 16 single-rank planners (starts / ends: [G][4])
+ * as one chain of batched launches on `stream` (one k_tsp_group evaluation per iteration over
+ * every goal's slots).  Each planner's results equal sspp_ces_plan on it alone.  Planners that
+ * differ in scene, vias, checks, bounds or CES configuration run one by one.  No reference
+ * counterpart: BASELINE configs[4] is build-defined.                      */
+int sspp_ces_plan_group(sspp_ces* const* ces, int G, const double* starts, const double* ends, int iterate,
+                        int iterations, void* stream);
 int sspp_ces_get_buffers(const sspp_ces* ces, sspp_ces_buffers* out);
 /* multi-rank exchange: this rank's slots_per_rank slots as packed f64 records
  * [L, C_nf, C_wf, cost, status, vias(4K)] (5 + 4K doubles each) into d_out; unpack scatters

@@ -151,6 +151,7 @@ SIGNATURES = {
     "sspp_ces_eval": (C.c_int, [_vp, _i, _vp]),
     "sspp_ces_update": (C.c_int, [_vp, _vp]),
     "sspp_ces_plan": (C.c_int, [_vp, _d, _d, _i, _i, _vp]),
+    "sspp_ces_plan_group": (C.c_int, [_vp, _i, _d, _d, _i, _i, _vp]),
     "sspp_ces_get_buffers": (C.c_int, [_vp, C.POINTER(CesBuffers)]),
     "sspp_ces_read": (C.c_int, [_vp, C.POINTER(CesState), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                 _vp, _vp]),

@@ -118,14 +118,27 @@ __device__ __forceinline__ void block_sum4(double (&v)[4], double* s_red) {
 
 // plan()'s prologue: reset() (iterate == 0) or keep the distribution, then the iteration's
 // fixed seeds: mean set with z >= cfg.z_min (tsp_planner.h:82-84) and the forwarded best.
-__global__ __launch_bounds__(128) void k_ces_begin(CesK c, int iterate, CesReset r, CesHdr* h,
-                                                   double* mean, double* sigma,
-                                                   const double* lbest, double* fixed) {
+// Planner::reset's initial mean (tsp_planner.h:54-69 + Distribution::reset, tsp_distribution.h:16-29):
+// entry e = 4 i + d of the linear vias, the same operations as sspp_ces_begin's host loop (no
+// contraction: ces.hip is built with -ffp-contract=off on both sides)
+__host__ __device__ inline double ces_mean0(const CesK& c, int total_points, const double* start, const double* end,
+                                            int e) {
+    const int i = e >> 2, d = e & 3;
+    const double t = (double)(i + 1) / (total_points - 1);
+    double v = (1.0 - t) * start[d] + t * end[d];
+    if (d == 2) v = v < c.z_min ? c.z_min : v;
+    if (d == 2) v = v < c.dist_z_min ? c.dist_z_min : v;
+    return v < c.lo[d] ? c.lo[d] : (c.hi[d] < v ? c.hi[d] : v);
+}
+
+__device__ __forceinline__ void ces_begin_body(const CesK& c, int iterate, const double* mean0, double sigma0,
+                                               CesHdr* h, double* mean, double* sigma, const double* lbest,
+                                               double* fixed) {
     const int e = threadIdx.x;
     const int hb = iterate ? h->has_best : 0;
     if (e < c.K * 4) {
-        double m = iterate ? mean[e] : r.mean0[e];
-        if (!iterate) { mean[e] = m; sigma[e] = r.sigma0; }
+        double m = iterate ? mean[e] : mean0[e];
+        if (!iterate) { mean[e] = m; sigma[e] = sigma0; }
         const int d = e & 3;
         fixed[e] = (d == 2 && m < c.z_min) ? c.z_min : m;
         fixed[c.K * 4 + e] = lbest[e];
@@ -139,6 +152,35 @@ __global__ __launch_bounds__(128) void k_ces_begin(CesK c, int iterate, CesReset
         h->best_cost = INFINITY;
     }
 }
+__global__ __launch_bounds__(128) void k_ces_begin(CesK c, int iterate, CesReset r, CesHdr* h,
+                                                   double* mean, double* sigma,
+                                                   const double* lbest, double* fixed) {
+    ces_begin_body(c, iterate, r.mean0, r.sigma0, h, mean, sigma, lbest, fixed);
+}
+
+// multi-goal iterations (sspp_ces_plan_group): every goal's device state and buffers, goal g in
+// blockIdx.z of each batched launch
+constexpr int kMaxCesGoals = 16;
+struct CesGoalDev {
+    CesHdr* h;
+    double *mean, *sigma, *lbest, *fixed;
+    unsigned char* status;
+    double *cost, *vias, *L, *Cnf, *Cwf;
+    int *rank, *by_rank, *nsucc, *elite;
+    unsigned char* stage;
+    double start[4], end[4];
+};
+struct CesGroupDev {
+    CesGoalDev g[kMaxCesGoals];
+};
+__global__ __launch_bounds__(128) void k_ces_begin_group(CesK c, int iterate, int total_points, double sigma0,
+                                                         CesGroupDev G) {
+    const CesGoalDev& q = G.g[blockIdx.z];
+    __shared__ double s_m0[kMaxVias * 4];
+    if (!iterate && threadIdx.x < c.K * 4) s_m0[threadIdx.x] = ces_mean0(c, total_points, q.start, q.end, threadIdx.x);
+    __syncthreads();
+    ces_begin_body(c, iterate, s_m0, sigma0, q.h, q.mean, q.sigma, q.lbest, q.fixed);
+}
 
 // ---- elite selection by rank counting (three launches, no sort, no host round trip) ----
 // The elites are the successes of rank < k in the (cost, slot) order — EliteSelector::select's
@@ -147,9 +189,8 @@ __global__ __launch_bounds__(128) void k_ces_begin(CesK c, int iterate, CesReset
 // each success is scattered to by_rank[rank[s]] (k_ces_scatter).  rank[] and the success
 // counter are re-armed by the kernels that consume them (zeroed once at creation).
 constexpr int kRankTile = 256;
-__global__ __launch_bounds__(kRankTile) void k_ces_rank(int nslots, const double* __restrict__ cost,
-                                                        const unsigned char* __restrict__ status,
-                                                        int* rank, int* nsucc) {
+__device__ __forceinline__ void ces_rank_body(int nslots, const double* __restrict__ cost,
+                                              const unsigned char* __restrict__ status, int* rank, int* nsucc) {
     __shared__ unsigned long long s_k[kRankTile];
     const int ts = blockIdx.x, tk = blockIdx.y, tid = threadIdx.x;
     const int j0 = tk * kRankTile, s = ts * kRankTile + tid, j = j0 + tid;
@@ -181,13 +222,22 @@ __global__ __launch_bounds__(kRankTile) void k_ces_rank(int nslots, const double
     }
     if (cnt) atomicAdd(rank + s, cnt);
 }
-__global__ __launch_bounds__(256) void k_ces_scatter(int nslots, const double* __restrict__ cost,
-                                                     const unsigned char* __restrict__ status,
-                                                     int* rank, int* by_rank) {
+__global__ __launch_bounds__(kRankTile) void k_ces_rank(int nslots, const double* __restrict__ cost,
+                                                        const unsigned char* __restrict__ status,
+                                                        int* rank, int* nsucc) {
+    ces_rank_body(nslots, cost, status, rank, nsucc);
+}
+__device__ __forceinline__ void ces_scatter_body(int nslots, const double* __restrict__ cost,
+                                                 const unsigned char* __restrict__ status, int* rank, int* by_rank) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s >= nslots) return;
     if (status[s] && okey(cost[s]) != kNoKey) by_rank[rank[s]] = s;
     rank[s] = 0;  // re-armed for the next update
+}
+__global__ __launch_bounds__(256) void k_ces_scatter(int nslots, const double* __restrict__ cost,
+                                                     const unsigned char* __restrict__ status,
+                                                     int* rank, int* by_rank) {
+    ces_scatter_body(nslots, cost, status, rank, by_rank);
 }
 
 // Pinned staging layout read by sspp_ces_read: [header, 64 B] [L | C_nf | C_wf | cost : n each]
@@ -218,8 +268,8 @@ __host__ __device__ inline StageView stage_view(unsigned char* base, int n, int 
 // stage != nullptr: the iteration's results also go straight into sspp_ces_read's pinned staging
 // (the values this workgroup writes, from registers; the per-slot results of the evaluation),
 // so reading it back needs no staging launch.
-__global__ __launch_bounds__(kCesThreads) void k_ces_update(
-    CesK c, int fused, const unsigned char* __restrict__ status, const double* __restrict__ cost,
+__device__ __forceinline__ void ces_update_body(
+    const CesK& c, int fused, const unsigned char* __restrict__ status, const double* __restrict__ cost,
     const int* __restrict__ by_rank, int* nsucc_p, const double* __restrict__ vias,
     const double* __restrict__ LT, const double* __restrict__ LH, CesHdr* h, double* mean,
     double* sigma, double* lbest, int* elite_out, const double* __restrict__ Lsl,
@@ -384,6 +434,30 @@ __global__ __launch_bounds__(kCesThreads) void k_ces_update(
             *sv.hdr = o;
         }
     }
+}
+
+__global__ __launch_bounds__(kCesThreads) void k_ces_update(
+    CesK c, int fused, const unsigned char* __restrict__ status, const double* __restrict__ cost,
+    const int* __restrict__ by_rank, int* nsucc_p, const double* __restrict__ vias,
+    const double* __restrict__ LT, const double* __restrict__ LH, CesHdr* h, double* mean,
+    double* sigma, double* lbest, int* elite_out, const double* __restrict__ Lsl,
+    const double* __restrict__ Cnfsl, const double* __restrict__ Cwfsl, unsigned char* stage) {
+    ces_update_body(c, fused, status, cost, by_rank, nsucc_p, vias, LT, LH, h, mean, sigma, lbest, elite_out, Lsl,
+                    Cnfsl, Cwfsl, stage);
+}
+__global__ __launch_bounds__(kRankTile) void k_ces_rank_group(int nslots, CesGroupDev G) {
+    const CesGoalDev& q = G.g[blockIdx.z];
+    ces_rank_body(nslots, q.cost, q.status, q.rank, q.nsucc);
+}
+__global__ __launch_bounds__(256) void k_ces_scatter_group(int nslots, CesGroupDev G) {
+    const CesGoalDev& q = G.g[blockIdx.z];
+    ces_scatter_body(nslots, q.cost, q.status, q.rank, q.by_rank);
+}
+__global__ __launch_bounds__(kCesThreads) void k_ces_update_group(CesK c, int fused, const double* __restrict__ LT,
+                                                                  const double* __restrict__ LH, CesGroupDev G) {
+    const CesGoalDev& q = G.g[blockIdx.z];
+    ces_update_body(c, fused, q.status, q.cost, q.by_rank, q.nsucc, q.vias, LT, LH, q.h, q.mean, q.sigma, q.lbest,
+                    q.elite, q.L, q.Cnf, q.Cwf, q.stage);
 }
 
 // Multi-rank exchange: a rank's slots as packed records [L, C_nf, C_wf, cost, status, vias]
@@ -713,6 +787,110 @@ int sspp_ces_plan(sspp_ces* p, const double* start, const double* end, int itera
         if (rc) return rc;
         if ((rc = sspp_ces_eval(p, 0, stream))) return rc;
         if ((rc = sspp_ces_update(p, stream))) return rc;
+    }
+    return SSPP_OK;
+}
+
+// Several planners' iterations as one chain of batched launches: per iteration one
+// k_ces_begin_group, one k_tsp_group over every goal's slots, then k_ces_rank_group /
+// k_ces_scatter_group (lists above kCesThreads) and one k_ces_update_group — 3-5 launches for all
+// goals instead of 3-5 per goal, and the goals' evaluations share the chip instead of following
+// one another.  Each planner's state, buffers, seed and Philox ids are its own, so every result
+// equals sspp_ces_plan on that planner alone (test_ces_plan_group_matches_single).  The planners
+// must share the evaluation (scene, vias, checks, bounds, costs) and the CES configuration; a
+// group that does not, or whose slot lists are small enough for the pair-split evaluation, runs
+// goal by goal (sspp_ces_plan on each, same results).
+int sspp_ces_plan_group(sspp_ces* const* ps, int G, const double* starts, const double* ends, int iterate,
+                        int iterations, void* stream) {
+    sspp::clear_error();
+    if (!ps || !starts || !ends || G < 1 || iterations < 1)
+        return sspp::set_error(SSPP_E_INVAL, "sspp_ces_plan_group: bad argument");
+    const sspp_ces* p0 = ps[0];
+    for (int g = 0; g < G; ++g)
+        if (!ps[g] || ps[g]->world != 1)
+            return sspp::set_error(SSPP_E_INVAL, "sspp_ces_plan_group: single-rank planners only");
+    const CesK c0 = ces_k(p0);
+    bool same = G <= kMaxCesGoals;
+    for (int g = 1; g < G && same; ++g) {
+        const CesK c = ces_k(ps[g]);
+        same = std::memcmp(&c, &c0, sizeof c) == 0 && ps[g]->cfg.total_points == p0->cfg.total_points &&
+               ps[g]->cfg.sigma0 == p0->cfg.sigma0 && ps[g]->fused == p0->fused;
+        for (int h = 0; h < g && same; ++h) same = ps[h] != ps[g];
+    }
+    hipStream_t st = (hipStream_t)stream;
+    auto one_by_one = [&]() {
+        for (int g = 0; g < G; ++g) {
+            int rc = sspp_ces_plan(ps[g], starts + 4 * g, ends + 4 * g, iterate, iterations, stream);
+            if (rc) return rc;
+        }
+        return (int)SSPP_OK;
+    };
+    if (!same) return one_by_one();
+    double s0 = p0->cfg.sigma0;  // the sigma clamps of sspp_ces_begin
+    s0 = s0 < p0->cfg.stddev_min ? p0->cfg.stddev_min : s0;
+    s0 = s0 > p0->cfg.stddev_max ? p0->cfg.stddev_max : s0;
+    s0 = s0 < p0->cfg.sigma_floor ? p0->cfg.sigma_floor : s0;
+    CesGroupDev gd{};
+    std::vector<sspp_job*> jobs(G);
+    std::vector<sspp::TspCesEval> evs(G);
+    std::vector<sspp::TspCesOut> outs(G);
+    for (int g = 0; g < G; ++g) {
+        sspp_ces* p = ps[g];
+        CesGoalDev& q = gd.g[g];
+        q.h = p->d_hdr; q.mean = p->d_mean; q.sigma = p->d_sigma; q.lbest = p->d_lbest; q.fixed = p->d_fixed;
+        q.status = p->d_status; q.cost = p->d_cost; q.vias = p->d_vias; q.L = p->d_L; q.Cnf = p->d_Cnf;
+        q.Cwf = p->d_Cwf; q.rank = p->d_rank; q.by_rank = p->d_by_rank; q.nsucc = p->d_nsucc; q.elite = p->d_elite;
+        for (int i = 0; i < 4; ++i) {
+            q.start[i] = p->start[i] = starts[4 * g + i];
+            q.end[i] = p->end[i] = ends[4 * g + i];
+        }
+        jobs[g] = p->job;
+        sspp::TspCesEval& e = evs[g];
+        e.fixed = p->d_fixed; e.nfixed = &p->d_hdr->nfixed; e.mean = p->d_mean; e.sigma = p->d_sigma;
+        e.slot0 = 0; e.samples = p->cfg.samples;
+        for (int i = 0; i < 4; ++i) { e.start[i] = p->start[i]; e.end[i] = p->end[i]; }
+        outs[g] = sspp::TspCesOut{p->d_L, p->d_Cnf, p->d_Cwf, p->d_cost, p->d_vias, p->d_status};
+    }
+    const int n = p0->nslots;
+    const int fused = n <= kCesThreads && p0->fused;
+    const int nt = (n + kRankTile - 1) / kRankTile;
+    for (int t = 0; t < iterations; ++t) {
+        for (int g = 0; g < G; ++g) {
+            sspp_ces* p = ps[g];
+            note_stream(p, st);
+            p->staged_iter = -1;
+            evs[g].first_id = p->iter * (long long)p->cfg.samples;
+            gd.g[g].stage = fused ? p->h_stage : nullptr;
+        }
+        hipLaunchKernelGGL(k_ces_begin_group, dim3(1, 1, G), dim3(128), 0, st, c0, (t > 0 || iterate) ? 1 : 0,
+                           p0->cfg.total_points, s0, gd);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_err(e, "k_ces_begin_group launch");
+        int rc = sspp::tsp_eval_ces_group(jobs.data(), evs.data(), outs.data(), G, n, stream);
+        if (rc == SSPP_E_UNSUPPORTED && t == 0) {
+            // the evaluation cannot be batched: this iteration's begin ran for every goal, so
+            // finish it goal by goal, then the remaining iterations likewise
+            sspp::clear_error();
+            for (int g = 0; g < G; ++g) {
+                if ((rc = sspp_ces_eval(ps[g], 0, stream)) || (rc = sspp_ces_update(ps[g], stream))) return rc;
+                if (iterations > 1 && (rc = sspp_ces_plan(ps[g], starts + 4 * g, ends + 4 * g, 1, iterations - 1, stream)))
+                    return rc;
+            }
+            return SSPP_OK;
+        }
+        if (rc) return rc;
+        if (!fused) {
+            hipLaunchKernelGGL(k_ces_rank_group, dim3(nt, nt, G), dim3(kRankTile), 0, st, n, gd);
+            hipLaunchKernelGGL(k_ces_scatter_group, dim3(nt, 1, G), dim3(256), 0, st, n, gd);
+        }
+        hipLaunchKernelGGL(k_ces_update_group, dim3(1, 1, G), dim3(kCesThreads), 0, st, c0, fused, p0->d_LT,
+                           p0->d_LH, gd);
+        e = hipGetLastError();
+        if (e != hipSuccess) return hip_err(e, "k_ces_update_group launch");
+        for (int g = 0; g < G; ++g) {
+            ps[g]->iter++;
+            ps[g]->staged_iter = fused ? ps[g]->iter : -1;
+        }
     }
     return SSPP_OK;
 }

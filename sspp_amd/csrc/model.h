@@ -52,6 +52,13 @@ struct TspCesEval {
 int tsp_eval_ces(sspp_job* j, const TspCesEval* e, int64_t n, double* d_L, double* d_Cnf,
                  double* d_Cwf, uint8_t* d_status, double* d_cost, double* d_vias_out,
                  void* stream);
+// several goals' CES evaluations in one k_tsp_group launch (ces.hip sspp_ces_plan_group)
+struct TspCesOut {
+    double *L, *Cnf, *Cwf, *cost, *vias;
+    uint8_t* status;
+};
+int tsp_eval_ces_group(sspp_job* const* jobs, const TspCesEval* evs, const TspCesOut* outs, int G, int64_t n,
+                       void* stream);
 // sspp_job_create_sspp with the hit-order pre-pass off the caller's path: the job starts in gap /
 // bisection order and swaps in the hit order at the first launch after the pre-pass lands (the
 // drop-in planner's first plan(), planner.hip; results are identical in every order)

@@ -2091,10 +2091,43 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
 #ifndef SSPP_TSP_WAVES_PER_EU_CB  // with the exact cylinder-box test (its live state doubles)
 #define SSPP_TSP_WAVES_PER_EU_CB 2
 #endif
+// The per-problem values of a TaskSpacePlanner launch: a k_tsp launch's own (TspK), or one goal's
+// of a multi-goal launch (k_tsp_group, TspGoals)
+struct TspVar {
+    const double* start;
+    const double* end;
+    const double* fixed;
+    const int* nfixed;
+    unsigned long long seed;
+    long long first_id;
+};
+__device__ __forceinline__ TspVar tsp_var(const TspK& a) {
+    return TspVar{a.start, a.end, a.fixed, a.nfixed, a.seed, a.first_id};
+}
+// multi-goal launches (sspp_ces_plan_group): one CES iteration of up to kMaxGoals independent
+// planners, goal g's workgroups [g nblk, (g + 1) nblk); the goal's problem, distribution and
+// output buffers ride in the kernel arguments
+constexpr int kMaxGoals = 16;
+struct TspGoal {
+    double start[4], end[4];
+    unsigned long long seed;
+    long long first_id;
+    const double* fixed;
+    const int* nfixed;
+    const double* mean;
+    const double* sigma;
+    double *vias_out, *oL, *oCnf, *oCwf, *ocost;
+    unsigned char* ostatus;
+};
+struct TspGoals {
+    TspGoal g[kMaxGoals];
+    int n, nblk;
+};
+
 // k_tsp's prologue, shared with k_tsp_pp: the candidates' via sets (given, CES fixed seeds or
 // Sampler::sample_set draws) into s_V [cpb][n][4], vias_out, then PathModel::fromVias into
 // s_ctrl [cpb][n][4].  Every thread of the workgroup calls it (it synchronises).
-__device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __restrict__ Minv,
+__device__ __forceinline__ void tsp_prologue(const TspK& a, const TspVar& pv, const double* __restrict__ Minv,
                                              const double* __restrict__ mean,
                                              const double* __restrict__ sigma,
                                              const double* __restrict__ vias_in,
@@ -2105,8 +2138,8 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
     const int n = a.n, K = a.K, ndof = n * D;
     for (int e = tid; e < cpb * 2 * D; e += nthr) {
         const int s = e / (2 * D), r = e - s * 2 * D;
-        if (r < D) s_V[s * ndof + r] = a.start[r];
-        else s_V[s * ndof + (n - 1) * D + (r - D)] = a.end[r - D];
+        if (r < D) s_V[s * ndof + r] = pv.start[r];
+        else s_V[s * ndof + (n - 1) * D + (r - D)] = pv.end[r - D];
     }
     if (vias_in) {
         for (int e = tid; e < nvalid * K * D; e += nthr) {
@@ -2123,7 +2156,7 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
             if (a.ces) {
                 const long long slot = a.slot0 + cand0 + s;
                 if (slot < nfx) {  // mean set / forwarded best: no sampling
-                    s_V[s * ndof + D + r] = a.fixed[(slot * K + v) * D + i];
+                    s_V[s * ndof + D + r] = pv.fixed[(slot * K + v) * D + i];
                     continue;
                 }
                 gi = slot - nfx;
@@ -2132,7 +2165,7 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
                     continue;
                 }
             }
-            const unsigned long long g = (unsigned long long)(a.first_id + gi);
+            const unsigned long long g = (unsigned long long)(pv.first_id + gi);
             const double m = mean[v * D + i], sg = sigma[v * D + i];
             double val;
             if (i < 3) {
@@ -2140,20 +2173,20 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const double* __rest
                 val = 0.0;
                 for (int t = 0; t < 99; ++t) {
                     double z0, z1;
-                    normal_pair(a.seed, g, (unsigned)(((v * 4 + i) << 7) | t), 1u, &z0, &z1);
+                    normal_pair(pv.seed, g, (unsigned)(((v * 4 + i) << 7) | t), 1u, &z0, &z1);
                     val = z0 * sg;
                     val = val + m;
                     if (!(val < a.lo[i] || val > a.hi[i])) { ok = true; break; }
                 }
                 if (!ok) {
-                    double u = uniform01(a.seed, g, (unsigned)(((v * 4 + i) << 7) | 127), 1u);
+                    double u = uniform01(pv.seed, g, (unsigned)(((v * 4 + i) << 7) | 127), 1u);
                     val = u * (a.hi[i] - a.lo[i]);
                     val = val + a.lo[i];
                 }
                 if (i == 2 && val < a.z_min) val = a.z_min;
             } else if (a.lo[3] != a.hi[3]) {
                 double z0, z1;
-                normal_pair(a.seed, g, (unsigned)((v * 4 + 3) << 7), 1u, &z0, &z1);
+                normal_pair(pv.seed, g, (unsigned)((v * 4 + 3) << 7), 1u, &z0, &z1);
                 val = z0 * sg;
                 val = val + m;
                 const double range = a.hi[3] - a.lo[3];
@@ -2219,21 +2252,20 @@ constexpr int kDefPairs = 8;
 #ifndef SSPP_TSP_WAVES_PER_EU_DEF
 #define SSPP_TSP_WAVES_PER_EU_DEF 4
 #endif
-template <int NM, bool ONEGEOM, int CB, bool UP = false, int DEF = 0>
-__global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
-                                              : (CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
-                                                         : (ONEGEOM ? SSPP_TSP_WAVES_PER_EU : SSPP_TSP_WAVES_PER_EU_MG))) void k_tsp(
-    TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+// k_tsp's body: workgroup blk of a problem (k_tsp: the launch's; k_tsp_group: a goal's)
+template <int NM, bool ONEGEOM, int CB, bool UP, int DEF>
+__device__ __forceinline__ void tsp_body(
+    const TspK& a, const TspVar& pv, const SceneT& T, const double* __restrict__ tab, const int* __restrict__ span,
     const double* __restrict__ Minv, const double* __restrict__ mean,
     const double* __restrict__ sigma, const double* __restrict__ vias_in,
     double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
     double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
-    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best, int blk) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int D = 4, P = 2, P1 = 3;
     const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, cp = a.cp;
     const int slot = tid / lpc, lane = tid - slot * lpc;
-    const long long cand0 = (long long)blockIdx.x * cpb;
+    const long long cand0 = (long long)blk * cpb;
     const int ndof = n * D;
     double* s_V = smem;                      // [cpb][n][4]
     double* s_ctrl = s_V + cpb * ndof;       // [cpb][n][4]
@@ -2250,8 +2282,8 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
     int* s_nitems = s_items + kBlock * npr;
 
     const long long nvalid = min((long long)cpb, a.B - cand0);
-    const long long nfx = a.ces ? (long long)*a.nfixed : 0;  // uniform: scalar load
-    tsp_prologue(a, Minv, mean, sigma, vias_in, vias_out, tid, kBlock, cpb, cand0, nvalid, nfx, s_V, s_ctrl);
+    const long long nfx = a.ces ? (long long)*pv.nfixed : 0;  // uniform: scalar load
+    tsp_prologue(a, pv, Minv, mean, sigma, vias_in, vias_out, tid, kBlock, cpb, cand0, nvalid, nfx, s_V, s_ctrl);
 
     // Evaluator::eval_one_pass (tsp_evaluator.h:18-32), waypoint i = 1..cp per lane
     const bool valid = slot < nvalid;
@@ -2414,10 +2446,39 @@ __global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
         for (int s = 0; s < nvalid; ++s) {
             if (!s_stat[s]) continue;
             bb.count++;
-            if (s_best[s] < bb.cost) { bb.cost = s_best[s]; bb.idx = a.first_id + cand0 + s; }
+            if (s_best[s] < bb.cost) { bb.cost = s_best[s]; bb.idx = pv.first_id + cand0 + s; }
         }
     }
-    finish_batch(bb, part, sync, best);
+    if (part || best) finish_batch(bb, part, sync, best);  // (CES slot mode: records unused)
+}
+
+template <int NM, bool ONEGEOM, int CB, bool UP = false, int DEF = 0>
+__global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
+                                              : (CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
+                                                         : (ONEGEOM ? SSPP_TSP_WAVES_PER_EU : SSPP_TSP_WAVES_PER_EU_MG))) void k_tsp(
+    TspK a, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ Minv, const double* __restrict__ mean,
+    const double* __restrict__ sigma, const double* __restrict__ vias_in,
+    double* __restrict__ vias_out, double* __restrict__ oL, double* __restrict__ oCnf,
+    double* __restrict__ oCwf, double* __restrict__ ocost, unsigned char* __restrict__ ostatus,
+    BlockBest* __restrict__ part, ArgminSync* sync, sspp_best* best) {
+    tsp_body<NM, ONEGEOM, CB, UP, DEF>(a, tsp_var(a), T, tab, span, Minv, mean, sigma, vias_in, vias_out, oL, oCnf,
+                                       oCwf, ocost, ostatus, part, sync, best, (int)blockIdx.x);
+}
+
+// one CES iteration's evaluation of every goal of a multi-goal launch (sspp_ces_plan_group): the
+// same body per workgroup, the goal's values and buffers from the arguments
+template <int NM, bool ONEGEOM, int CB, bool UP = false, int DEF = 0>
+__global__ __launch_bounds__(kBlock, DEF == 1 ? SSPP_TSP_WAVES_PER_EU_DEF
+                                              : (CB == 1 ? SSPP_TSP_WAVES_PER_EU_CB
+                                                         : (ONEGEOM ? SSPP_TSP_WAVES_PER_EU : SSPP_TSP_WAVES_PER_EU_MG))) void k_tsp_group(
+    TspK a, TspGoals G, SceneT T, const double* __restrict__ tab, const int* __restrict__ span,
+    const double* __restrict__ Minv) {
+    const int g = (int)blockIdx.x / G.nblk, blk = (int)blockIdx.x - g * G.nblk;
+    const TspGoal& q = G.g[g];
+    const TspVar pv{q.start, q.end, q.fixed, q.nfixed, q.seed, q.first_id};
+    tsp_body<NM, ONEGEOM, CB, UP, DEF>(a, pv, T, tab, span, Minv, q.mean, q.sigma, nullptr, q.vias_out, q.oL, q.oCnf,
+                                       q.oCwf, q.ocost, q.ostatus, nullptr, nullptr, nullptr, blk);
 }
 
 // ---------------------------------------------------------------- TaskSpacePlanner, pair-split
@@ -2448,7 +2509,7 @@ __global__ __launch_bounds__(64 * G, 2) void k_tsp_pp(
     const long long nvalid = 1;
     const long long nfx = a.ces ? (long long)*a.nfixed : 0;
     for (int e = tid; e < 64 * 64 / 4; e += NT) ((unsigned*)s_nd)[e] = 0u;
-    tsp_prologue(a, Minv, mean, sigma, vias_in, vias_out, tid, NT, 1, cand0, nvalid, nfx, s_V, s_ctrl);
+    tsp_prologue(a, tsp_var(a), Minv, mean, sigma, vias_in, vias_out, tid, NT, 1, cand0, nvalid, nfx, s_V, s_ctrl);
     const unsigned long long mask = hull_mask<D, NM, 1>(s_ctrl, n, np, (cpair_t)T.pairs,
                                                         (cgeom_t)T.geoms, (cmover_t)T.movers);
     // this wave's pairs: k = g (mod G)
@@ -2540,7 +2601,7 @@ __global__ __launch_bounds__(64 * G, 2) void k_tsp_pp2(
     double* s_V = smem;           // [n][4]
     double* s_ctrl = s_V + ndof;  // [n][4]
     const long long nfx = a.ces ? (long long)*a.nfixed : 0;
-    tsp_prologue(a, Minv, mean, sigma, vias_in, pg == 0 ? vias_out : nullptr, tid, NT, 1, cand0, 1, nfx,
+    tsp_prologue(a, tsp_var(a), Minv, mean, sigma, vias_in, pg == 0 ? vias_out : nullptr, tid, NT, 1, cand0, 1, nfx,
                  s_V, s_ctrl);
     const unsigned long long mask = hull_mask<D, NM, 1>(s_ctrl, n, np, (cpair_t)T.pairs,
                                                         (cgeom_t)T.geoms, (cmover_t)T.movers);
@@ -2988,6 +3049,36 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
     return hipGetLastError();
 }
 
+// multi-goal evaluation (k_tsp_group): the k_tsp instantiation entry_tsp picks for mode 0 / 3 / 4
+template <int Unused>
+hipError_t entry_tsp_group(const TspK& k, const TspGoals& goals, const sspp_job* j, int nblk, hipStream_t st,
+                           int mode) {
+    const SceneT tt = scene_t(j->scene);
+#define SSPP_LAUNCH_TSPG(OG, CBV, UPV, DEFV)                                                            \
+    hipLaunchKernelGGL((k_tsp_group<1, OG, CBV, UPV, DEFV>), dim3(nblk), dim3(kBlock), lds, st, k, goals, tt, \
+                       j->d_tab, j->d_span, j->d_Minv)
+    const bool og = k.sc.onegeom && k.sc.npairs > 0;
+    const int cbm = k.sc.cylbox ? (k.sc.cbup ? 2 : 1) : 0;
+    const bool up = k.sc.upright && cbm != 1;
+    const int def = mode == 3 ? 1 : (mode == 4 ? 2 : 0);
+    const size_t lds = def == 1 ? j->lds + tsp_def_lds(k.sc.npairs) : (def == 2 ? j->lds + tsp_def2_lds(k.sc.npairs) : j->lds);
+#define SSPP_LAUNCH_TSPG_ALL(DEFV)                                                                        \
+    if (og && cbm == 1) SSPP_LAUNCH_TSPG(true, 1, false, DEFV);                                           \
+    else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSPG(true, 2, true, DEFV); else SSPP_LAUNCH_TSPG(true, 2, false, DEFV); } \
+    else if (og && up) SSPP_LAUNCH_TSPG(true, 0, true, DEFV);                                             \
+    else if (og) SSPP_LAUNCH_TSPG(true, 0, false, DEFV);                                                  \
+    else if (cbm == 1) SSPP_LAUNCH_TSPG(false, 1, false, DEFV);                                           \
+    else if (cbm == 2) { if (up) SSPP_LAUNCH_TSPG(false, 2, true, DEFV); else SSPP_LAUNCH_TSPG(false, 2, false, DEFV); } \
+    else if (up) SSPP_LAUNCH_TSPG(false, 0, true, DEFV);                                                  \
+    else SSPP_LAUNCH_TSPG(false, 0, false, DEFV);
+    if (def == 1) { SSPP_LAUNCH_TSPG_ALL(1) }
+    else if (def == 2) { SSPP_LAUNCH_TSPG_ALL(2) }
+    else { SSPP_LAUNCH_TSPG_ALL(0) }
+#undef SSPP_LAUNCH_TSPG_ALL
+#undef SSPP_LAUNCH_TSPG
+    return hipGetLastError();
+}
+
 #define SSPK_ENTRY_DECL(X, D, P)                                                                          \
     X template hipError_t entry_c2f_p<D, P>(const SsppC2F&, const sspp_job*, const SsppPtrs&, int, hipStream_t); \
     X template hipError_t entry_census_p<D, P>(const sspp_job*, int, unsigned long long, unsigned long long*,   \
@@ -2995,6 +3086,7 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
 #define SSPK_TSP_DECL(X)                                                                                  \
     X template hipError_t entry_tsp<0>(const TspK&, const sspp_job*, int, const double*, const double*,    \
                                        const double*, double*, double*, double*, double*, double*, uint8_t*, \
-                                       sspp_best*, hipStream_t, int);
+                                       sspp_best*, hipStream_t, int);                                       \
+    X template hipError_t entry_tsp_group<0>(const TspK&, const TspGoals&, const sspp_job*, int, hipStream_t, int);
 
 }  // namespace sspk

@@ -1298,6 +1298,34 @@ extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args*
     return SSPP_OK;
 }
 
+// the launch's TspK for job j (run_tsp, tsp_eval_ces_group)
+static TspK tsp_k(const sspp_job* j, int64_t first_id, int64_t B) {
+    TspK k{};
+    k.sc = kscene(j->scene, true, j->tsp_generic != 0);
+    k.n = j->n; k.K = j->K; k.cp = j->cp;
+    for (int i = 0; i < 4; ++i) { k.start[i] = j->start[i]; k.end[i] = j->end[i]; k.lo[i] = j->lo[i]; k.hi[i] = j->hi[i]; }
+    k.z_min = j->z_min; k.seed = j->seed; k.first_id = first_id; k.B = B;
+    k.w_col = j->w_col; k.floor_z_min = j->floor_z_min; k.floor_margin = j->floor_margin;
+    k.floor_scale = j->floor_scale;
+    k.lpc = j->lpc; k.cpb = j->cpb;
+    return k;
+}
+
+// k_tsp's deferred-polygon forms (modes 3 / 4) where they apply, else the inline form (0); the
+// pair-split forms (1 / 2) are run_tsp's choice for small batches
+static int tsp_large_mode(const sspp_job* j, const TspK& k) {
+    const int pp_opt = j->tsp_form;
+    bool has_bb = false;
+    for (const DPair& pr : j->scene->pairs) has_bb |= j->scene->geoms[pr.gm].type == 6 && pr.otype == 6;
+    const bool def_ok = j->cp <= j->lpc && k.sc.npairs >= 1 && k.sc.npairs <= kDefPairs && has_bb &&
+                        j->lds + tsp_def_lds(k.sc.npairs) <= 64 * 1024;
+    if (def_ok && (pp_opt < 0 || pp_opt == 3)) return 3;
+    const bool def2_ok = j->cp <= j->lpc && k.sc.npairs >= 1 && k.sc.npairs <= 64 && has_bb &&
+                         j->lds + tsp_def2_lds(k.sc.npairs) <= 64 * 1024;
+    if (def2_ok && (pp_opt < 0 || pp_opt == 4)) return 4;
+    return 0;
+}
+
 static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t B, double* d_L,
                    double* d_Cnf, double* d_Cwf, uint8_t* d_status, double* d_cost,
                    double* d_vias_out, sspp_best* d_best, void* stream,
@@ -1307,14 +1335,7 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     if (B < 1 || B > j->max_batch) return sspp::set_error(SSPP_E_INVAL, "batch size out of range");
     if (!d_L || !d_Cnf || !d_Cwf || !d_status || !d_cost)
         return sspp::set_error(SSPP_E_INVAL, "null output");
-    TspK k{};
-    k.sc = kscene(j->scene, true, j->tsp_generic != 0);
-    k.n = j->n; k.K = j->K; k.cp = j->cp;
-    for (int i = 0; i < 4; ++i) { k.start[i] = j->start[i]; k.end[i] = j->end[i]; k.lo[i] = j->lo[i]; k.hi[i] = j->hi[i]; }
-    k.z_min = j->z_min; k.seed = j->seed; k.first_id = first_id; k.B = B;
-    k.w_col = j->w_col; k.floor_z_min = j->floor_z_min; k.floor_margin = j->floor_margin;
-    k.floor_scale = j->floor_scale;
-    k.lpc = j->lpc; k.cpb = j->cpb;
+    TspK k = tsp_k(j, first_id, B);
     const double* mean = j->d_mean;
     const double* sigma = j->d_sigma;
     if (ces) {
@@ -1352,17 +1373,10 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     // the deferred-polygon form of k_tsp (mode 3): one waypoint per lane, few pairs, some of them
     // box-box (the polygons it defers); the default for such batches above the pair-split sizes.
     // (A form in rounds for many pairs — the gripper's 48 — measured more registers than the
-    // inline narrowphase: the polygons of divergent pairs need the pair data in VGPRs.)
-    bool has_bb = false;
-    for (const DPair& pr : j->scene->pairs) has_bb |= j->scene->geoms[pr.gm].type == 6 && pr.otype == 6;
-    const bool def_ok = j->cp <= j->lpc && k.sc.npairs >= 1 && k.sc.npairs <= kDefPairs && has_bb &&
-                        j->lds + tsp_def_lds(k.sc.npairs) <= 64 * 1024;
-    if (mode == 0 && def_ok && (pp_opt < 0 || pp_opt == 3)) mode = 3;
-    // the lane-local deferred polygons (mode 4): one waypoint per lane, up to 64 pairs, some of them
+    // inline narrowphase: the polygons of divergent pairs need the pair data in VGPRs.)  The
+    // lane-local deferred polygons (mode 4): one waypoint per lane, up to 64 pairs, some of them
     // box-box; the default where mode 3 does not apply (the gripper's 48 pairs)
-    const bool def2_ok = j->cp <= j->lpc && k.sc.npairs >= 1 && k.sc.npairs <= 64 && has_bb &&
-                         j->lds + tsp_def2_lds(k.sc.npairs) <= 64 * 1024;
-    if (mode == 0 && def2_ok && (pp_opt < 0 || pp_opt == 4)) mode = 4;
+    if (mode == 0) mode = tsp_large_mode(j, k);
     const int nblk = mode == 2 ? (int)B * npg : mode == 1 ? (int)B : (int)((B + j->cpb - 1) / j->cpb);
     j->last_form = mode;
     hipStream_t st = (hipStream_t)stream;
@@ -1386,6 +1400,59 @@ int sspp::tsp_eval_ces(sspp_job* j, const TspCesEval* e, int64_t n, double* d_L,
         return sspp::set_error(SSPP_E_INVAL, "tsp_eval_ces: null argument");
     return run_tsp(j, nullptr, e->first_id, n, d_L, d_Cnf, d_Cwf, d_status, d_cost, d_vias_out,
                    nullptr, stream, e);
+}
+
+// Multi-goal CES evaluation (ces.hip sspp_ces_plan_group): one k_tsp_group launch over every goal's
+// slots [0, n).  The goals' jobs must describe the same evaluation (scene, spline, checks, bounds,
+// costs) and differ only in start / end, seed, distribution and buffers; SSPP_E_UNSUPPORTED when
+// they do not, or when run_tsp would pick a pair-split form for n slots (the caller then
+// evaluates goal by goal).
+int sspp::tsp_eval_ces_group(sspp_job* const* jobs, const TspCesEval* evs, const TspCesOut* outs, int G,
+                             int64_t n, void* stream) {
+    sspp::clear_error();
+    if (!jobs || !evs || !outs || G < 1 || n < 1) return sspp::set_error(SSPP_E_INVAL, "tsp_eval_ces_group: bad argument");
+    if (G > kMaxGoals) return sspp::set_error(SSPP_E_UNSUPPORTED, "more goals than one launch holds");
+    const sspp_job* j0 = jobs[0];
+    for (int g = 0; g < G; ++g) {
+        const sspp_job* j = jobs[g];
+        if (!j || j->kind != 1 || n > j->max_batch) return sspp::set_error(SSPP_E_INVAL, "tsp_eval_ces_group: bad job");
+        bool same = j->scene == j0->scene && j->n == j0->n && j->K == j0->K && j->cp == j0->cp &&
+                    j->lpc == j0->lpc && j->cpb == j0->cpb && j->lds == j0->lds && j->z_min == j0->z_min &&
+                    j->w_col == j0->w_col && j->floor_z_min == j0->floor_z_min &&
+                    j->floor_margin == j0->floor_margin && j->floor_scale == j0->floor_scale &&
+                    j->tsp_generic == j0->tsp_generic && j->tsp_form == j0->tsp_form &&
+                    j->d_tab && j->h_knots == j0->h_knots && evs[g].samples == evs[0].samples &&
+                    evs[g].slot0 == 0;
+        for (int i = 0; i < 4; ++i) same = same && j->lo[i] == j0->lo[i] && j->hi[i] == j0->hi[i];
+        if (!same) return sspp::set_error(SSPP_E_UNSUPPORTED, "goals differ beyond start / end / seed");
+        const TspCesEval& e = evs[g];
+        const TspCesOut& o = outs[g];
+        if (!e.fixed || !e.nfixed || !e.mean || !e.sigma || !o.L || !o.Cnf || !o.Cwf || !o.cost || !o.status || !o.vias)
+            return sspp::set_error(SSPP_E_INVAL, "tsp_eval_ces_group: null argument");
+    }
+    TspK k = tsp_k(j0, 0, n);
+    k.ces = 1; k.slot0 = 0; k.samples = evs[0].samples;
+    const bool pp_ok = j0->cp <= 64 && k.sc.npairs <= 64 && n <= j0->part_cap;
+    const int pp_opt = j0->tsp_form;
+    if (pp_ok && (pp_opt < 0 ? n <= kTspPpMaxBatch : (pp_opt == 1 || pp_opt == 2)))
+        return sspp::set_error(SSPP_E_UNSUPPORTED, "pair-split batch size: goal by goal");
+    const int mode = tsp_large_mode(j0, k);
+    TspGoals goals{};
+    goals.n = G;
+    goals.nblk = (int)((n + j0->cpb - 1) / j0->cpb);
+    for (int g = 0; g < G; ++g) {
+        const TspCesEval& e = evs[g];
+        const TspCesOut& o = outs[g];
+        TspGoal& q = goals.g[g];
+        for (int i = 0; i < 4; ++i) { q.start[i] = e.start[i]; q.end[i] = e.end[i]; }
+        q.seed = jobs[g]->seed; q.first_id = e.first_id;
+        q.fixed = e.fixed; q.nfixed = e.nfixed; q.mean = e.mean; q.sigma = e.sigma;
+        q.vias_out = o.vias; q.oL = o.L; q.oCnf = o.Cnf; q.oCwf = o.Cwf; q.ocost = o.cost; q.ostatus = o.status;
+        jobs[g]->last_form = mode;
+    }
+    hipError_t e = entry_tsp_group<0>(k, goals, j0, goals.nblk * G, (hipStream_t)stream, mode);
+    if (e != hipSuccess) return hip_fail(e, "k_tsp_group launch");
+    return SSPP_OK;
 }
 
 extern "C" int sspp_job_tsp_sample_score(sspp_job* j, int64_t first_id, int64_t B, double* d_L, double* d_Cnf,

@@ -463,6 +463,20 @@ class CesPlanner:
         check(lib().sspp_ces_plan(self._h, _dptr(s), _dptr(e), int(bool(iterate)),
                                   int(iterations), _stream(stream)), "ces plan")
 
+    @staticmethod
+    def plan_group(planners, starts, ends, iterate=False, iterations=1, stream=None):
+        """iterations x plan(start_g, end_g, iterate) of every planner, as one chain of batched
+        launches on `stream` (sspp_ces_plan_group: one k_tsp_group per iteration over every
+        goal's slots).  Each planner's results equal its own plan(); single-rank planners that
+        share the scene, vias, checks, bounds and CES configuration (others run one by one)."""
+        pls = list(planners)
+        G = len(pls)
+        s = _f64(np.asarray(starts, dtype=np.float64).reshape(G, 4), 4 * G)
+        e = _f64(np.asarray(ends, dtype=np.float64).reshape(G, 4), 4 * G)
+        hs = (C.c_void_p * G)(*[p._h.value for p in pls])
+        check(lib().sspp_ces_plan_group(C.cast(hs, C.c_void_p), G, _dptr(s), _dptr(e), int(bool(iterate)), int(iterations),
+                                        _stream(stream)), "ces plan group")
+
     def read(self):
         """Synchronous copy of the last iteration: per-candidate results and the state."""
         st = CesState()

@@ -427,3 +427,40 @@ def test_elite_fraction_above_one_rejected(cuda):
     with pytest.raises(S.SsppError, match="elite_fraction"):
         S.CesPlanner(scene, sample_count=100, check_points=32, elite_fraction=1.5)
     S.CesPlanner(scene, sample_count=100, check_points=32, elite_fraction=1.0)  # accepted
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("samples,iters", [(4096, 3), (300, 2)])
+def test_ces_plan_group_matches_single(cuda, samples, iters):
+    """sspp_ces_plan_group (BASELINE configs[4]: every goal's CES iteration in one chain of batched
+    launches, one k_tsp_group evaluation per iteration) against each planner's own sspp_ces_plan:
+    every read() field bit-identical per goal after `iters` iterations, then one more iteration
+    continuing both (iterate=True).  300 samples is the pair-split size: the group runs goal by
+    goal there, with the same results."""
+    import bench
+    import sspp_amd as S
+    model = S.Model(ROBOCRANE)
+    body = model.body_id("gripper_collision_with_block/")
+    scene = S.Scene(model, 1, body)
+    goals = bench.MULTIGOAL
+    starts = np.array([g[0] for g in goals])
+    ends = np.array([g[1] for g in goals])
+
+    def make():
+        return [S.CesPlanner(scene, sample_count=samples, check_points=128, init_points=3,
+                             limits_min=bench.MG_LO, limits_max=bench.MG_HI, seed=S.DEFAULT_SEED + g)
+                for g in range(len(goals))]
+    solo, group = make(), make()
+    for p, st, en in zip(solo, starts, ends):
+        p.plan(st, en, iterate=False, iterations=iters)
+    S.CesPlanner.plan_group(group, starts, ends, iterate=False, iterations=iters)
+    for round_ in range(2):
+        for g, (a, b) in enumerate(zip(solo, group)):
+            ra, rb = a.read(), b.read()
+            for k in ra:
+                np.testing.assert_array_equal(np.asarray(ra[k]), np.asarray(rb[k]), err_msg="goal %d %s" % (g, k))
+        if round_ == 0:
+            for p, st, en in zip(solo, starts, ends):
+                p.plan(st, en, iterate=True, iterations=1)
+            S.CesPlanner.plan_group(group, starts, ends, iterate=True, iterations=1)
+    assert sum(p.read()["n_success"] for p in solo) > 0

@@ -15,9 +15,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import KERNEL_REV  # noqa: E402  (records of another kernel revision are not attached)
 
 # record keys: the bench config, or config_b<batch>_w<waypoints> off the default shape
-KERNEL = {"robocrane": "k_sspp_c2f", "stacking": "k_tsp", "multigoal": "k_tsp",
+KERNEL = {"robocrane": "k_sspp_c2f", "stacking": "k_tsp", "multigoal": "k_tsp_group",
           "robocrane_b32768_w256": "k_sspp_c2f", "robocrane_spl20": "k_sspp_c2f"}
-PER_LAUNCH = {"robocrane": 40 * 4096, "stacking": 16384, "multigoal": 4098,
+PER_LAUNCH = {"robocrane": 40 * 4096, "stacking": 16384, "multigoal": 8 * 4098,
               "robocrane_b32768_w256": 40 * 32768, "robocrane_spl20": 20 * 4096}
 STEPS = {"robocrane": "--steps 80 --warmup 4 (40 steps x 4096 candidates per launch)",
          "stacking": "--config stacking --steps 4 --warmup 1",
