@@ -72,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--tsp-form", type=int, default=None,
                     help="stacking: force the k_tsp form (SSPP_OPT_TSP_FORM 0..3; tuning, every form "
                          "gives bit-identical results)")
+    ap.add_argument("--tsp-rep", type=int, default=None,
+                    help="stacking: k_tsp sub-batches per workgroup (SSPP_OPT_TSP_REP 1..8, -1 by "
+                         "batch size; tuning, bit-identical results)")
     ap.add_argument("--mg-group", type=int, default=1, choices=[0, 1],
                     help="multigoal: this rank's goals as one chain of batched launches per "
                          "iteration (sspp_ces_plan_group, one k_tsp_group over every goal; default) "
@@ -211,6 +214,9 @@ def setup_stacking(args, device):
     if args.tsp_form is not None:
         for j in jobs:
             j.set_option(S.OPT_TSP_FORM, args.tsp_form)
+    if args.tsp_rep is not None:
+        for j in jobs:
+            j.set_option(S.OPT_TSP_REP, args.tsp_rep)
     bufs = [j.alloc(B, device=device) for j in jobs]
     job = jobs[0]
 
@@ -232,7 +238,8 @@ def setup_stacking(args, device):
     # 3 deferred box-box contact polygons, ...)
     ctx = dict(kind="tsp", job=job, start=start, end=end, mean=mean, sigma=sigma, lo=lo, hi=hi,
                cp=cp, scene_path=model.path, body=model.body_id("block1"),
-               effective=lambda: dict(tsp_form=int(job.get_option(S.OPT_TSP_FORM))))
+               effective=lambda: dict(tsp_form=int(job.get_option(S.OPT_TSP_FORM)),
+                                      tsp_rep=int(job.get_option(S.OPT_TSP_REP))))
     return B, step, kernel_only, bytes_per, flops_per, meta, ctx
 
 

@@ -168,7 +168,7 @@ SIGNATURES = {
 OPT_SHAPE_NT, OPT_SHAPE_G1, OPT_ORDER, OPT_TSP_FORM, OPT_TSP_GENERIC = 1, 2, 3, 4, 5
 OPT_SAMPLER, OPT_LAST_NT, OPT_LAST_G1, OPT_WP_ORDER, OPT_PREPASS_US, OPT_NPAIRS = 6, 7, 8, 9, 10, 11
 OPT_CYLBOX, OPT_F32, OPT_LAST_F32, OPT_CREATE_US, OPT_PREPASS_STATE = 12, 13, 14, 15, 16
-OPT_SPLIT, OPT_LAST_SPLIT = 17, 18
+OPT_SPLIT, OPT_LAST_SPLIT, OPT_TSP_REP = 17, 18, 19
 OPT_CES_FUSED = 101
 
 

@@ -31,6 +31,13 @@
 #include <vector>
 
 #include "model.h"
+#ifdef SSPP_TSP_STATS  // profiling builds only: point_collide's pair work (tools/tsp_stats.py)
+__device__ unsigned long long g_tsp_stats[16];
+#define TSP_STAT(i, c) do { const unsigned long long m_ = __ballot(c), a_ = __ballot(1);                  \
+        if (__lane_id() == __builtin_ctzll(a_) && m_) atomicAdd(&g_tsp_stats[i], (unsigned long long)__popcll(m_)); } while (0)
+#else
+#define TSP_STAT(i, c) do { } while (0)
+#endif
 #ifdef SSPP_C2F_STATS  // profiling builds only (tools/build_variant.sh stats -DSSPP_C2F_STATS)
 __device__ unsigned long long g_c2f_stats[16];
 #define SSPP_CB_STAT(i) atomicAdd(&g_c2f_stats[i], 1ull)
@@ -221,6 +228,7 @@ struct TspK {
     double* rec_term;       // [B][64][64]
     unsigned* arrive;       // [B], zero between launches (the last arriver re-arms it)
     int npg;                // workgroups per candidate
+    int rep;                // k_tsp: sub-batches of cpb candidates per workgroup (tsp_rep)
 };
 
 // ---------------------------------------------------------------- Philox4x32-10 + Box-Muller
@@ -583,6 +591,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
         rec_pose[3] = mR[0][0]; rec_pose[4] = mR[0][1]; rec_pose[5] = mR[0][3]; rec_pose[6] = mR[0][4];
         rec_pose[7] = mR[0][8];
     }
+    if (DEEP) TSP_STAT(6, true);  // waypoint lanes
     double acc = 0.0;
     int cur = -1;
     double gp[3], gmat[9];
@@ -627,6 +636,13 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
         }
         const bool near = pair_near(pr, G.rbound, gp, op, om);
         int nd = 0, nc = 0;
+        if (DEEP) {
+            TSP_STAT(0, true);
+            TSP_STAT(1, near);
+            TSP_STAT(2, near && G.type == 6 && pr.otype == 6);
+            TSP_STAT(3, near && (G.type == 5 || pr.otype == 5));
+            TSP_STAT(4, near && (G.type == 0 || pr.otype == 0));
+        }
         if (near) {
             if (!ONEGEOM && !have_rot) {
                 const bool second = NM > 1 && G.mover == 1;
@@ -648,6 +664,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                 nc = collide<DEEP, CB, DEEP, false, UP>(pr.otype, op, om, pr.osize, G.type, gp, gmat, G.size, pr.margin, &nd);
             }
         }
+        if (DEEP) TSP_STAT(5, nd > 0);
         if (RECD) ((unsigned char*)rec_nd)[k] = (unsigned char)nd;
         if (!DEEP) {
             // the loop trip is wave-uniform, so every active lane reaches this vote
@@ -2265,29 +2282,38 @@ __device__ __forceinline__ void tsp_body(
     constexpr int D = 4, P = 2, P1 = 3;
     const int tid = threadIdx.x, lpc = a.lpc, cpb = a.cpb, n = a.n, cp = a.cp;
     const int slot = tid / lpc, lane = tid - slot * lpc;
-    const long long cand0 = (long long)blk * cpb;
+    // rep sub-batches of cpb candidates per workgroup: one prologue (sampling, QR) over all of
+    // them, then the waypoint loop per sub-batch (tsp_rep: fewer, longer workgroups)
+    // (the deferred-polygon form 3 only: in the other forms the loop's live state costs spills)
+    const int rep = (DEF == 1 && a.rep > 1) ? a.rep : 1, cpr = cpb * rep;
+    const long long candR = (long long)blk * cpr;
     const int ndof = n * D;
-    double* s_V = smem;                      // [cpb][n][4]
-    double* s_ctrl = s_V + cpb * ndof;       // [cpb][n][4]
-    double* s_wsum = s_ctrl + cpb * ndof;    // [3][4]
+    double* s_V = smem;                      // [cpr][n][4]
+    double* s_ctrl = s_V + cpr * ndof;       // [cpr][n][4]
+    double* s_wsum = s_ctrl + cpr * ndof;    // [3][4]
     double* s_best = s_wsum + 3 * (kBlock / 64);
-    int* s_stat = (int*)(s_best + 4);        // [cpb]
+    int* s_stat = (int*)(s_best + (cpr > 4 ? cpr : 4));  // [cpr]
     // DEF 1: per-lane records [kBlock][np] (terms, counts), mover poses [kBlock][8], deferred list;
     // DEF 2: per-lane counts [kBlock][np] and mover poses only
     const int npr = DEF ? a.sc.npairs : 0;
-    double* s_rterm = (double*)(s_stat + ((cpb + 1) & ~1));
+    double* s_rterm = (double*)(s_stat + ((cpr + 1) & ~1));
     double* s_rpose = s_rterm + (DEF == 1 ? kBlock * npr : 0);
     unsigned char* s_rnd = (unsigned char*)(s_rpose + (DEF ? kBlock * 8 : 0));
     int* s_items = (int*)(s_rnd + ((kBlock * npr + 3) & ~3));
     int* s_nitems = s_items + kBlock * npr;
 
-    const long long nvalid = min((long long)cpb, a.B - cand0);
+    const long long nvR = min((long long)cpr, a.B - candR);
     const long long nfx = a.ces ? (long long)*pv.nfixed : 0;  // uniform: scalar load
-    tsp_prologue(a, pv, Minv, mean, sigma, vias_in, vias_out, tid, kBlock, cpb, cand0, nvalid, nfx, s_V, s_ctrl);
+    tsp_prologue(a, pv, Minv, mean, sigma, vias_in, vias_out, tid, kBlock, cpr, candR, nvR, nfx, s_V, s_ctrl);
 
+    for (int r = 0; r < rep; ++r) {  // workgroup-uniform
+    const long long cand0 = candR + (long long)r * cpb;
+    const long long nvalid = min((long long)cpb, a.B - cand0);  // <= 0 past a ragged batch's end
+    if (DEF == 1 && nvalid <= 0) break;  // (the other forms have one sub-batch)
+    if (r > 0) __syncthreads();  // the previous sub-batch is done with the sums and records
     // Evaluator::eval_one_pass (tsp_evaluator.h:18-32), waypoint i = 1..cp per lane
     const bool valid = slot < nvalid;
-    const double* myc = s_ctrl + slot * ndof;
+    const double* myc = s_ctrl + (r * cpb + slot) * ndof;
     const unsigned long long mask = hull_mask<D, NM, 1>(myc, n, a.sc.npairs, (cpair_t)T.pairs,
                                                         (cgeom_t)T.geoms, (cmover_t)T.movers);
     double aL = 0.0, aC = 0.0, aW = 0.0;
@@ -2436,17 +2462,18 @@ __device__ __forceinline__ void tsp_body(
         }
         oL[c] = L; oCnf[c] = Cn; oCwf[c] = Cw; ocost[c] = cost;
         ostatus[c] = (unsigned char)st;
-        s_stat[slot] = st;
-        s_best[slot] = cost;
+        s_stat[r * cpb + slot] = st;
+        s_best[r * cpb + slot] = cost;
     }
+    }  // sub-batches
     __syncthreads();
     BlockBest bb;
     if (tid == 0) {
         bb.cost = INFINITY; bb.idx = -1; bb.count = 0; bb.pad = 0;
-        for (int s = 0; s < nvalid; ++s) {
+        for (int s = 0; s < nvR; ++s) {
             if (!s_stat[s]) continue;
             bb.count++;
-            if (s_best[s] < bb.cost) { bb.cost = s_best[s]; bb.idx = pv.first_id + cand0 + s; }
+            if (s_best[s] < bb.cost) { bb.cost = s_best[s]; bb.idx = pv.first_id + candR + s; }
         }
     }
     if (part || best) finish_batch(bb, part, sync, best);  // (CES slot mode: records unused)
@@ -2691,6 +2718,12 @@ inline size_t tsp_def_lds(int np) {
 inline size_t tsp_def2_lds(int np) {
     return sizeof(double) * (size_t)kBlock * 8 + (((size_t)kBlock * np + 7) & ~(size_t)7) + 16;
 }
+// k_tsp's LDS before the DEF records, for rep sub-batches of cpb candidates (tsp_body's layout)
+inline size_t tsp_base_lds(int cpb, int n, int rep) {
+    const int cpr = cpb * (rep > 1 ? rep : 1);
+    return sizeof(double) * ((size_t)2 * cpr * n * 4 + 3 * (kBlock / 64) + (cpr > 4 ? cpr : 4)) +
+           sizeof(int) * (size_t)((cpr + 1) & ~1);
+}
 
 inline int lanes_for(int items) {
     int l = ((items + 63) / 64) * 64;
@@ -2761,6 +2794,7 @@ struct sspp_job {
     // TaskSpacePlanner options (sspp_job_set_option): evaluation form (-1 automatic, 0 k_tsp,
     // 1 k_tsp_pp, 2 k_tsp_pp2) and the generic (non-upright) narrowphase
     int tsp_form = -1, tsp_generic = 0, last_form = -1;
+    int tsp_rep = -1, last_rep = 1;     // SSPP_OPT_TSP_REP
     unsigned* d_pp_nd = nullptr;     // k_tsp_pp2 records / arrival counters (allocated on first use)
     double* d_pp_term = nullptr;
     unsigned* d_pp_arrive = nullptr;
@@ -3031,7 +3065,8 @@ hipError_t entry_tsp(const TspK& k, const sspp_job* j, int nblk, const double* m
     // pp == 3: the deferred-polygon form (host-checked: one waypoint per lane, <= kDefPairs pairs);
     // pp == 4: the lane-local deferred polygons (one waypoint per lane, <= 64 pairs)
     const int def = pp == 3 ? 1 : (pp == 4 ? 2 : 0);
-    const size_t lds = def == 1 ? j->lds + tsp_def_lds(k.sc.npairs) : (def == 2 ? j->lds + tsp_def2_lds(k.sc.npairs) : j->lds);
+    const size_t base = tsp_base_lds(j->cpb, j->n, k.rep);
+    const size_t lds = def == 1 ? base + tsp_def_lds(k.sc.npairs) : (def == 2 ? base + tsp_def2_lds(k.sc.npairs) : base);
 #define SSPP_LAUNCH_TSP_ALL(DEFV)                                                                         \
     if (og && cbm == 1) SSPP_LAUNCH_TSP(true, 1, false, DEFV);                                            \
     else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSP(true, 2, true, DEFV); else SSPP_LAUNCH_TSP(true, 2, false, DEFV); } \
@@ -3061,7 +3096,8 @@ hipError_t entry_tsp_group(const TspK& k, const TspGoals& goals, const sspp_job*
     const int cbm = k.sc.cylbox ? (k.sc.cbup ? 2 : 1) : 0;
     const bool up = k.sc.upright && cbm != 1;
     const int def = mode == 3 ? 1 : (mode == 4 ? 2 : 0);
-    const size_t lds = def == 1 ? j->lds + tsp_def_lds(k.sc.npairs) : (def == 2 ? j->lds + tsp_def2_lds(k.sc.npairs) : j->lds);
+    const size_t base = tsp_base_lds(j->cpb, j->n, k.rep);
+    const size_t lds = def == 1 ? base + tsp_def_lds(k.sc.npairs) : (def == 2 ? base + tsp_def2_lds(k.sc.npairs) : base);
 #define SSPP_LAUNCH_TSPG_ALL(DEFV)                                                                        \
     if (og && cbm == 1) SSPP_LAUNCH_TSPG(true, 1, false, DEFV);                                           \
     else if (og && cbm == 2) { if (up) SSPP_LAUNCH_TSPG(true, 2, true, DEFV); else SSPP_LAUNCH_TSPG(true, 2, false, DEFV); } \

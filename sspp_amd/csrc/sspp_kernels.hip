@@ -1214,6 +1214,11 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
             if (j->kind != 0 || value < 0 || value > 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SPLIT: 0 or 1");
             j->opt_split = (int)value;
             return SSPP_OK;
+        case SSPP_OPT_TSP_REP:
+            if (j->kind != 1 || value < -1 || value == 0 || value > 8)
+                return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_REP: -1 or 1..8");
+            j->tsp_rep = (int)value;
+            return SSPP_OK;
     }
     return sspp::set_error(SSPP_E_INVAL, "unknown or read-only option");
 }
@@ -1238,6 +1243,7 @@ extern "C" int sspp_job_get_option(const sspp_job* j, int key, int64_t* value) {
         case SSPP_OPT_CREATE_US: *value = (int64_t)(j->create_ms * 1e3); return SSPP_OK;
         case SSPP_OPT_SPLIT: *value = j->opt_split; return SSPP_OK;
         case SSPP_OPT_LAST_SPLIT: *value = j->last_split; return SSPP_OK;
+        case SSPP_OPT_TSP_REP: *value = j->kind == 1 ? j->last_rep : 0; return SSPP_OK;
         case SSPP_OPT_PREPASS_STATE: *value = j->prepass_state.load(std::memory_order_acquire); return SSPP_OK;
     }
     return sspp::set_error(SSPP_E_INVAL, "unknown option");
@@ -1296,6 +1302,14 @@ extern "C" int sspp_job_create_tsp(const sspp_scene* scene, const sspp_tsp_args*
     }
     *out = j;
     return SSPP_OK;
+}
+
+// default sub-batches per k_tsp workgroup (form 3): enough to bring the grid down to about one
+// resident round of 4-wave workgroups (1024 on 256 CUs), at most 8.  Stacking (16384 candidates,
+// 2 per sub-batch): 8 — 91.8 / 107.0 / 117.3 / 123.2 M cand/s at 1 / 2 / 4 / 8 (profiles/r05u_*)
+static int tsp_auto_rep(const sspp_job* j, int64_t B) {
+    const int64_t r = B / ((int64_t)j->cpb * 1024);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(8, r));
 }
 
 // the launch's TspK for job j (run_tsp, tsp_eval_ces_group)
@@ -1377,7 +1391,17 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     // lane-local deferred polygons (mode 4): one waypoint per lane, up to 64 pairs, some of them
     // box-box; the default where mode 3 does not apply (the gripper's 48 pairs)
     if (mode == 0) mode = tsp_large_mode(j, k);
-    const int nblk = mode == 2 ? (int)B * npg : mode == 1 ? (int)B : (int)((B + j->cpb - 1) / j->cpb);
+    // k_tsp forms: rep sub-batches per workgroup (SSPP_OPT_TSP_REP; -1: REP_AUTO below)
+    k.rep = 1;
+    if (mode == 3) {
+        int rep = j->tsp_rep > 0 ? j->tsp_rep : tsp_auto_rep(j, B);
+        const size_t extra = tsp_def_lds(k.sc.npairs);
+        while (rep > 1 && tsp_base_lds(j->cpb, j->n, rep) + extra > 64 * 1024) --rep;
+        k.rep = rep;
+    }
+    j->last_rep = k.rep;
+    const int cpr = j->cpb * k.rep;
+    const int nblk = mode == 2 ? (int)B * npg : mode == 1 ? (int)B : (int)((B + cpr - 1) / cpr);
     j->last_form = mode;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e0 = entry_tsp<0>(k, j, nblk, mean, sigma, d_vias, d_vias_out, d_L, d_Cnf, d_Cwf, d_cost, d_status,
@@ -1431,7 +1455,7 @@ int sspp::tsp_eval_ces_group(sspp_job* const* jobs, const TspCesEval* evs, const
             return sspp::set_error(SSPP_E_INVAL, "tsp_eval_ces_group: null argument");
     }
     TspK k = tsp_k(j0, 0, n);
-    k.ces = 1; k.slot0 = 0; k.samples = evs[0].samples;
+    k.ces = 1; k.slot0 = 0; k.samples = evs[0].samples; k.rep = 1;
     const bool pp_ok = j0->cp <= 64 && k.sc.npairs <= 64 && n <= j0->part_cap;
     const int pp_opt = j0->tsp_form;
     if (pp_ok && (pp_opt < 0 ? n <= kTspPpMaxBatch : (pp_opt == 1 || pp_opt == 2)))
@@ -1656,6 +1680,17 @@ extern "C" int sspp_best_reduce_steps(const sspp_best* d_parts, int R, int G, ss
     return SSPP_OK;
 }
 
+#ifdef SSPP_TSP_STATS
+extern "C" int sspp_debug_tsp_stats(unsigned long long* out, int reset) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tsp_stats), sizeof(unsigned long long) * 16);
+    if (reset) {
+        unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tsp_stats), z, sizeof z);
+    }
+    return 0;
+}
+#endif
 #ifdef SSPP_C2F_STATS
 extern "C" int sspp_debug_c2f_stats(unsigned long long* out, int reset) {
     hipDeviceSynchronize();

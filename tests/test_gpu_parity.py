@@ -738,3 +738,31 @@ def test_split_launch_is_invisible(robocrane, sigma, spl, B):
         np.testing.assert_array_equal(x, y)
     if sigma >= 0.08:  # (sigma 0.02 stays near the infeasible straight path: nothing feasible)
         assert (b1[:, 2] > 0).any()
+
+
+@pytest.mark.parametrize("rep", [2, 3, 8])
+def test_tsp_rep_is_invisible(cuda, rep):
+    """SSPP_OPT_TSP_REP (k_tsp sub-batches per workgroup, one prologue for all of them) against
+    one sub-batch per workgroup: every output bit-identical, the argmin record included, on a
+    ragged batch (not a multiple of the workgroup's candidates)."""
+    import sspp_amd as S
+    import torch
+    model = S.Model(os.path.join(SCENES, "stacking.xml"))
+    scene = S.Scene(model, 1, "block1")
+    start = model.body_point("block1") + np.array([0, 0, 0.02, 0])
+    end = model.body_point("block2") + np.array([0, 0, 0.22, 0])
+    mean = (start + 0.5 * (end - start)).reshape(1, 4)
+    sigma = np.full((1, 4), 0.2)
+    lo, hi = np.array([-0.5, -0.5, 0.0, -1.6]), np.array([0.5, 0.5, 0.6, 1.6])
+    B = 3001
+    res = {}
+    for r in (1, rep):
+        job = S.TspJob(scene, start, end, 1, 128, mean=mean, sigma=sigma, lo=lo, hi=hi, z_min=0.0, max_batch=B)
+        job.set_option(S.OPT_TSP_REP, r)
+        q = job.alloc(B)
+        job.sample_score(77, B, q["L"], q["Cnf"], q["Cwf"], q["status"], q["cost"], q["best"])
+        torch.cuda.synchronize()
+        assert job.get_option(S.OPT_TSP_REP) == r
+        res[r] = {k: v.cpu().numpy() for k, v in q.items()}
+    for k in res[1]:
+        np.testing.assert_array_equal(res[rep][k], res[1][k], err_msg=k)
