@@ -31,6 +31,10 @@
 #include <vector>
 
 #include "model.h"
+// k_tsp forms (bit f = form f) that run several sub-batches per workgroup (SSPP_OPT_TSP_REP)
+#ifndef SSPP_TSP_REP_FORMS
+#define SSPP_TSP_REP_FORMS (1 << 3)
+#endif
 #ifdef SSPP_TSP_STATS  // profiling builds only: point_collide's pair work (tools/tsp_stats.py)
 __device__ unsigned long long g_tsp_stats[16];
 #define TSP_STAT(i, c) do { const unsigned long long m_ = __ballot(c), a_ = __ballot(1);                  \
@@ -2284,8 +2288,9 @@ __device__ __forceinline__ void tsp_body(
     const int slot = tid / lpc, lane = tid - slot * lpc;
     // rep sub-batches of cpb candidates per workgroup: one prologue (sampling, QR) over all of
     // them, then the waypoint loop per sub-batch (tsp_rep: fewer, longer workgroups)
-    // (the deferred-polygon form 3 only: in the other forms the loop's live state costs spills)
-    const int rep = (DEF == 1 && a.rep > 1) ? a.rep : 1, cpr = cpb * rep;
+    // (forms in SSPP_TSP_REP_FORMS only: elsewhere the loop's live state costs spills)
+    constexpr bool REP_OK = ((SSPP_TSP_REP_FORMS >> (DEF == 1 ? 3 : DEF == 2 ? 4 : 0)) & 1) != 0;
+    const int rep = (REP_OK && a.rep > 1) ? a.rep : 1, cpr = cpb * rep;
     const long long candR = (long long)blk * cpr;
     const int ndof = n * D;
     double* s_V = smem;                      // [cpr][n][4]
@@ -2306,10 +2311,11 @@ __device__ __forceinline__ void tsp_body(
     const long long nfx = a.ces ? (long long)*pv.nfixed : 0;  // uniform: scalar load
     tsp_prologue(a, pv, Minv, mean, sigma, vias_in, vias_out, tid, kBlock, cpr, candR, nvR, nfx, s_V, s_ctrl);
 
-    for (int r = 0; r < rep; ++r) {  // workgroup-uniform
+    // one sub-batch; the forms without sub-batches compile it once, with no loop around it
+    auto sub = [&](const int r) -> bool {
     const long long cand0 = candR + (long long)r * cpb;
     const long long nvalid = min((long long)cpb, a.B - cand0);  // <= 0 past a ragged batch's end
-    if (DEF == 1 && nvalid <= 0) break;  // (the other forms have one sub-batch)
+    if (REP_OK && nvalid <= 0) return false;  // past a ragged batch's end
     if (r > 0) __syncthreads();  // the previous sub-batch is done with the sums and records
     // Evaluator::eval_one_pass (tsp_evaluator.h:18-32), waypoint i = 1..cp per lane
     const bool valid = slot < nvalid;
@@ -2465,7 +2471,14 @@ __device__ __forceinline__ void tsp_body(
         s_stat[r * cpb + slot] = st;
         s_best[r * cpb + slot] = cost;
     }
-    }  // sub-batches
+    return true;
+    };
+    if constexpr (REP_OK) {
+        for (int r = 0; r < rep; ++r)  // workgroup-uniform
+            if (!sub(r)) break;
+    } else {
+        sub(0);
+    }
     __syncthreads();
     BlockBest bb;
     if (tid == 0) {

@@ -1312,6 +1312,15 @@ static int tsp_auto_rep(const sspp_job* j, int64_t B) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(8, r));
 }
 
+// sub-batches per workgroup for a k_tsp launch of form `mode` (1 where the form runs one)
+static int tsp_rep_for(const sspp_job* j, const TspK& k, int mode, int64_t B) {
+    if ((mode != 3 && mode != 4) || !((SSPP_TSP_REP_FORMS >> mode) & 1)) return 1;
+    int rep = j->tsp_rep > 0 ? j->tsp_rep : tsp_auto_rep(j, B);
+    const size_t extra = mode == 3 ? tsp_def_lds(k.sc.npairs) : tsp_def2_lds(k.sc.npairs);
+    while (rep > 1 && tsp_base_lds(j->cpb, j->n, rep) + extra > 64 * 1024) --rep;
+    return rep;
+}
+
 // the launch's TspK for job j (run_tsp, tsp_eval_ces_group)
 static TspK tsp_k(const sspp_job* j, int64_t first_id, int64_t B) {
     TspK k{};
@@ -1392,13 +1401,7 @@ static int run_tsp(sspp_job* j, const double* d_vias, int64_t first_id, int64_t 
     // box-box; the default where mode 3 does not apply (the gripper's 48 pairs)
     if (mode == 0) mode = tsp_large_mode(j, k);
     // k_tsp forms: rep sub-batches per workgroup (SSPP_OPT_TSP_REP; -1: REP_AUTO below)
-    k.rep = 1;
-    if (mode == 3) {
-        int rep = j->tsp_rep > 0 ? j->tsp_rep : tsp_auto_rep(j, B);
-        const size_t extra = tsp_def_lds(k.sc.npairs);
-        while (rep > 1 && tsp_base_lds(j->cpb, j->n, rep) + extra > 64 * 1024) --rep;
-        k.rep = rep;
-    }
+    k.rep = tsp_rep_for(j, k, mode, B);
     j->last_rep = k.rep;
     const int cpr = j->cpb * k.rep;
     const int nblk = mode == 2 ? (int)B * npg : mode == 1 ? (int)B : (int)((B + cpr - 1) / cpr);
@@ -1455,15 +1458,16 @@ int sspp::tsp_eval_ces_group(sspp_job* const* jobs, const TspCesEval* evs, const
             return sspp::set_error(SSPP_E_INVAL, "tsp_eval_ces_group: null argument");
     }
     TspK k = tsp_k(j0, 0, n);
-    k.ces = 1; k.slot0 = 0; k.samples = evs[0].samples; k.rep = 1;
+    k.ces = 1; k.slot0 = 0; k.samples = evs[0].samples;
     const bool pp_ok = j0->cp <= 64 && k.sc.npairs <= 64 && n <= j0->part_cap;
     const int pp_opt = j0->tsp_form;
     if (pp_ok && (pp_opt < 0 ? n <= kTspPpMaxBatch : (pp_opt == 1 || pp_opt == 2)))
         return sspp::set_error(SSPP_E_UNSUPPORTED, "pair-split batch size: goal by goal");
     const int mode = tsp_large_mode(j0, k);
+    k.rep = tsp_rep_for(j0, k, mode, n * G);
     TspGoals goals{};
     goals.n = G;
-    goals.nblk = (int)((n + j0->cpb - 1) / j0->cpb);
+    goals.nblk = (int)((n + (int64_t)j0->cpb * k.rep - 1) / ((int64_t)j0->cpb * k.rep));
     for (int g = 0; g < G; ++g) {
         const TspCesEval& e = evs[g];
         const TspCesOut& o = outs[g];
@@ -1473,6 +1477,7 @@ int sspp::tsp_eval_ces_group(sspp_job* const* jobs, const TspCesEval* evs, const
         q.fixed = e.fixed; q.nfixed = e.nfixed; q.mean = e.mean; q.sigma = e.sigma;
         q.vias_out = o.vias; q.oL = o.L; q.oCnf = o.Cnf; q.oCwf = o.Cwf; q.ocost = o.cost; q.ostatus = o.status;
         jobs[g]->last_form = mode;
+        jobs[g]->last_rep = k.rep;
     }
     hipError_t e = entry_tsp_group<0>(k, goals, j0, goals.nblk * G, (hipStream_t)stream, mode);
     if (e != hipSuccess) return hip_fail(e, "k_tsp_group launch");
