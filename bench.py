@@ -73,7 +73,7 @@ def parse(argv=None):
                     help="stacking: force the k_tsp form (SSPP_OPT_TSP_FORM 0..3; tuning, every form "
                          "gives bit-identical results)")
     ap.add_argument("--tsp-rep", type=int, default=None,
-                    help="stacking: k_tsp sub-batches per workgroup (SSPP_OPT_TSP_REP 1..8, -1 by "
+                    help="stacking: k_tsp sub-batches per workgroup (SSPP_OPT_TSP_REP 1..16, -1 by "
                          "batch size; tuning, bit-identical results)")
     ap.add_argument("--mg-group", type=int, default=1, choices=[0, 1],
                     help="multigoal: this rank's goals as one chain of batched launches per "

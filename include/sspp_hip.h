@@ -247,7 +247,7 @@ void sspp_job_free(sspp_job* job);
                                    workgroup finishes its own.  Results identical either way      */
 #define SSPP_OPT_LAST_SPLIT 18  /* get: the last launch was split                                */
 #define SSPP_OPT_TSP_REP 19     /* TaskSpacePlanner k_tsp form 3: sub-batches of candidates
-                                   per workgroup (one prologue for all of them), 1..8, -1 by batch
+                                   per workgroup (one prologue for all of them), 1..16, -1 by batch
                                    size; get: the last k_tsp launch's                            */
 int sspp_job_set_option(sspp_job* job, int key, int64_t value);
 int sspp_job_get_option(const sspp_job* job, int key, int64_t* value);

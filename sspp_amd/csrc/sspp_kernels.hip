@@ -1215,8 +1215,8 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
             j->opt_split = (int)value;
             return SSPP_OK;
         case SSPP_OPT_TSP_REP:
-            if (j->kind != 1 || value < -1 || value == 0 || value > 8)
-                return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_REP: -1 or 1..8");
+            if (j->kind != 1 || value < -1 || value == 0 || value > 16)
+                return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_REP: -1 or 1..16");
             j->tsp_rep = (int)value;
             return SSPP_OK;
     }
