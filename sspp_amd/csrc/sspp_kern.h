@@ -1789,6 +1789,16 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         unsigned long long* s_id = s_bits + kMaxSteps;
         unsigned* s_cnt = (unsigned*)(s_id + kMaxSteps);
         const int nsteps = a.nsteps;
+        // one round trip for the header and the list's first NT entries: each thread reads
+        // entry tid before it knows the list's length (entries past it are stale and unused)
+        const unsigned nl = __hip_atomic_load(&q.hdr->nlist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned lost = __hip_atomic_load(&q.hdr->lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long rb = 0ull, rid = 0ull, rst = 0ull;
+        if (best_base) {
+            rb = __hip_atomic_load(&q.res[tid].bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rid = __hip_atomic_load(&q.res[tid].id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rst = __hip_atomic_load(&q.res[tid].step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         for (int e = tid; e < nsteps; e += NT) {
             s_bits[e] = __hip_atomic_load(q.hdr->bestbits + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_cnt[e] = __hip_atomic_load(q.hdr->count_feas + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1796,8 +1806,8 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         }
         __syncthreads();
         if (best_base) {
-            const unsigned nl = __hip_atomic_load(&q.hdr->nlist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (unsigned i = tid; i < nl; i += NT) {
+            if ((unsigned)tid < nl && rb == s_bits[rst]) atomicMin(s_id + rst, rid);
+            for (unsigned i = tid + NT; i < nl; i += NT) {
                 const unsigned long long bits = __hip_atomic_load(&q.res[i].bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long id = __hip_atomic_load(&q.res[i].id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const int st = (int)__hip_atomic_load(&q.res[i].step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1811,7 +1821,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                 best_base[e].cost = has ? __longlong_as_double((long long)s_bits[e]) : INFINITY;
                 best_base[e].index = has ? (long long)s_id[e] : -1;
                 best_base[e].count = s_cnt[e];
-                best_base[e].reserved = __hip_atomic_load(&q.hdr->lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                best_base[e].reserved = lost;
             }
             __hip_atomic_store(q.hdr->bestbits + e, 0x7FF0000000000000ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(q.hdr->count_feas + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
