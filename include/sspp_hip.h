@@ -107,7 +107,9 @@ typedef struct sspp_best {
     double cost;      /* +inf when no candidate is feasible */
     int64_t index;    /* global candidate id, -1 when none */
     int64_t count;    /* number of feasible candidates in the batch */
-    int64_t reserved;
+    int64_t reserved; /* 0; a split launch (SSPP_OPT_SPLIT) writes the survivor tickets its hang
+                         guard abandoned, which is 0 unless the launch was not one resident
+                         round (then the step's outputs are incomplete)                   */
 } sspp_best;
 
 typedef struct sspp_scene_info {
