@@ -182,6 +182,32 @@ def setup_robocrane(args, device):
         for j in jobs:
             j.set_option(S.OPT_ORDER, order)
 
+    def validate():
+        # after the timed region: no split launch of any job lost a survivor (the queue's
+        # lost-work check, cumulative per job; a loss would also be in that step's record)
+        lost = sum(j.get_option(S._lib.OPT_SPLIT_LOST) for j in jobs)
+        if lost:
+            raise S.SsppError("split launches lost %d survivors" % lost)
+        return dict(split_lost=lost, split_handoffs=sum(j.get_option(S._lib.OPT_SPLIT_HANDOFFS) for j in jobs))
+
+    def timed_instance(first_id):
+        # one launch exactly as the timed loop issues it (the roofline's executor: jobs[0], the
+        # timed steps per launch); returns per-step (arc, feasible) of steps 0 and spl - 1, the
+        # launch's records and whether it was split
+        import torch
+        spl = roofline_spl(args)
+        if spl == 1:
+            return None
+        if "ex" not in roof:
+            kernel_only(0)  # builds the executor (the roofline launches normally have)
+        roof["ex"].enqueue(spl, first_id, B, roof["best"])
+        torch.cuda.synchronize()
+        arc, fe = roof["ex"].arc_bufs[0].cpu().numpy(), roof["ex"].feas_bufs[0].cpu().numpy()
+        steps = sorted({0, spl - 1})
+        return dict(spl=spl, steps=steps, split=bool(job.get_option(S._lib.OPT_LAST_SPLIT)),
+                    shape=job.config()["shape"], records=S.check_records(roof["best"]),
+                    arc={i: arc[i * B:(i + 1) * B] for i in steps}, feas={i: fe[i * B:(i + 1) * B] for i in steps})
+
     n_, D, p = 10, 7, 3
     # SURVEY §8(d) algorithmic work per candidate
     bytes_per = n_ * D * 8 + 8 + 1
@@ -194,7 +220,7 @@ def setup_robocrane(args, device):
     ctx = dict(kind="sspp", kernel_name="k_sspp_c2f", effective=job.config,
                job=job, knots=knots, ctrl0=ctrl0, W=W, scene_path=model.path, p=p,
                make_executor=make_executor, isolated_step_us=isolated_step_us, set_order=set_order,
-               per_launch=B * roofline_spl(args))
+               validate=validate, timed_instance=timed_instance, per_launch=B * roofline_spl(args))
     return B, step, kernel_only, bytes_per, flops_per, meta, ctx
 
 
@@ -329,14 +355,10 @@ def cpu_baseline(args, ctx, B, device):
     model = mjcf_ref.load(ctx["scene_path"])
     if ctx["kind"] == "multigoal":
         return cpu_baseline_multigoal(args, ctx, model, threads)
+    timed = None
     if ctx["kind"] == "sspp":
         job = ctx["job"]
         osc = O.Scene(model, 0, 7)
-        out = job.alloc(B, device=device, with_ctrl=True)
-        job.sample_score(0, B, out["arc"], out["feasible"], out["best"], ctrl_out=out["ctrl"])
-        torch.cuda.synchronize()
-        ctrl = out["ctrl"].cpu().numpy()
-        arc_g, feas_g = out["arc"].cpu().numpy(), out["feasible"].cpu().numpy()
 
         def run_on(c):
             return O.sspp_score(osc, ctx["knots"], ctx["p"], c, ctx["W"], nthreads=threads)
@@ -344,6 +366,35 @@ def cpu_baseline(args, ctx, B, device):
         def sample(first, n):
             return O.sample_sspp(ctx["ctrl0"], ctx["p"], 0.08, np.ones(7), S.DEFAULT_SEED, first, n,
                                  sampler=O.SAMPLER_FP32 if args.sampler == "fp32" else O.SAMPLER_FP64)
+        # parity on the timed kernel instance itself: one launch of the timed loop's shape (same
+        # executor, steps per launch, split survivor queue), its first and last steps against
+        # the oracle on the same Philox candidates (the sampler is bit-exact with the oracle's)
+        first_t = 1 << 42
+        timed = ctx["timed_instance"](first_t)
+        if timed is not None:
+            par = dict(instance=dict(steps_per_launch=timed["spl"], split=timed["split"], shape=timed["shape"],
+                                     steps_checked=timed["steps"]),
+                       candidates=0, max_abs_cost_diff=0.0, feasible_identical=True, argmin_identical=True,
+                       record_identical=True)
+            for i in timed["steps"]:
+                f0 = first_t + i * B
+                arc_c, feas_c = run_on(sample(f0, B))
+                arc_g, feas_g = timed["arc"][i], timed["feas"][i]
+                fin = np.isfinite(arc_c) & np.isfinite(arc_g)
+                k = O.argmin(arc_c, feas_c)[0]
+                rec = S.decode_best(timed["records"][i])
+                par["candidates"] += B
+                if fin.any():
+                    par["max_abs_cost_diff"] = max(par["max_abs_cost_diff"], float(np.abs(arc_c[fin] - arc_g[fin]).max()))
+                par["feasible_identical"] &= bool(np.array_equal(feas_c, feas_g))
+                par["argmin_identical"] &= bool(k == O.argmin(arc_g, feas_g)[0])
+                par["record_identical"] &= bool(rec[1] == (f0 + k if k >= 0 else -1) and rec[2] == int(feas_c.sum()))
+        else:
+            out = job.alloc(B, device=device, with_ctrl=True)
+            job.sample_score(0, B, out["arc"], out["feasible"], out["best"], ctrl_out=out["ctrl"])
+            torch.cuda.synchronize()
+            ctrl = out["ctrl"].cpu().numpy()
+            arc_g, feas_g = out["arc"].cpu().numpy(), out["feasible"].cpu().numpy()
     else:
         job = ctx["job"]
         osc = O.Scene(model, 1, ctx["body"])
@@ -362,13 +413,16 @@ def cpu_baseline(args, ctx, B, device):
         def sample(first, n):
             return O.sample_tsp(ctx["mean"], ctx["sigma"], ctx["lo"], ctx["hi"], 0.0,
                                 S.DEFAULT_SEED, first, n)
-    # parity on the GPU's own step-0 batch (identical control points / via sets)
-    arc_c, feas_c = run_on(ctrl)
-    fin = np.isfinite(arc_c) & np.isfinite(arc_g)
-    parity = dict(candidates=int(B),
-                  max_abs_cost_diff=float(np.abs(arc_c[fin] - arc_g[fin]).max()) if fin.any() else 0.0,
-                  feasible_identical=bool(np.array_equal(feas_c, feas_g)),
-                  argmin_identical=bool(O.argmin(arc_c, feas_c)[0] == O.argmin(arc_g, feas_g)[0]))
+    if timed is not None:
+        parity = par
+    else:
+        # parity on the GPU's own step-0 batch (identical control points / via sets)
+        arc_c, feas_c = run_on(ctrl)
+        fin = np.isfinite(arc_c) & np.isfinite(arc_g)
+        parity = dict(candidates=int(B),
+                      max_abs_cost_diff=float(np.abs(arc_c[fin] - arc_g[fin]).max()) if fin.any() else 0.0,
+                      feasible_identical=bool(np.array_equal(feas_c, feas_g)),
+                      argmin_identical=bool(O.argmin(arc_c, feas_c)[0] == O.argmin(arc_g, feas_g)[0]))
     # timed: successive batches (sampling included, as in the GPU step) for ~cpu_seconds; the
     # sampler (single-threaded oracle call) and the scorer (OpenMP over candidates) are timed
     # separately as well, so their rates can be told apart
@@ -939,6 +993,8 @@ def main(argv=None):
     # batch (one launch of B candidates, which runs at the latency shape)
     if "effective" in ctx:
         meta.update(ctx["effective"]())
+    if "validate" in ctx:  # the timed launches lost no work (raises otherwise)
+        meta.update(ctx["validate"]())
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, ctx, B, device)

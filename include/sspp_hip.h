@@ -63,6 +63,7 @@ extern "C" {
 #define SSPP_E_NOMEM (-4)
 #define SSPP_E_UNSUPPORTED (-5)
 #define SSPP_E_IO (-6)
+#define SSPP_E_INCOMPLETE (-7) /* a result record reports lost work (sspp_best::reserved != 0) */
 
 /* MuJoCo mjtGeom codes for the supported primitives */
 #define SSPP_GEOM_PLANE 0
@@ -107,9 +108,12 @@ typedef struct sspp_best {
     double cost;      /* +inf when no candidate is feasible */
     int64_t index;    /* global candidate id, -1 when none */
     int64_t count;    /* number of feasible candidates in the batch */
-    int64_t reserved; /* 0; a split launch (SSPP_OPT_SPLIT) writes the survivor tickets its hang
-                         guard abandoned, which is 0 unless the launch was not one resident
-                         round (then the step's outputs are incomplete)                   */
+    int64_t reserved; /* candidates the launch could not finish: 0.  A split launch
+                         (SSPP_OPT_SPLIT) counts its finished survivors against the reserved
+                         queue slots and writes any shortfall here; the reductions below sum
+                         it; every consumer of a record (sspp_best_check, sspp_best_reduce,
+                         the planners, the Python layer) refuses a non-zero value with
+                         SSPP_E_INCOMPLETE, because the step's outputs are then incomplete  */
 } sspp_best;
 
 typedef struct sspp_scene_info {
@@ -248,6 +252,14 @@ void sspp_job_free(sspp_job* job);
                                    and finish queued survivors, whoever sampled them; 0 each
                                    workgroup finishes its own.  Results identical either way      */
 #define SSPP_OPT_LAST_SPLIT 18  /* get: the last launch was split                                */
+#define SSPP_OPT_SPLIT_LINGER_US 20 /* split launches: microseconds a ticket waits for a slot that is
+                                   not reserved yet before it hands the slot to the launch's last
+                                   workgroup (default 10000; 0 = at once: tests).  Results
+                                   identical for every value                                     */
+#define SSPP_OPT_SPLIT_DROP 21  /* tests only: 1 = the last workgroup drops handed-over slots
+                                   instead of finishing them, so the lost-work check must fire  */
+#define SSPP_OPT_SPLIT_HANDOFFS 22 /* get (synchronous): slots handed to last workgroups so far */
+#define SSPP_OPT_SPLIT_LOST 23  /* get (synchronous): survivors lost so far (0 unless DROP)     */
 #define SSPP_OPT_TSP_REP 19     /* TaskSpacePlanner k_tsp form 3: sub-batches of candidates
                                    per workgroup (one prologue for all of them), 1..16, -1 by batch
                                    size; get: the last k_tsp launch's                            */
@@ -386,6 +398,8 @@ void sspp_steps_free(sspp_steps* ex);
 
 /* ---- multi-GPU helpers: reduce gathered per-rank results (lowest cost, lowest id) ---- */
 int sspp_best_reduce(const sspp_best* parts, int n, sspp_best* out);          /* host */
+/* SSPP_OK, or SSPP_E_INCOMPLETE when any of the n records reports lost work (reserved != 0) */
+int sspp_best_check(const sspp_best* recs, int n);                            /* host */
 int sspp_best_reduce_device(const sspp_best* d_parts, int n, sspp_best* d_out,
                             void* stream);                                    /* device, async */
 /* G steps gathered from R ranks: d_parts [R][G] -> d_out [G] (device, async)              */

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("SSPP_LIB_PATH") or PRODUCT_LIB_PATH
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "sspp_hip.h")
 
 SSPP_OK = 0
+SSPP_E_INCOMPLETE = -7  # a result record reports lost work (sspp_best::reserved != 0)
 MODE_QPOS = 0
 MODE_BODY = 1
 
@@ -123,6 +124,7 @@ SIGNATURES = {
                                 C.POINTER(C.c_size_t)]),
     "sspp_job_free": (None, [_vp]),
     "sspp_best_reduce": (C.c_int, [C.POINTER(Best), _i, C.POINTER(Best)]),
+    "sspp_best_check": (C.c_int, [C.POINTER(Best), _i]),
     "sspp_best_reduce_device": (C.c_int, [_vp, _i, _vp, _vp]),
     "sspp_best_reduce_steps": (C.c_int, [_vp, _i, _i, _vp, _vp]),
     "sspp_steps_enqueue_sspp": (C.c_int, [C.POINTER(_vp), _i, C.POINTER(_vp), _i64, _i, _i,
@@ -169,6 +171,7 @@ OPT_SHAPE_NT, OPT_SHAPE_G1, OPT_ORDER, OPT_TSP_FORM, OPT_TSP_GENERIC = 1, 2, 3, 
 OPT_SAMPLER, OPT_LAST_NT, OPT_LAST_G1, OPT_WP_ORDER, OPT_PREPASS_US, OPT_NPAIRS = 6, 7, 8, 9, 10, 11
 OPT_CYLBOX, OPT_F32, OPT_LAST_F32, OPT_CREATE_US, OPT_PREPASS_STATE = 12, 13, 14, 15, 16
 OPT_SPLIT, OPT_LAST_SPLIT, OPT_TSP_REP = 17, 18, 19
+OPT_SPLIT_LINGER_US, OPT_SPLIT_DROP, OPT_SPLIT_HANDOFFS, OPT_SPLIT_LOST = 20, 21, 22, 23
 OPT_CES_FUSED = 101
 
 

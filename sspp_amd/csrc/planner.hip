@@ -292,6 +292,7 @@ extern "C" int sspp_plan_sspp(const sspp_scene* scene, int dof, const double* st
     std::memcpy(arc_out, p->h_sarc.p, sizeof(double) * B);
     std::memcpy(feasible_out, p->h_sfeas.p, (size_t)B);
     *best_out = *p->h_sbest.p;
+    if ((rc = sspp_best_check(best_out, 1))) return rc;
     if (ctrl_out) std::memcpy(ctrl_out, p->h_ctrl.p, sizeof(double) * B * nd);
     return SSPP_OK;
 }
@@ -339,6 +340,9 @@ extern "C" int sspp_planner_score(sspp_planner* p, const double* knots, int degr
         return rc;
     if (arc_out) std::memcpy(arc_out, p->h_sarc.p, sizeof(double) * B);
     if (feasible_out) std::memcpy(feasible_out, p->h_sfeas.p, (size_t)B);
-    if (best_out) *best_out = *p->h_sbest.p;
+    if (best_out) {
+        *best_out = *p->h_sbest.p;
+        if ((rc = sspp_best_check(best_out, 1))) return rc;
+    }
     return SSPP_OK;
 }

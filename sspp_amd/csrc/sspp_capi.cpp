@@ -115,8 +115,25 @@ int sspp_spline_eval(const double* knots, int n_knots, int degree, const double*
     return SSPP_OK;
 }
 
+int sspp_best_check(const sspp_best* recs, int n) {
+    if (!recs || n < 0) return sspp::set_error(SSPP_E_INVAL, "null argument");
+    int64_t lost = 0, first = -1;
+    for (int i = 0; i < n; ++i)
+        if (recs[i].reserved != 0) {
+            lost += recs[i].reserved;
+            if (first < 0) first = i;
+        }
+    if (lost)
+        return sspp::set_error(SSPP_E_INCOMPLETE, "result record " + std::to_string(first) + " reports " +
+                                                      std::to_string(lost) +
+                                                      " lost candidates (split launch survivor queue): the "
+                                                      "step's outputs are incomplete");
+    return SSPP_OK;
+}
+
 int sspp_best_reduce(const sspp_best* parts, int n, sspp_best* out) {
     if (!parts || !out || n < 0) return sspp::set_error(SSPP_E_INVAL, "null argument");
+    if (const int rc = sspp_best_check(parts, n)) return rc;
     sspp_best b;
     b.cost = INFINITY; b.index = -1; b.count = 0; b.reserved = 0;
     for (int i = 0; i < n; ++i) {

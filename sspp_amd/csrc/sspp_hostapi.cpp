@@ -69,7 +69,8 @@ int run_job_host(const sspp_scene* scene, const double* knots, int degree, const
         return rc;
     if (feasible_out && (rc = hipck(hipMemcpy(feasible_out, d_feas.p, (size_t)B, hipMemcpyDeviceToHost), "copy feasible")))
         return rc;
-    if (best_out && (rc = hipck(hipMemcpy(best_out, d_best.p, sizeof(sspp_best), hipMemcpyDeviceToHost), "copy best")))
+    if (best_out && ((rc = hipck(hipMemcpy(best_out, d_best.p, sizeof(sspp_best), hipMemcpyDeviceToHost), "copy best")) ||
+                     (rc = sspp_best_check(best_out, 1))))
         return rc;
     if (ctrl_out && !ctrl_in &&
         (rc = hipck(hipMemcpy(ctrl_out, d_ctrl.p, sizeof(double) * nd * B, hipMemcpyDeviceToHost), "copy ctrl")))

@@ -903,16 +903,24 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
 // shard b % 64).  A workgroup pops with a ticket (one fetch-add on the shard's taken counter: a
 // compare-and-swap pop serialises a shard's consumers on the atomic's round trip, 93 vs 61 us) and
 // waits until its slot is reserved, or leaves once every producer of the shard has pushed and
-// the ticket is past the final count.  Waiting is deadlock-free because the launch is one
-// resident round (c2f_one_round: every producer runs to its push whatever the consumers do);
-// kLingerTicks only guards against a hang if that ever failed, counting the abandoned tickets.
+// the ticket is past the final count.  No ticket is ever dropped: a ticket whose wait exceeds the
+// launch's linger (SsppC2F::linger, 10 ms by default; SSPP_OPT_SPLIT_LINGER_US) is handed over
+// to the launch's last workgroup (SurvPtrs::orphan), which finishes it after every producer has
+// pushed.  So waiting cannot deadlock even when other kernels share the chip (a waiter blocks at
+// most one workgroup slot for at most the linger), and the ready words of every reserved slot are
+// re-armed by the last workgroup, whatever happened.  The last workgroup also counts the finished
+// survivors against the reserved slots: a shortfall (lost work; never observed, and impossible
+// unless the queue's storage is overrun) is written to every step record's `reserved` field, and
+// every host consumer of a record refuses it (SSPP_E_INCOMPLETE).
 // A reserved slot's producer is resident (it reserved the slot) and sets the ready word shortly.
+// The ready word is stored with release and read with acquire semantics at agent scope (the rows
+// before it are agent-scope stores and loads).
 // Each step's argmin: a feasible survivor takes part in an agent-scope atomicMin on its arc's bits
 // (non-negative doubles order like their bits) and the feasible count; one whose arc was not
 // above the minimum it saw is listed; the last workgroup to finish (sharded arrival counters, as
 // finish_batch) picks the lowest global id at each step's minimum from that list, writes the
 // records and re-arms the queue for the next launch on the job's stream.
-constexpr unsigned long long kLingerTicks = 1000000;  // 10 ms of the 100 MHz wall clock (a hang guard)
+constexpr unsigned long long kLingerTicksDefault = 1000000;  // 10 ms of the 100 MHz wall clock
 #ifndef SSPP_QUEUE_WAITERS  // tickets per shard that may wait for slots not reserved yet
 #define SSPP_QUEUE_WAITERS 4
 #endif
@@ -929,15 +937,20 @@ struct SurvShard {
 struct SurvQ {
     SurvShard shard[kSurvShards];
     unsigned nlist;                    // entries of the argmin list (SurvPtrs::res)
-    unsigned lost;                     // tickets abandoned by the hang guard (0 on a resident launch)
-    unsigned pad2[30];
+    unsigned lost;                     // survivors the launch could not finish (0; see above)
+    unsigned norphan;                  // tickets handed over to the last workgroup (SurvPtrs::orphan)
+    unsigned served;                   // survivors finished (checked against the reserved slots)
+    unsigned long long handoffs;       // tickets handed over, over the job's life (never re-armed)
+    unsigned long long lost_total;     // lost survivors over the job's life (never re-armed)
+    unsigned pad2[24];
     unsigned arrive_sh[8][32];         // arrival counters (8 shards, own cache lines)
     unsigned arrive_top[32];
     unsigned long long bestbits[kMaxSteps];  // per step: min arc of a feasible survivor (bits)
     unsigned count_feas[kMaxSteps];    // per step: feasible survivors
 };
 // a slot's ready word: bit 63 ready, bit 62 undecided cylinder-box pair, bits 32..39 the step of
-// the launch, bits 0..31 the candidate within the step (0: not ready; re-armed by its consumer)
+// the launch, bits 0..31 the candidate within the step (0: not ready; re-armed by the last
+// workgroup of the launch that used it)
 __host__ __device__ inline unsigned long long surv_word(int step, long long lc, bool defer) {
     return (1ull << 63) | ((unsigned long long)defer << 62) | ((unsigned long long)(unsigned)step << 32) |
            (unsigned long long)(unsigned)lc;
@@ -951,6 +964,7 @@ struct SurvPtrs {
     double* ctrl;      // [cap][nrd]  the survivors' own control-point rows
     float* ctrl32;     // [cap][nrd]  their FP32 copies
     SurvBest* res;     // [cap]       the argmin list (SurvQ::nlist entries)
+    unsigned* orphan;  // [cap]       handed-over tickets (global slots; one per workgroup at most)
     long long cap;
     int shard_cap;     // slots per shard: shard s owns [s * shard_cap, (s + 1) * shard_cap)
 };
@@ -984,6 +998,9 @@ struct SsppC2F {
     float feps, fplim;
     int split;     // the survivor queue (SurvQ) instead of phases 2-4 in the workgroup
     int nsteps;    // steps in this launch
+    int drop_orphans;            // tests only (SSPP_OPT_SPLIT_DROP): the last workgroup drops the
+                                 // handed-over tickets, which the lost-work check must report
+    unsigned long long linger;   // wall-clock ticks a ticket waits before it is handed over
 };
 
 #ifdef SSPP_C2F_STATS
@@ -1347,6 +1364,19 @@ __device__ SSPP_CB_INLINE bool c2f_cb_exact(const double* sm, int mine, int fix,
     return false;
 }
 
+// A queued survivor's own rows (slot t) into LDS at o_own, doubles and their FP32 copies
+template <int NT>
+__device__ __forceinline__ void surv_load_rows(const SurvPtrs& q, unsigned t, int nrd, double* smem, float* s_f32,
+                                               int o_own) {
+    for (int e = threadIdx.x; e < nrd; e += NT) {
+        const long long o = (long long)t * nrd + e;
+        smem[o_own + e] = __longlong_as_double(
+            (long long)__hip_atomic_load((unsigned long long*)q.ctrl + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        s_f32[o_own + e] =
+            __uint_as_float(__hip_atomic_load((unsigned*)q.ctrl32 + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+}
+
 // One queued survivor, finished by the whole workgroup (the split launch's consumers, see SurvQ):
 // phase 2 over waypoints j0 .. npts-1 of the job's order in passes of NT (a colliding survivor
 // usually stops after its first pass; 124 remaining waypoints are one pass of the 128-thread
@@ -1681,7 +1711,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         if (tid < nvalid) {
             const int slot = s_surv[tid];
             if (slot >= 0) {
-                __hip_atomic_store(q.rec + slot, surv_word(step, cand0 + tid, s_defer[tid] != 0), __ATOMIC_RELAXED,
+                __hip_atomic_store(q.rec + slot, surv_word(step, cand0 + tid, s_defer[tid] != 0), __ATOMIC_RELEASE,
                                    __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 arc[tid + cand0] = INFINITY;
@@ -1719,8 +1749,13 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                                 t = ~0u;
                                 break;
                             }
-                            if (wall_clock64() - w0 > kLingerTicks) {  // never on a resident launch
-                                __hip_atomic_fetch_add(&q.hdr->lost, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (wall_clock64() - w0 >= a.linger) {
+                                // handed over: the last workgroup finishes this slot (if it is
+                                // ever reserved) once every producer has pushed
+                                const unsigned k = __hip_atomic_fetch_add(&q.hdr->norphan, 1u, __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT);
+                                __hip_atomic_store(q.orphan + k, t + shs * (unsigned)q.shard_cap, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
                                 t = ~0u;
                                 break;
                             }
@@ -1732,7 +1767,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                         t += shs * (unsigned)q.shard_cap;
                         while ((w = __hip_atomic_load(q.rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0ull)
                             __builtin_amdgcn_s_sleep(1);
-                        __hip_atomic_store(q.rec + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the producer's release
                     }
                     s_ctl[0] = 1;
                     s_ctl[1] = (int)t;
@@ -1743,16 +1778,11 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                 const unsigned t = (unsigned)s_ctl[1];
                 if (t == ~0u) break;
                 const unsigned long long w = ((unsigned long long)(unsigned)s_ctl[2] << 32) | (unsigned)s_ctl[3];
-                for (int e = tid; e < nrd; e += NT) {
-                    const long long o = (long long)t * nrd + e;
-                    smem[o_own + e] = __longlong_as_double((long long)__hip_atomic_load(
-                        (unsigned long long*)q.ctrl + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    s_f32[o_own + e] = __uint_as_float(
-                        __hip_atomic_load((unsigned*)q.ctrl32 + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                }
+                surv_load_rows<NT>(q, t, nrd, smem, s_f32, o_own);
                 __syncthreads();
                 surv_finish<D, NM, P, ONEGEOM, NT>(a, TT, otab, otab32, ospan, atab, aspan, smem, s_f32, o_fix, o_own,
                                                    s_ctl, s_vsum, w, t, arc_base, feas_base, best_base != nullptr, q);
+                if (tid == 0) __hip_atomic_fetch_add(&q.hdr->served, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
 #ifdef SSPP_WG_TIMING
@@ -1781,9 +1811,69 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         }
         __syncthreads();
         if (!s_last[0]) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #ifdef SSPP_WG_TIMING
         const unsigned long long t_ep = wall_clock64();
 #endif
+        // every producer has pushed and every other workgroup has left: finish the handed-over
+        // tickets (the initial spline is still in LDS), then count the finished survivors against
+        // the reserved slots and re-arm every reserved slot's ready word
+        {
+            const unsigned no = __hip_atomic_load(&q.hdr->norphan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int* s_ctl = s_surv;
+            for (unsigned k = 0; k < no; ++k) {  // workgroup-uniform
+                if (tid == 0) {
+                    const unsigned slot = __hip_atomic_load(q.orphan + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned sh_o = slot / (unsigned)q.shard_cap, lt = slot - sh_o * (unsigned)q.shard_cap;
+                    unsigned long long w = 0ull;
+                    if (!a.drop_orphans &&
+                        lt < __hip_atomic_load(&q.hdr->shard[sh_o].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        // reserved, and its producer has pushed (it arrived): the word is set
+                        w = __hip_atomic_load(q.rec + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    }
+                    s_ctl[0] = 1;
+                    s_ctl[1] = (int)slot;
+                    s_ctl[2] = (int)(unsigned)(w >> 32);
+                    s_ctl[3] = (int)(unsigned)w;
+                }
+                __syncthreads();
+                const unsigned long long w = ((unsigned long long)(unsigned)s_ctl[2] << 32) | (unsigned)s_ctl[3];
+                if (w == 0ull) {  // never reserved (the ticket was past the final count), or dropped (tests)
+                    __syncthreads();
+                    continue;
+                }
+                const unsigned t = (unsigned)s_ctl[1];
+                surv_load_rows<NT>(q, t, nrd, smem, s_f32, o_own);
+                __syncthreads();
+                surv_finish<D, NM, P, ONEGEOM, NT>(a, TT, otab, otab32, ospan, atab, aspan, smem, s_f32, o_fix, o_own,
+                                                   s_ctl, s_vsum, w, t, arc_base, feas_base, best_base != nullptr, q);
+                if (tid == 0) __hip_atomic_fetch_add(&q.hdr->served, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the outputs, list entries and counts
+            __syncthreads();
+            // reserved slots: re-arm their ready words, count them against the finished survivors
+            unsigned nres = 0;
+            for (int s = 0; s < kSurvShards; ++s) {
+                const unsigned c = __hip_atomic_load(&q.hdr->shard[s].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                nres += c;
+                for (unsigned e = tid; e < c; e += NT)
+                    __hip_atomic_store(q.rec + (unsigned)s * (unsigned)q.shard_cap + e, 0ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (tid == 0) {
+                const unsigned served = __hip_atomic_load(&q.hdr->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (served < nres) {
+                    __hip_atomic_fetch_add(&q.hdr->lost, nres - served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&q.hdr->lost_total, (unsigned long long)(nres - served), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (no) __hip_atomic_fetch_add(&q.hdr->handoffs, (unsigned long long)no, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         // LDS is free: the per-step minimum bits, ids and feasible counts
         unsigned long long* s_bits = (unsigned long long*)smem;
         unsigned long long* s_id = s_bits + kMaxSteps;
@@ -1836,6 +1926,8 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             __hip_atomic_store(&q.hdr->arrive_top[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->nlist, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->lost, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q.hdr->norphan, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q.hdr->served, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef SSPP_WG_TIMING
             g_p2_t[8 * 4095] = t_ep;
             g_p2_t[8 * 4095 + 1] = wall_clock64();
@@ -2853,6 +2945,9 @@ struct sspp_job {
     double* d_sq_ctrl = nullptr;
     float* d_sq_ctrl32 = nullptr;
     SurvBest* d_sq_res = nullptr;
+    unsigned* d_sq_orphan = nullptr;
+    int opt_linger_us = 10000;          // SSPP_OPT_SPLIT_LINGER_US (10 ms)
+    int opt_split_drop = 0;             // SSPP_OPT_SPLIT_DROP (tests)
     long long sq_cap = 0;               // survivors the buffers hold (x sq_nrd doubles each)
     int sq_nrd = 0;
 };
@@ -2928,14 +3023,15 @@ inline KScene kscene_job(const sspp_job* j, bool sampled) {
 // need every producer resident); the occupancy query is cached per (kernel, LDS)
 inline bool c2f_one_round(const sspp_job* j, const void* fn, int nt, int lds, int nblk) {
     static thread_local const void* c_fn = nullptr;
-    static thread_local int c_lds = -1, c_wgs = 0;
-    if (fn != c_fn || lds != c_lds) {
-        int per_cu = 0, dev = 0, ncu = 0;
+    static thread_local int c_lds = -1, c_wgs = 0, c_dev = -1;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (fn != c_fn || lds != c_lds || dev != c_dev) {
+        int per_cu = 0, ncu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, (size_t)lds) != hipSuccess ||
-            hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             per_cu = ncu = 0;
-        c_fn = fn; c_lds = lds; c_wgs = per_cu * ncu;
+        c_fn = fn; c_lds = lds; c_dev = dev; c_wgs = per_cu * ncu;
     }
     (void)j;
     return nblk <= c_wgs;

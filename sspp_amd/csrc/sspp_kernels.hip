@@ -33,12 +33,13 @@ constexpr int kArgminThreads = 1024;
 __global__ __launch_bounds__(kArgminThreads) void k_argmin(const BlockBest* __restrict__ part,
                                                            int nparts, sspp_best* out) {
     __shared__ double sc[kArgminThreads / 64];
-    __shared__ long long si[kArgminThreads / 64], sn[kArgminThreads / 64];
+    __shared__ long long si[kArgminThreads / 64], sn[kArgminThreads / 64], sl[kArgminThreads / 64];
     double bc = INFINITY;
-    long long bi = -1, cnt = 0;
+    long long bi = -1, cnt = 0, lost = 0;  // lost: the records' `reserved` (lost survivors), summed
     for (int i = threadIdx.x; i < nparts; i += kArgminThreads) {
         const BlockBest b = part[i];
         cnt += b.count;
+        lost += b.pad;
         if (better(b.cost, b.idx, bc, bi)) { bc = b.cost; bi = b.idx; }
     }
 #pragma unroll
@@ -46,22 +47,24 @@ __global__ __launch_bounds__(kArgminThreads) void k_argmin(const BlockBest* __re
         const double oc = __shfl_xor(bc, off, 64);
         const long long oi = __shfl_xor(bi, off, 64);
         cnt += __shfl_xor(cnt, off, 64);
+        lost += __shfl_xor(lost, off, 64);
         if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
     }
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sc[w] = bc; si[w] = bi; sn[w] = cnt; }
+    if ((threadIdx.x & 63) == 0) { sc[w] = bc; si[w] = bi; sn[w] = cnt; sl[w] = lost; }
     __syncthreads();
     if (threadIdx.x == 0) {
         double c = sc[0];
-        long long i = si[0], n = sn[0];
+        long long i = si[0], n = sn[0], l = sl[0];
         for (int k = 1; k < kArgminThreads / 64; ++k) {
             n += sn[k];
+            l += sl[k];
             if (better(sc[k], si[k], c, i)) { c = sc[k]; i = si[k]; }
         }
         out->cost = i < 0 ? INFINITY : c;
         out->index = i;
         out->count = n;
-        out->reserved = 0;
+        out->reserved = l;
     }
 }
 
@@ -789,8 +792,11 @@ static double f32_eps(const sspp_scene* sc, const std::vector<DPair>& t) {
     double S = 1.0;
     for (const DPair& pr : t) {
         const DGeom& G = sc->geoms[pr.gm];
-        const double ext = G.rbound + pr.orbound + pr.margin;
-        double far = 0.0;
+        // the moving geom's offset from its mover's root scales the FP32 pose error like an extent
+        double gofs = 0.0, far = 0.0;
+        for (int k = 0; k < 3; ++k) gofs += G.pos[k] * G.pos[k];
+        gofs = std::sqrt(gofs);
+        const double ext = G.rbound + pr.orbound + pr.margin + gofs;
         for (int k = 0; k < 3; ++k) far = std::max(far, std::fabs(pr.opos[k]));
         if (!(ext <= 8.0) || !(far <= 2.0 * kF32PosLimit) || G.rbound <= 0.0) return 0.0;
         S = std::max(S, ext);
@@ -1005,9 +1011,11 @@ static int survq_reserve(sspp_job* j, int64_t cands, int nrd) {
     }
     if (cands <= j->sq_cap && nrd == j->sq_nrd) return SSPP_OK;
     HIPCHK(hipDeviceSynchronize());  // earlier launches may still use the old buffers
-    for (void* p : {(void*)j->d_sq_rec, (void*)j->d_sq_ctrl, (void*)j->d_sq_ctrl32, (void*)j->d_sq_res})
+    for (void* p : {(void*)j->d_sq_rec, (void*)j->d_sq_ctrl, (void*)j->d_sq_ctrl32, (void*)j->d_sq_res,
+                    (void*)j->d_sq_orphan})
         if (p) (void)hipFree(p);
     j->d_sq_rec = nullptr; j->d_sq_ctrl = nullptr; j->d_sq_ctrl32 = nullptr; j->d_sq_res = nullptr;
+    j->d_sq_orphan = nullptr;
     j->sq_cap = 0;
     const size_t n = (size_t)cands, nr = (size_t)std::max(1, nrd);
     HIPCHK(hipMalloc((void**)&j->d_sq_rec, sizeof(unsigned long long) * n));
@@ -1015,6 +1023,8 @@ static int survq_reserve(sspp_job* j, int64_t cands, int nrd) {
     HIPCHK(hipMalloc((void**)&j->d_sq_ctrl, sizeof(double) * n * nr));
     HIPCHK(hipMalloc((void**)&j->d_sq_ctrl32, sizeof(float) * n * nr));
     HIPCHK(hipMalloc((void**)&j->d_sq_res, sizeof(SurvBest) * n));
+    // handed-over tickets: one per workgroup at most, and a launch has at most `cands` workgroups
+    HIPCHK(hipMalloc((void**)&j->d_sq_orphan, sizeof(unsigned) * n));
     j->sq_cap = cands;
     j->sq_nrd = nrd;
     return SSPP_OK;
@@ -1092,7 +1102,12 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         const int shard_cap = ((nb_all + kSurvShards - 1) / kSurvShards) * cpb;
         int rc = survq_reserve(j, (int64_t)shard_cap * kSurvShards, nrd);
         if (rc) return rc;
-        q = SurvPtrs{j->d_sq_hdr, j->d_sq_rec, j->d_sq_ctrl, j->d_sq_ctrl32, j->d_sq_res, j->sq_cap, shard_cap};
+        q = SurvPtrs{j->d_sq_hdr, j->d_sq_rec, j->d_sq_ctrl, j->d_sq_ctrl32, j->d_sq_res, j->d_sq_orphan, j->sq_cap,
+                     shard_cap};
+        c.linger = (unsigned long long)j->opt_linger_us * 100ull;  // the 100 MHz wall clock
+        c.drop_orphans = j->opt_split_drop;
+        // the last workgroup's per-step minimum bits, ids and counts reuse the LDS from offset 0
+        c.lds = std::max(c.lds, (int)(20 * kMaxSteps));
     }
     SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best, q, &split_used};
     const int nb = nblk * steps;
@@ -1214,6 +1229,15 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
             if (j->kind != 0 || value < 0 || value > 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SPLIT: 0 or 1");
             j->opt_split = (int)value;
             return SSPP_OK;
+        case SSPP_OPT_SPLIT_LINGER_US:
+            if (j->kind != 0 || value < 0 || value > 1000000)
+                return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SPLIT_LINGER_US: 0..1000000");
+            j->opt_linger_us = (int)value;
+            return SSPP_OK;
+        case SSPP_OPT_SPLIT_DROP:
+            if (j->kind != 0 || value < 0 || value > 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SPLIT_DROP: 0 or 1");
+            j->opt_split_drop = (int)value;
+            return SSPP_OK;
         case SSPP_OPT_TSP_REP:
             if (j->kind != 1 || value < -1 || value == 0 || value > 16)
                 return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_REP: -1 or 1..16");
@@ -1243,6 +1267,18 @@ extern "C" int sspp_job_get_option(const sspp_job* j, int key, int64_t* value) {
         case SSPP_OPT_CREATE_US: *value = (int64_t)(j->create_ms * 1e3); return SSPP_OK;
         case SSPP_OPT_SPLIT: *value = j->opt_split; return SSPP_OK;
         case SSPP_OPT_LAST_SPLIT: *value = j->last_split; return SSPP_OK;
+        case SSPP_OPT_SPLIT_LINGER_US: *value = j->opt_linger_us; return SSPP_OK;
+        case SSPP_OPT_SPLIT_DROP: *value = j->opt_split_drop; return SSPP_OK;
+        case SSPP_OPT_SPLIT_HANDOFFS:
+        case SSPP_OPT_SPLIT_LOST: {  // synchronous read of the queue header (tests, diagnostics)
+            *value = 0;
+            if (!j->d_sq_hdr) return SSPP_OK;
+            SurvQ h;
+            HIPCHK(hipDeviceSynchronize());
+            HIPCHK(hipMemcpy(&h, j->d_sq_hdr, sizeof(SurvQ), hipMemcpyDeviceToHost));
+            *value = (int64_t)(key == SSPP_OPT_SPLIT_HANDOFFS ? h.handoffs : h.lost_total);
+            return SSPP_OK;
+        }
         case SSPP_OPT_TSP_REP: *value = j->kind == 1 ? j->last_rep : 0; return SSPP_OK;
         case SSPP_OPT_PREPASS_STATE: *value = j->prepass_state.load(std::memory_order_acquire); return SSPP_OK;
     }
@@ -1521,7 +1557,7 @@ extern "C" void sspp_job_free(sspp_job* j) {
     prepass_drop(j);
     if (j->pre_stream) (void)hipStreamSynchronize(j->pre_stream);
     for (void* q : {(void*)j->d_sq_hdr, (void*)j->d_sq_rec, (void*)j->d_sq_ctrl, (void*)j->d_sq_ctrl32,
-                    (void*)j->d_sq_res})
+                    (void*)j->d_sq_res, (void*)j->d_sq_orphan})
         if (q) (void)hipFree(q);
     for (void* q : j->retired) if (q) (void)hipFree(q);
     for (void* q : {(void*)j->d_hits, (void*)j->d_census_pairs}) if (q) (void)hipFree(q);
@@ -1572,10 +1608,11 @@ __global__ __launch_bounds__(64) void k_argmin_steps(const BlockBest* __restrict
     // block g: lexicographic (cost, id) reduction of parts[r * G + g], r < R (one wave)
     const int g = blockIdx.x;
     double bc = INFINITY;
-    long long bi = -1, cnt = 0;
+    long long bi = -1, cnt = 0, lost = 0;  // lost: the records' `reserved`, summed (a shortfall stays visible)
     for (int r = threadIdx.x; r < R; r += 64) {
         const BlockBest b = parts[(long long)r * G + g];
         cnt += b.count;
+        lost += b.pad;
         if (better(b.cost, b.idx, bc, bi)) { bc = b.cost; bi = b.idx; }
     }
 #pragma unroll
@@ -1583,13 +1620,14 @@ __global__ __launch_bounds__(64) void k_argmin_steps(const BlockBest* __restrict
         const double oc = __shfl_xor(bc, off, 64);
         const long long oi = __shfl_xor(bi, off, 64);
         cnt += __shfl_xor(cnt, off, 64);
+        lost += __shfl_xor(lost, off, 64);
         if (better(oc, oi, bc, bi)) { bc = oc; bi = oi; }
     }
     if (threadIdx.x == 0) {
         out[g].cost = bi < 0 ? INFINITY : bc;
         out[g].index = bi;
         out[g].count = cnt;
-        out[g].reserved = 0;
+        out[g].reserved = lost;
     }
 }
 }  // namespace

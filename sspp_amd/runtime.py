@@ -52,19 +52,32 @@ def best_tensor(device="cuda"):
     return _torch().zeros(4, dtype=_torch().int64, device=device)
 
 
-def decode_best(t):
-    """(cost, index, count) from a best buffer (torch tensor or numpy int64[4])."""
+def check_records(t):
+    """Refuse result records that report lost work: any record (int64 [..., 4] tensor or array)
+    whose `reserved` field is non-zero raises SsppError through sspp_best_check
+    (SSPP_E_INCOMPLETE).  Returns the records as a numpy int64 [n, 4] array."""
     a = t.detach().cpu().numpy() if hasattr(t, "detach") else np.asarray(t)
-    a = np.ascontiguousarray(a.astype(np.int64))
+    a = np.ascontiguousarray(a.astype(np.int64).reshape(-1, 4))
+    if a.shape[0] and np.any(a[:, 3] != 0):
+        check(lib().sspp_best_check(a.ctypes.data_as(C.POINTER(Best)), int(a.shape[0])), "result record")
+    return a
+
+
+def decode_best(t):
+    """(cost, index, count) from a best buffer (torch tensor or numpy int64[4]); a record that
+    reports lost work raises SsppError (check_records)."""
+    a = check_records(t)[0]
     cost = a[:1].view(np.float64)[0]
     return float(cost), int(a[1]), int(a[2])
 
 
 def reduce_best(parts):
-    """Global argmin over gathered per-rank records: lowest cost, lowest global id on ties."""
+    """Global argmin over gathered per-rank records (cost, index, count[, reserved]): lowest
+    cost, lowest id on ties; a record with reserved != 0 raises SsppError."""
     arr = (Best * len(parts))()
-    for i, (c, idx, cnt) in enumerate(parts):
-        arr[i].cost, arr[i].index, arr[i].count = c, idx, cnt
+    for i, p in enumerate(parts):
+        arr[i].cost, arr[i].index, arr[i].count = p[0], p[1], p[2]
+        arr[i].reserved = p[3] if len(p) > 3 else 0
     out = Best()
     check(lib().sspp_best_reduce(arr, len(parts), C.byref(out)), "sspp_best_reduce")
     return out.cost, out.index, out.count
@@ -331,6 +344,7 @@ class SsppSteps:
     def __init__(self, jobs, streams, B, arc_bufs, feas_bufs, steps_per_launch=1):
         nb = len(jobs)
         self._keep = (jobs, streams, arc_bufs, feas_bufs)
+        self.arc_bufs, self.feas_bufs = arc_bufs, feas_bufs  # each branch's last launch's outputs
         self._J = (C.c_void_p * nb)(*[j._h for j in jobs])
         self._S = (C.c_void_p * nb)(*[_stream(s).value for s in streams])
         self._A = (C.c_void_p * nb)(*[_ptr(a).value for a in arc_bufs])
@@ -542,6 +556,6 @@ def device_count():
 
 
 __all__ = ["Model", "Scene", "SsppJob", "TspJob", "CesPlanner", "SsppSteps", "reduce_best_steps", "all_gather_records",
-           "torch_stream", "interpolate", "spline_eval", "best_tensor",
+           "torch_stream", "interpolate", "spline_eval", "best_tensor", "check_records",
            "decode_best", "reduce_best", "reduce_best_device", "device_count", "DEFAULT_SEED",
            "SAMPLER_FP64", "SAMPLER_FP32", "math"]

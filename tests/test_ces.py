@@ -464,3 +464,57 @@ def test_ces_plan_group_matches_single(cuda, samples, iters):
                 p.plan(st, en, iterate=True, iterations=1)
             S.CesPlanner.plan_group(group, starts, ends, iterate=True, iterations=1)
     assert sum(p.read()["n_success"] for p in solo) > 0
+
+
+@pytest.mark.gpu
+def test_ces_plan_group_matches_oracle(cuda):
+    """k_tsp_group (the multi-goal bench's evaluation: every goal's slots in one grid) directly
+    against the oracle, not through the per-goal planners: BASELINE configs[4] at 4096 samples x
+    128 checks, all 8 goals, two group iterations (reset, then iterate with the forwarded best).
+    Per goal and iteration, on the device's own via sets: the Philox samples, status, costs
+    (<= 1e-12 relative), then elites / best slot / mean / sigma / last best bit-identical to
+    O.ces_update (tsp_planner.h:121-142)."""
+    import bench
+    import sspp_amd as S
+    model = S.Model(ROBOCRANE)
+    body = model.body_id("gripper_collision_with_block/")
+    scene = S.Scene(model, 1, body)
+    osc = O.Scene(mjcf_ref.load(ROBOCRANE), 1, body)
+    lo, hi = bench.MG_LO, bench.MG_HI
+    samples, checks = 4096, 128
+    goals = bench.MULTIGOAL
+    starts = np.array([g[0] for g in goals])
+    ends = np.array([g[1] for g in goals])
+    pls = [S.CesPlanner(scene, sample_count=samples, check_points=checks, init_points=3, limits_min=lo,
+                        limits_max=hi, seed=S.DEFAULT_SEED + g) for g in range(len(goals))]
+    prev = [None] * len(goals)
+    for t in range(2):
+        S.CesPlanner.plan_group(pls, starts, ends, iterate=t > 0, iterations=1)
+        for g, pl in enumerate(pls):
+            st, en = starts[g], ends[g]
+            if prev[g] is None:
+                m_in, s_in = O.ces_reset(st, en, 3, lo=lo, hi=hi)
+                lb_in, hb_in = np.zeros((1, 4)), False
+            else:
+                p = prev[g]
+                m_in, s_in, lb_in, hb_in = p["mean"], p["sigma"], p["last_best"], p["has_best"]
+            r = pl.read()
+            nfx = 2 if (t > 0 and hb_in) else 1
+            assert r["n_fixed"] == nfx and r["n_candidates"] == nfx + samples
+            smp = O.sample_tsp(m_in, s_in, lo, hi, 0.0, S.DEFAULT_SEED + g, t * samples, samples)
+            assert np.abs(r["vias"][nfx:] - smp).max() <= 1e-12
+            L, Cnf, Cwf, stt, cost = O.tsp_score(osc, st, en, r["vias"], checks)
+            np.testing.assert_array_equal(r["status"], stt)
+            fin = np.isfinite(cost)
+            np.testing.assert_array_equal(np.isfinite(r["cost"]), fin)
+            for a, b in ((r["cost"][fin], cost[fin]), (r["L"], L), (r["C_nf"], Cnf), (r["C_wf"], Cwf)):
+                assert (np.abs(a - b) <= 1e-12 * np.maximum(1.0, np.abs(b))).all()
+            m, s, lb, hb, ns, el, bs = O.ces_update(r["cost"], r["status"], r["vias"], m_in, s_in, lb_in, hb_in,
+                                                    lo=lo, hi=hi)
+            assert r["n_success"] == ns and r["best_slot"] == bs and r["has_best"] == hb
+            np.testing.assert_array_equal(r["elites"], el)
+            np.testing.assert_array_equal(r["mean"], m)
+            np.testing.assert_array_equal(r["sigma"], s)
+            np.testing.assert_array_equal(r["last_best"], lb)
+            prev[g] = r
+    assert sum(p["n_success"] > 0 for p in prev) >= 6

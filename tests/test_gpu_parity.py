@@ -473,6 +473,9 @@ def test_multistep_launch_matches_oracle(robocrane, sigma, spl):
         ex.enqueue(G, first + rep * G * stride, stride, best)
         torch.cuda.synchronize()
         assert job.config()["shape"] == "128x4"
+        # the split instance (survivor queue) for single-geom sampled tables; sigma 0.3 reaches a
+        # second geom, which is never split
+        assert job.get_option(S._lib.OPT_LAST_SPLIT) == (1 if sigma <= 0.12 else 0)
         arc, fe, got = arcs[0].cpu().numpy(), feas[0].cpu().numpy(), best.cpu()
         for i in (0, 7, G - 1):
             f0 = first + (rep * G + i) * stride
@@ -766,3 +769,84 @@ def test_tsp_rep_is_invisible(cuda, rep):
         res[r] = {k: v.cpu().numpy() for k, v in q.items()}
     for k in res[1]:
         np.testing.assert_array_equal(res[rep][k], res[1][k], err_msg=k)
+
+
+def _split_run(job, spl, first, B=4096):
+    """One split launch of spl steps through the executor: (arc, feas, records) on the host."""
+    import sspp_amd as S
+    import torch
+    arcs = [torch.empty(spl * B, dtype=torch.float64, device="cuda")]
+    feas = [torch.empty(spl * B, dtype=torch.uint8, device="cuda")]
+    ex = S.SsppSteps([job], [torch.cuda.current_stream()], B, arcs, feas, steps_per_launch=spl)
+    best = torch.zeros((spl, 4), dtype=torch.int64, device="cuda")
+    ex.enqueue(spl, first, B, best)
+    torch.cuda.synchronize()
+    assert job.get_option(S._lib.OPT_LAST_SPLIT) == 1
+    return arcs[0].cpu().numpy(), feas[0].cpu().numpy(), best.cpu().numpy()
+
+
+def _split_vs_oracle(oscene, knots, ctrl0, sigma, spl, first, arc, fe, recs, steps, B=4096):
+    import sspp_amd as S
+    for i in steps:
+        f0 = first + i * B
+        ctrl = O.sample_sspp(ctrl0, 3, sigma, np.ones(7), 0x5EED, f0, B)
+        arc_o, feas_o = O.sspp_score(oscene, knots, 3, ctrl, 128)
+        np.testing.assert_array_equal(fe[i * B:(i + 1) * B], feas_o)
+        assert arc_err(arc[i * B:(i + 1) * B], arc_o) <= COST_TOL
+        k, _ = O.argmin(arc_o, feas_o)
+        d = S.decode_best(recs[i])
+        assert d[1] == (f0 + k if k >= 0 else -1) and d[2] == int(feas_o.sum()), (i, d, k)
+
+
+def test_split_handoff_is_invisible(robocrane):
+    """SSPP_OPT_SPLIT_LINGER_US = 0: every ticket that would wait for a slot not reserved yet is
+    handed to the launch's last workgroup at once (the path a waiter takes after its linger
+    expires).  Nothing is lost: the handed-over survivors are finished there, every output equals
+    the default-linger launch bit for bit and the oracle, and no record reports lost work."""
+    import sspp_amd as S
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    spl, first = 20, 31 * 4096
+    res = {}
+    for linger in (0, 10000):
+        job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=4096)
+        job.set_option(S._lib.OPT_SPLIT_LINGER_US, linger)
+        for rep in range(2):  # the second launch reuses the re-armed queue
+            res[linger, rep] = _split_run(job, spl, first + rep * spl * 4096)
+        res[linger, "handoffs"] = job.get_option(S._lib.OPT_SPLIT_HANDOFFS)
+        assert job.get_option(S._lib.OPT_SPLIT_LOST) == 0
+    assert res[0, "handoffs"] > 0  # the hand-over path ran
+    for rep in range(2):
+        for a, b in zip(res[0, rep], res[10000, rep]):
+            np.testing.assert_array_equal(a, b)
+        S.check_records(res[0, rep][2])
+    arc, fe, recs = res[0, 1]
+    _split_vs_oracle(oscene, knots, ctrl0, 0.08, spl, first + spl * 4096, arc, fe, recs, (0, 9, spl - 1))
+
+
+def test_split_lost_work_fails_loudly_and_does_not_poison(robocrane):
+    """SSPP_OPT_SPLIT_DROP (tests only) makes the last workgroup drop the handed-over survivors:
+    the launch's lost-work check must report them in every step record (`reserved`), the Python
+    layer must refuse those records (SsppError, SSPP_E_INCOMPLETE) and the job must count them.
+    The next normal launch on the same queue must equal the oracle bit for bit: the last
+    workgroup re-arms every reserved slot, so nothing stale reaches the next launch."""
+    import sspp_amd as S
+    _, scene, oscene = robocrane
+    knots, ctrl0 = linear_init(START7, END7, 10)
+    spl, first = 20, 53 * 4096
+    job = S.SsppJob(scene, knots, 3, ctrl0, 0.08, np.ones(7), 128, max_batch=4096)
+    job.set_option(S._lib.OPT_SPLIT_LINGER_US, 0)
+    job.set_option(S._lib.OPT_SPLIT_DROP, 1)
+    _, _, recs = _split_run(job, spl, first)
+    lost = job.get_option(S._lib.OPT_SPLIT_LOST)
+    assert lost > 0 and (recs[:, 3] == lost).all()
+    with pytest.raises(S.SsppError, match="lost candidates"):
+        S.decode_best(recs[0])
+    with pytest.raises(S.SsppError, match="lost candidates"):
+        S.check_records(recs)
+    job.set_option(S._lib.OPT_SPLIT_DROP, 0)
+    job.set_option(S._lib.OPT_SPLIT_LINGER_US, 10000)
+    first2 = first + spl * 4096
+    arc, fe, recs = _split_run(job, spl, first2)
+    assert (recs[:, 3] == 0).all() and job.get_option(S._lib.OPT_SPLIT_LOST) == lost
+    _split_vs_oracle(oscene, knots, ctrl0, 0.08, spl, first2, arc, fe, recs, range(spl))

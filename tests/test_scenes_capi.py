@@ -164,3 +164,31 @@ def test_host_best_reduce():
     inf = float("inf")
     assert S.reduce_best([(inf, -1, 0), (2.0, 7, 3), (2.0, 5, 1), (3.0, 1, 9)]) == (2.0, 5, 13)
     assert S.reduce_best([(inf, -1, 0), (inf, -1, 0)]) == (inf, -1, 0)
+
+
+def test_records_reporting_lost_work_are_refused():
+    """A step record whose `reserved` field is non-zero (a split launch's lost-work check found
+    survivors it could not finish) is refused by every host consumer: sspp_best_check /
+    sspp_best_reduce (SSPP_E_INCOMPLETE) and the Python layer (decode_best, check_records,
+    reduce_best).  A clean record passes."""
+    ok = np.zeros(4, np.int64)
+    ok[:1] = np.array([1.5]).view(np.int64)
+    ok[1], ok[2] = 17, 3
+    assert S.decode_best(ok) == (1.5, 17, 3)
+    bad = ok.copy()
+    bad[3] = 2
+    with pytest.raises(S.SsppError, match="lost candidates"):
+        S.decode_best(bad)
+    with pytest.raises(S.SsppError, match="lost candidates"):
+        S.check_records(np.stack([ok, bad]))
+    S.check_records(np.stack([ok, ok]))
+    with pytest.raises(S.SsppError, match="lost candidates"):
+        S.reduce_best([(1.5, 17, 3, 0), (2.0, 4, 1, 1)])
+    arr = (_lib.Best * 2)()
+    arr[1].reserved = 5
+    assert _lib.lib().sspp_best_check(arr, 2) == _lib.SSPP_E_INCOMPLETE
+    out = _lib.Best()
+    assert _lib.lib().sspp_best_reduce(arr, 2, C.byref(out)) == _lib.SSPP_E_INCOMPLETE
+    assert "5 lost candidates" in _lib.last_error()
+    arr[1].reserved = 0
+    assert _lib.lib().sspp_best_check(arr, 2) == 0
