@@ -7,7 +7,7 @@ JOBS     ?= 8
 CXXSTD    = -std=c++17
 # -ffp-contract=off: every fma in the kernels is explicit (bitwise parity with oracle/)
 HIPFLAGS  = $(CXXSTD) -O3 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
-            -Wall -Wno-unused-function -Wno-unused-result
+            -Wall -Wno-unused-function -Wno-unused-result $(EXTRA)
 HOSTFLAGS = $(CXXSTD) -O2 -fPIC -ffp-contract=off -Wall -mfma
 
 SRC      = sspp_amd/csrc

@@ -921,6 +921,35 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
 // finish_batch) picks the lowest global id at each step's minimum from that list, writes the
 // records and re-arms the queue for the next launch on the job's stream.
 constexpr unsigned long long kLingerTicksDefault = 1000000;  // 10 ms of the 100 MHz wall clock
+#ifdef SSPP_DEBUG_PROGRESS  // progress beacons of the split launch, readable by the host while it runs
+#define SSPP_BEACON(B_PH, B_X, B_Y)                                                                                   \
+    do {                                                                                                        \
+        if (q.beacon && threadIdx.x == 0) {                                                                     \
+            __hip_atomic_store(q.beacon + 4 * blockIdx.x + 1, (unsigned)(B_X), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+            __hip_atomic_store(q.beacon + 4 * blockIdx.x + 2, (unsigned)(B_Y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+            __hip_atomic_store(q.beacon + 4 * blockIdx.x, (unsigned)(B_PH), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);    \
+        }                                                                                                       \
+    } while (0)
+// wave 1's progress (thread 64) in the workgroup's fourth word
+#define SSPP_BEACON1(B_PH)                                                                                      \
+    do {                                                                                                        \
+        if (q.beacon && threadIdx.x == 64)                                                                      \
+            __hip_atomic_store(q.beacon + 4 * blockIdx.x + 3, (unsigned)(B_PH), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+    } while (0)
+#else
+#define SSPP_BEACON(B_PH, B_X, B_Y) do { } while (0)
+#define SSPP_BEACON1(B_PH) do { } while (0)
+#endif
+#ifndef SSPP_QUEUE_FENCES  // 1: ready words release / acquire at agent scope; 0: relaxed (A/B)
+#define SSPP_QUEUE_FENCES 1
+#endif
+#if SSPP_QUEUE_FENCES
+#define SSPP_QUEUE_RELEASE_ORDER __ATOMIC_RELEASE
+#define SSPP_QUEUE_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#else
+#define SSPP_QUEUE_RELEASE_ORDER __ATOMIC_RELAXED
+#define SSPP_QUEUE_ACQUIRE() do { } while (0)
+#endif
 #ifndef SSPP_QUEUE_WAITERS  // tickets per shard that may wait for slots not reserved yet
 #define SSPP_QUEUE_WAITERS 4
 #endif
@@ -965,6 +994,8 @@ struct SurvPtrs {
     float* ctrl32;     // [cap][nrd]  their FP32 copies
     SurvBest* res;     // [cap]       the argmin list (SurvQ::nlist entries)
     unsigned* orphan;  // [cap]       handed-over tickets (global slots; one per workgroup at most)
+    unsigned* beacon;  // debugging builds (-DSSPP_DEBUG_PROGRESS): [grid][4] progress words in mapped
+                       // host memory (SSPP_OPT_DEBUG_BEACONS); null otherwise
     long long cap;
     int shard_cap;     // slots per shard: shard s owns [s * shard_cap, (s + 1) * shard_cap)
 };
@@ -1400,6 +1431,8 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
     const unsigned long long w_t0 = wall_clock64(), c0 = clock64();
     unsigned w_np = 0, w_nf = 0;
 #endif
+    SSPP_BEACON(20, slot, 0);
+    SSPP_BEACON1(20);
     for (int jb = 0; jb < R; jb += NT) {  // workgroup-uniform
         // a uniform exit once a pass has found a contact (every thread's read precedes the barrier)
         if (jb > 0 && !__syncthreads_or(__hip_atomic_load(s_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
@@ -1438,8 +1471,12 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
         ++w_np;
 #endif
     }
+    SSPP_BEACON(21, slot, 0);
+    SSPP_BEACON1(21);
     __syncthreads();
-    const bool feas = s_ctl[0] != 0;
+    const bool feas = __builtin_amdgcn_readfirstlane(s_ctl[0]) != 0;
+    SSPP_BEACON(22, slot, feas);
+    SSPP_BEACON1(22);
 #ifdef SSPP_WG_TIMING
     const unsigned long long c1 = clock64();
 #endif
@@ -1461,6 +1498,8 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
             acc = wave_sum(acc);
             if (lane == 0) s_vsum[vw] = acc;
         }
+        SSPP_BEACON(23, slot, 0);
+        SSPP_BEACON1(23);
         __syncthreads();
         total = s_vsum[0];
         for (int w = 1; w < nvw; ++w) total = total + s_vsum[w];
@@ -1491,6 +1530,8 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
 #endif
     }
     (void)slot;
+    SSPP_BEACON(24, slot, 0);
+    SSPP_BEACON1(24);
     __syncthreads();  // the next survivor may overwrite the rows and the flags
 }
 
@@ -1681,6 +1722,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     WG_PH(3);
     if constexpr (SPLIT) {
         static_assert(NM == 1 && ONEGEOM && !CBX, "split launches: single-geom movers without cylinder-box pairs");
+        SSPP_BEACON(3, 0, 0);
         // ---- producer: one queue reservation per workgroup (survivors in candidate order), the
         // survivors' rows written through to the coherent level, then each slot's ready word; the
         // other candidates' outputs are final here
@@ -1711,7 +1753,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         if (tid < nvalid) {
             const int slot = s_surv[tid];
             if (slot >= 0) {
-                __hip_atomic_store(q.rec + slot, surv_word(step, cand0 + tid, s_defer[tid] != 0), __ATOMIC_RELEASE,
+                __hip_atomic_store(q.rec + slot, surv_word(step, cand0 + tid, s_defer[tid] != 0), SSPP_QUEUE_RELEASE_ORDER,
                                    __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 arc[tid + cand0] = INFINITY;
@@ -1723,23 +1765,32 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         if (tid == 0)
             __hip_atomic_fetch_add(&q.hdr->shard[blockIdx.x % kSurvShards].pushed, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-        // ---- consumers: every workgroup pops survivors until the queue is empty
-        {
-            const unsigned nb_all = gridDim.x, shs = blockIdx.x % kSurvShards;
-            const unsigned nwg_s = (nb_all - shs + kSurvShards - 1) / kSurvShards;  // producers of the shard
-            SurvShard* const sh = q.hdr->shard + shs;
-            int* s_ctl = s_surv;  // [0] feasible, [1] slot, [2..3] the ready word
-            for (;;) {  // workgroup-uniform
-                if (tid == 0) {
+        SSPP_BEACON(4, 0, 0);
+        // ---- consumers: every workgroup pops survivors until the queue is empty; the launch's last
+        // workgroup to arrive then finishes the handed-over slots in the same loop (one copy of
+        // surv_finish in the kernel: a second inlined copy for the hand-over list raised the
+        // instance's SGPR spills 385 -> 539)
+        const unsigned nb_all = gridDim.x, shs = blockIdx.x % kSurvShards;
+        const unsigned nwg_s = (nb_all - shs + kSurvShards - 1) / kSurvShards;  // producers of the shard
+        SurvShard* const sh = q.hdr->shard + shs;
+        int* s_ctl = s_surv;      // [0] feasible, [1] slot, [2..3] the ready word
+        int* s_last = s_surv + cpb;
+        bool last = false;        // workgroup-uniform: the launch's last workgroup, on the hand-over list
+        unsigned ko = 0, no = 0;  // (thread 0) position in the hand-over list, its length
+        for (;;) {  // workgroup-uniform (the slot and word come from LDS through readfirstlane)
+            if (tid == 0) {
+                unsigned t = ~0u;
+                unsigned long long w = 0ull;
+                if (!last) {
                     // a ticket: the shard's next slot in reservation order, reserved now or later —
                     // unless SSPP_QUEUE_WAITERS tickets already wait for slots not reserved yet:
                     // then this workgroup leaves (those waiters, and every producer after its
                     // push, serve the slots still to come; a waiter leaves once the shard is done)
-                    unsigned t = ~0u;
                     const unsigned tk0 = __hip_atomic_load(&sh->taken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const unsigned ct0 = __hip_atomic_load(&sh->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if ((int)(tk0 - ct0) < SSPP_QUEUE_WAITERS) {
                         t = __hip_atomic_fetch_add(&sh->taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        SSPP_BEACON(5, t, ct0);
                         const unsigned long long w0 = wall_clock64();
                         for (;;) {
                             if (t < __hip_atomic_load(&sh->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
@@ -1762,97 +1813,106 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                             __builtin_amdgcn_s_sleep(SSPP_LINGER_SLEEP);
                         }
                     }
-                    unsigned long long w = 0ull;
                     if (t != ~0u) {  // the producer is resident (it reserved the slot): its word lands shortly
                         t += shs * (unsigned)q.shard_cap;
-                        while ((w = __hip_atomic_load(q.rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0ull)
+                        SSPP_BEACON(6, t, 0);
+                        const unsigned long long w1 = wall_clock64();
+                        while ((w = __hip_atomic_load(q.rec + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0ull) {
+                            if (wall_clock64() - w1 >= a.linger) break;  // bounded too: handed over
                             __builtin_amdgcn_s_sleep(1);
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // pairs with the producer's release
+                        }
+                        if (w == 0ull) {
+                            const unsigned k = __hip_atomic_fetch_add(&q.hdr->norphan, 1u, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(q.orphan + k, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            t = ~0u;
+                        } else {
+                            SSPP_QUEUE_ACQUIRE();  // pairs with the producer's release
+                        }
                     }
-                    s_ctl[0] = 1;
-                    s_ctl[1] = (int)t;
-                    s_ctl[2] = (int)(unsigned)(w >> 32);
-                    s_ctl[3] = (int)(unsigned)w;
+                } else {
+                    // the hand-over list: every producer has pushed (all workgroups arrived), so a
+                    // reserved slot's word is set; a slot past its shard's final count was never
+                    // reserved (SSPP_OPT_SPLIT_DROP, tests: every slot is dropped instead)
+                    while (ko < no && w == 0ull) {
+                        const unsigned slot = __hip_atomic_load(q.orphan + ko, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ++ko;
+                        const unsigned sh_o = slot / (unsigned)q.shard_cap, lt = slot - sh_o * (unsigned)q.shard_cap;
+                        if (!a.drop_orphans &&
+                            lt < __hip_atomic_load(&q.hdr->shard[sh_o].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                            w = __hip_atomic_load(q.rec + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (w != 0ull) {
+                                SSPP_QUEUE_ACQUIRE();
+                                t = slot;
+                            }
+                        }
+                    }
+                    SSPP_BEACON(11, ko, no);
+                }
+                s_ctl[0] = 1;
+                s_ctl[1] = (int)t;
+                s_ctl[2] = (int)(unsigned)(w >> 32);
+                s_ctl[3] = (int)(unsigned)w;
+            }
+            __syncthreads();
+            const unsigned t = (unsigned)__builtin_amdgcn_readfirstlane(s_ctl[1]);
+            if (t == ~0u) {
+                if (last) break;
+#ifdef SSPP_WG_TIMING
+                if (tid == 0 && blockIdx.x < (1 << 16)) {
+                    g_wg_t[4 * blockIdx.x] = wg_t0;
+                    g_wg_t[4 * blockIdx.x + 1] = wall_clock64();
+                    g_wg_t[4 * blockIdx.x + 2] = __smid();
+                    g_wg_t[4 * blockIdx.x + 3] = 0ull;
+                }
+#endif
+                SSPP_BEACON(8, 0, 0);
+                // ---- completion: sharded arrival; the last workgroup goes on with the hand-over list
+                const unsigned nblk = gridDim.x;
+                const int shd = blockIdx.x & 7, nsh = nblk < 8 ? (int)nblk : 8;
+                if (tid == 0) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    const unsigned shard_n = (nblk - shd + 7) >> 3;
+                    const unsigned prev = __hip_atomic_fetch_add(&q.hdr->arrive_sh[shd][0], 1u, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                    int lst = 0;
+                    if (prev == shard_n - 1) {
+                        const unsigned pt = __hip_atomic_fetch_add(&q.hdr->arrive_top[0], 1u, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                        lst = pt == (unsigned)nsh - 1;
+                    }
+                    s_last[0] = lst;
+                    if (lst) {
+                        SSPP_QUEUE_ACQUIRE();
+                        no = __hip_atomic_load(&q.hdr->norphan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                 }
                 __syncthreads();
-                const unsigned t = (unsigned)s_ctl[1];
-                if (t == ~0u) break;
-                const unsigned long long w = ((unsigned long long)(unsigned)s_ctl[2] << 32) | (unsigned)s_ctl[3];
-                surv_load_rows<NT>(q, t, nrd, smem, s_f32, o_own);
-                __syncthreads();
-                surv_finish<D, NM, P, ONEGEOM, NT>(a, TT, otab, otab32, ospan, atab, aspan, smem, s_f32, o_fix, o_own,
-                                                   s_ctl, s_vsum, w, t, arc_base, feas_base, best_base != nullptr, q);
-                if (tid == 0) __hip_atomic_fetch_add(&q.hdr->served, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int lst = __builtin_amdgcn_readfirstlane(s_last[0]);
+                SSPP_BEACON(9 + lst, no, 0);
+                if (!lst) return;
+                last = true;
+                continue;
             }
+            const unsigned long long w = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(s_ctl[2]) << 32) |
+                                         (unsigned)__builtin_amdgcn_readfirstlane(s_ctl[3]);
+            SSPP_BEACON(7, t, (unsigned)w);
+            SSPP_BEACON1(7);
+            surv_load_rows<NT>(q, t, nrd, smem, s_f32, o_own);
+            __syncthreads();
+            surv_finish<D, NM, P, ONEGEOM, NT>(a, TT, otab, otab32, ospan, atab, aspan, smem, s_f32, o_fix, o_own,
+                                               s_ctl, s_vsum, w, t, arc_base, feas_base, best_base != nullptr, q);
+            if (tid == 0) __hip_atomic_fetch_add(&q.hdr->served, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-#ifdef SSPP_WG_TIMING
-        if (tid == 0 && blockIdx.x < (1 << 16)) {
-            g_wg_t[4 * blockIdx.x] = wg_t0;
-            g_wg_t[4 * blockIdx.x + 1] = wall_clock64();
-            g_wg_t[4 * blockIdx.x + 2] = __smid();
-            g_wg_t[4 * blockIdx.x + 3] = 0ull;
-        }
-#endif
-        // ---- completion: sharded arrival, then the last workgroup finishes every step's argmin
-        __syncthreads();
-        const unsigned nblk = gridDim.x;
-        const int sh = blockIdx.x & 7, nsh = nblk < 8 ? (int)nblk : 8;
-        int* s_last = s_surv + cpb;
-        if (tid == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned shard_n = (nblk - sh + 7) >> 3;
-            const unsigned prev = __hip_atomic_fetch_add(&q.hdr->arrive_sh[sh][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int last = 0;
-            if (prev == shard_n - 1) {
-                const unsigned pt = __hip_atomic_fetch_add(&q.hdr->arrive_top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                last = pt == (unsigned)nsh - 1;
-            }
-            s_last[0] = last;
-        }
-        __syncthreads();
-        if (!s_last[0]) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #ifdef SSPP_WG_TIMING
         const unsigned long long t_ep = wall_clock64();
 #endif
-        // every producer has pushed and every other workgroup has left: finish the handed-over
-        // tickets (the initial spline is still in LDS), then count the finished survivors against
-        // the reserved slots and re-arm every reserved slot's ready word
+        // the last workgroup: every handed-over slot is finished; count the finished survivors
+        // against the reserved slots and re-arm every reserved slot's ready word
         {
-            const unsigned no = __hip_atomic_load(&q.hdr->norphan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int* s_ctl = s_surv;
-            for (unsigned k = 0; k < no; ++k) {  // workgroup-uniform
-                if (tid == 0) {
-                    const unsigned slot = __hip_atomic_load(q.orphan + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const unsigned sh_o = slot / (unsigned)q.shard_cap, lt = slot - sh_o * (unsigned)q.shard_cap;
-                    unsigned long long w = 0ull;
-                    if (!a.drop_orphans &&
-                        lt < __hip_atomic_load(&q.hdr->shard[sh_o].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        // reserved, and its producer has pushed (it arrived): the word is set
-                        w = __hip_atomic_load(q.rec + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    }
-                    s_ctl[0] = 1;
-                    s_ctl[1] = (int)slot;
-                    s_ctl[2] = (int)(unsigned)(w >> 32);
-                    s_ctl[3] = (int)(unsigned)w;
-                }
-                __syncthreads();
-                const unsigned long long w = ((unsigned long long)(unsigned)s_ctl[2] << 32) | (unsigned)s_ctl[3];
-                if (w == 0ull) {  // never reserved (the ticket was past the final count), or dropped (tests)
-                    __syncthreads();
-                    continue;
-                }
-                const unsigned t = (unsigned)s_ctl[1];
-                surv_load_rows<NT>(q, t, nrd, smem, s_f32, o_own);
-                __syncthreads();
-                surv_finish<D, NM, P, ONEGEOM, NT>(a, TT, otab, otab32, ospan, atab, aspan, smem, s_f32, o_fix, o_own,
-                                                   s_ctl, s_vsum, w, t, arc_base, feas_base, best_base != nullptr, q);
-                if (tid == 0) __hip_atomic_fetch_add(&q.hdr->served, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the outputs, list entries and counts
             __syncthreads();
-            // reserved slots: re-arm their ready words, count them against the finished survivors
+            SSPP_BEACON(12, no, 0);
             unsigned nres = 0;
             for (int s = 0; s < kSurvShards; ++s) {
                 const unsigned c = __hip_atomic_load(&q.hdr->shard[s].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1928,6 +1988,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             __hip_atomic_store(&q.hdr->lost, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->norphan, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->served, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            SSPP_BEACON(13, nl, lost);
 #ifdef SSPP_WG_TIMING
             g_p2_t[8 * 4095] = t_ep;
             g_p2_t[8 * 4095 + 1] = wall_clock64();
@@ -2948,6 +3009,7 @@ struct sspp_job {
     unsigned* d_sq_orphan = nullptr;
     int opt_linger_us = 10000;          // SSPP_OPT_SPLIT_LINGER_US (10 ms)
     int opt_split_drop = 0;             // SSPP_OPT_SPLIT_DROP (tests)
+    unsigned* dbg_beacon = nullptr;     // SSPP_OPT_DEBUG_BEACONS (-DSSPP_DEBUG_PROGRESS builds)
     long long sq_cap = 0;               // survivors the buffers hold (x sq_nrd doubles each)
     int sq_nrd = 0;
 };

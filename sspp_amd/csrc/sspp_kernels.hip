@@ -1102,8 +1102,8 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         const int shard_cap = ((nb_all + kSurvShards - 1) / kSurvShards) * cpb;
         int rc = survq_reserve(j, (int64_t)shard_cap * kSurvShards, nrd);
         if (rc) return rc;
-        q = SurvPtrs{j->d_sq_hdr, j->d_sq_rec, j->d_sq_ctrl, j->d_sq_ctrl32, j->d_sq_res, j->d_sq_orphan, j->sq_cap,
-                     shard_cap};
+        q = SurvPtrs{j->d_sq_hdr, j->d_sq_rec, j->d_sq_ctrl, j->d_sq_ctrl32, j->d_sq_res, j->d_sq_orphan, j->dbg_beacon,
+                     j->sq_cap, shard_cap};
         c.linger = (unsigned long long)j->opt_linger_us * 100ull;  // the 100 MHz wall clock
         c.drop_orphans = j->opt_split_drop;
         // the last workgroup's per-step minimum bits, ids and counts reuse the LDS from offset 0
@@ -1238,6 +1238,11 @@ extern "C" int sspp_job_set_option(sspp_job* j, int key, int64_t value) {
             if (j->kind != 0 || value < 0 || value > 1) return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_SPLIT_DROP: 0 or 1");
             j->opt_split_drop = (int)value;
             return SSPP_OK;
+#ifdef SSPP_DEBUG_PROGRESS
+        case 900:  // debugging builds: the split launch's progress beacons ([grid][4] words, mapped host memory)
+            j->dbg_beacon = (unsigned*)(uintptr_t)value;
+            return SSPP_OK;
+#endif
         case SSPP_OPT_TSP_REP:
             if (j->kind != 1 || value < -1 || value == 0 || value > 16)
                 return sspp::set_error(SSPP_E_INVAL, "SSPP_OPT_TSP_REP: -1 or 1..16");
