@@ -961,14 +961,17 @@ struct SurvShard {
     unsigned count;                    // slots reserved by the shard's producers
     unsigned taken;                    // slots popped by its consumers
     unsigned pushed;                   // producers whose slots are all ready
-    unsigned pad[29];                  // own 128-byte line
+    unsigned served;                   // its survivors finished (checked against count by the last workgroup;
+                                       // one counter per shard: a single launch-wide counter took every
+                                       // consumer through one contended atomic, 47 -> 75 us per 20-step launch)
+    unsigned pad[28];                  // own 128-byte line
 };
 struct SurvQ {
     SurvShard shard[kSurvShards];
     unsigned nlist;                    // entries of the argmin list (SurvPtrs::res)
     unsigned lost;                     // survivors the launch could not finish (0; see above)
     unsigned norphan;                  // tickets handed over to the last workgroup (SurvPtrs::orphan)
-    unsigned served;                   // survivors finished (checked against the reserved slots)
+    unsigned pad1;
     unsigned long long handoffs;       // tickets handed over, over the job's life (never re-armed)
     unsigned long long lost_total;     // lost survivors over the job's life (never re-armed)
     unsigned pad2[24];
@@ -1298,6 +1301,12 @@ __device__ __forceinline__ bool scan_pairs32(const float* q, bool live, unsigned
     return ghit;
 }
 
+// sum of a per-lane count over the wave
+__device__ __forceinline__ int wave_sum_u32(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
 // OR of a per-lane 64-bit mask over the wave, in scalar registers (the FP64 pass's pair loop
 // bound: only the pairs some lane left ambiguous)
 __device__ __forceinline__ unsigned long long wave_or64(unsigned long long m) {
@@ -1902,7 +1911,9 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             __syncthreads();
             surv_finish<D, NM, P, ONEGEOM, NT>(a, TT, otab, otab32, ospan, atab, aspan, smem, s_f32, o_fix, o_own,
                                                s_ctl, s_vsum, w, t, arc_base, feas_base, best_base != nullptr, q);
-            if (tid == 0) __hip_atomic_fetch_add(&q.hdr->served, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0)
+                __hip_atomic_fetch_add(&q.hdr->shard[t / (unsigned)q.shard_cap].served, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
         }
 #ifdef SSPP_WG_TIMING
         const unsigned long long t_ep = wall_clock64();
@@ -1913,19 +1924,28 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the outputs, list entries and counts
             __syncthreads();
             SSPP_BEACON(12, no, 0);
-            unsigned nres = 0;
+            // one shard per thread of the first wave (independent loads: a loop over the shards
+            // made 64 dependent round trips on the launch's critical path), then the re-arm stores
+            unsigned nlost = 0;
+            unsigned* s_cnt_sh = (unsigned*)smem;  // [kSurvShards] reserved slots per shard (the rows are done)
+            if (tid < kSurvShards) {
+                const unsigned c = __hip_atomic_load(&q.hdr->shard[tid].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned sv = __hip_atomic_load(&q.hdr->shard[tid].served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_cnt_sh[tid] = c;
+                nlost = sv < c ? c - sv : 0u;
+            }
+            if (tid < 64) nlost = (unsigned)wave_sum_u32((int)nlost);
+            __syncthreads();
             for (int s = 0; s < kSurvShards; ++s) {
-                const unsigned c = __hip_atomic_load(&q.hdr->shard[s].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                nres += c;
+                const unsigned c = s_cnt_sh[s];
                 for (unsigned e = tid; e < c; e += NT)
                     __hip_atomic_store(q.rec + (unsigned)s * (unsigned)q.shard_cap + e, 0ull, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
             if (tid == 0) {
-                const unsigned served = __hip_atomic_load(&q.hdr->served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (served < nres) {
-                    __hip_atomic_fetch_add(&q.hdr->lost, nres - served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(&q.hdr->lost_total, (unsigned long long)(nres - served), __ATOMIC_RELAXED,
+                if (nlost) {
+                    __hip_atomic_fetch_add(&q.hdr->lost, nlost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&q.hdr->lost_total, (unsigned long long)nlost, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
                 if (no) __hip_atomic_fetch_add(&q.hdr->handoffs, (unsigned long long)no, __ATOMIC_RELAXED,
@@ -1980,6 +2000,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             __hip_atomic_store(&q.hdr->shard[e].count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->shard[e].taken, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->shard[e].pushed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q.hdr->shard[e].served, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (tid == 0) {
             for (int k = 0; k < 8; ++k) __hip_atomic_store(&q.hdr->arrive_sh[k][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1987,7 +2008,6 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             __hip_atomic_store(&q.hdr->nlist, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->lost, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->norphan, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&q.hdr->served, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             SSPP_BEACON(13, nl, lost);
 #ifdef SSPP_WG_TIMING
             g_p2_t[8 * 4095] = t_ep;
