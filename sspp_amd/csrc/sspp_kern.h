@@ -913,35 +913,51 @@ __device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, 
 // unless the queue's storage is overrun) is written to every step record's `reserved` field, and
 // every host consumer of a record refuses it (SSPP_E_INCOMPLETE).
 // A reserved slot's producer is resident (it reserved the slot) and sets the ready word shortly.
-// The ready word is stored with release and read with acquire semantics at agent scope (the rows
-// before it are agent-scope stores and loads).
+// The ready word and the rows are agent-scope atomics ordered by s_waitcnt (SSPP_QUEUE_FENCES).
 // Each step's argmin: a feasible survivor takes part in an agent-scope atomicMin on its arc's bits
 // (non-negative doubles order like their bits) and the feasible count; one whose arc was not
 // above the minimum it saw is listed; the last workgroup to finish (sharded arrival counters, as
 // finish_batch) picks the lowest global id at each step's minimum from that list, writes the
 // records and re-arms the queue for the next launch on the job's stream.
 constexpr unsigned long long kLingerTicksDefault = 1000000;  // 10 ms of the 100 MHz wall clock
-#ifdef SSPP_DEBUG_PROGRESS  // progress beacons of the split launch, readable by the host while it runs
-#define SSPP_BEACON(B_PH, B_X, B_Y)                                                                                   \
+#ifdef SSPP_DEBUG_PROGRESS  // progress beacons of the split launch: plain stores into a [grid][8]
+// buffer (device memory for timing; mapped host memory to watch a launch that does not finish)
+#define SSPP_BEACON(B_PH, B_X, B_Y)                                                                              \
     do {                                                                                                        \
         if (q.beacon && threadIdx.x == 0) {                                                                     \
-            __hip_atomic_store(q.beacon + 4 * blockIdx.x + 1, (unsigned)(B_X), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
-            __hip_atomic_store(q.beacon + 4 * blockIdx.x + 2, (unsigned)(B_Y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
-            __hip_atomic_store(q.beacon + 4 * blockIdx.x, (unsigned)(B_PH), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);    \
+            q.beacon[8 * blockIdx.x + 1] = (unsigned)(B_X);                                                     \
+            q.beacon[8 * blockIdx.x + 2] = (unsigned)(B_Y);                                                     \
+            q.beacon[8 * blockIdx.x] = (unsigned)(B_PH);                                                        \
         }                                                                                                       \
     } while (0)
 // wave 1's progress (thread 64) in the workgroup's fourth word
 #define SSPP_BEACON1(B_PH)                                                                                      \
     do {                                                                                                        \
-        if (q.beacon && threadIdx.x == 64)                                                                      \
-            __hip_atomic_store(q.beacon + 4 * blockIdx.x + 3, (unsigned)(B_PH), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+        if (q.beacon && threadIdx.x == 64) q.beacon[8 * blockIdx.x + 3] = (unsigned)(B_PH);                    \
+    } while (0)
+// the 100 MHz wall clock's low word at a workgroup event, word 4 + B_K of its record
+#define SSPP_BEACON_T(B_K)                                                                                      \
+    do {                                                                                                        \
+        if (q.beacon && threadIdx.x == 0) q.beacon[8 * blockIdx.x + 4 + (B_K)] = (unsigned)wall_clock64();    \
     } while (0)
 #else
 #define SSPP_BEACON(B_PH, B_X, B_Y) do { } while (0)
 #define SSPP_BEACON1(B_PH) do { } while (0)
+#define SSPP_BEACON_T(B_K) do { } while (0)
 #endif
-#ifndef SSPP_QUEUE_FENCES  // 1: ready words release / acquire at agent scope; 0: relaxed (A/B)
-#define SSPP_QUEUE_FENCES 1
+// Ready-word ordering.  Every access to the queue's shared data (rows, ready words, counters)
+// is an agent-scope atomic (global_load / global_store ... sc1: coherent across the XCDs, not
+// held in a non-coherent cache level), and the protocol orders them with s_waitcnt: the producer
+// waits for its row stores to complete (vmcnt(0), each thread, then the workgroup barrier)
+// before it stores the ready word, and the consumer issues its row loads only after its load of
+// the word has returned.  That is the hardware ordering of CDNA4 for sc1 accesses.  The C++
+// release / acquire pair (SSPP_QUEUE_FENCES 1) compiles to buffer_wbl2 sc1 (write back this
+// XCD's whole L2) before each word store and buffer_inv sc1 (invalidate it) after each word
+// load: 49.4 -> 73.4 us per 20-step launch (profiles/r06d_*), for data that never passes
+// through those caches.  It stays a build option (tools/runs, A/B); the default is the
+// relaxed form.
+#ifndef SSPP_QUEUE_FENCES
+#define SSPP_QUEUE_FENCES 0
 #endif
 #if SSPP_QUEUE_FENCES
 #define SSPP_QUEUE_RELEASE_ORDER __ATOMIC_RELEASE
@@ -1593,6 +1609,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     const int nvalid = (int)min((long long)cpb, a.B - cand0);
     const long long first_id = a.first_id + step * a.step_stride;
     if (ABL & 64) return;
+    if constexpr (SPLIT) SSPP_BEACON_T(0);
 #ifdef SSPP_WG_TIMING
     const unsigned long long wg_t0 = wall_clock64();
     int wg_ns = -1;
@@ -1732,6 +1749,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     if constexpr (SPLIT) {
         static_assert(NM == 1 && ONEGEOM && !CBX, "split launches: single-geom movers without cylinder-box pairs");
         SSPP_BEACON(3, 0, 0);
+        SSPP_BEACON_T(1);
         // ---- producer: one queue reservation per workgroup (survivors in candidate order), the
         // survivors' rows written through to the coherent level, then each slot's ready word; the
         // other candidates' outputs are final here
@@ -1775,6 +1793,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             __hip_atomic_fetch_add(&q.hdr->shard[blockIdx.x % kSurvShards].pushed, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         SSPP_BEACON(4, 0, 0);
+        SSPP_BEACON_T(2);
         // ---- consumers: every workgroup pops survivors until the queue is empty; the launch's last
         // workgroup to arrive then finishes the handed-over slots in the same loop (one copy of
         // surv_finish in the kernel: a second inlined copy for the hand-over list raised the
@@ -1786,6 +1805,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         int* s_last = s_surv + cpb;
         bool last = false;        // workgroup-uniform: the launch's last workgroup, on the hand-over list
         unsigned ko = 0, no = 0;  // (thread 0) position in the hand-over list, its length
+        unsigned handed = 0;      // (thread 0) this workgroup handed a ticket over (it then leaves)
         for (;;) {  // workgroup-uniform (the slot and word come from LDS through readfirstlane)
             if (tid == 0) {
                 unsigned t = ~0u;
@@ -1816,6 +1836,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                                                                           __HIP_MEMORY_SCOPE_AGENT);
                                 __hip_atomic_store(q.orphan + k, t + shs * (unsigned)q.shard_cap, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
+                                handed = 1;
                                 t = ~0u;
                                 break;
                             }
@@ -1834,9 +1855,11 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                             const unsigned k = __hip_atomic_fetch_add(&q.hdr->norphan, 1u, __ATOMIC_RELAXED,
                                                                       __HIP_MEMORY_SCOPE_AGENT);
                             __hip_atomic_store(q.orphan + k, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            handed = 1;
                             t = ~0u;
                         } else {
                             SSPP_QUEUE_ACQUIRE();  // pairs with the producer's release
+                            __hip_atomic_store(q.rec + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
                         }
                     }
                 } else {
@@ -1852,6 +1875,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                             w = __hip_atomic_load(q.rec + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             if (w != 0ull) {
                                 SSPP_QUEUE_ACQUIRE();
+                                __hip_atomic_store(q.rec + slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                 t = slot;
                             }
                         }
@@ -1876,30 +1900,36 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                 }
 #endif
                 SSPP_BEACON(8, 0, 0);
-                // ---- completion: sharded arrival; the last workgroup goes on with the hand-over list
+                SSPP_BEACON_T(3);
+                // ---- completion: sharded arrival; the last workgroup goes on with the hand-over list.
+                // An arrival adds 1 + (handed over << 16), so the last arriver learns the list's
+                // length from the counters' old values (no further round trip on its critical path)
                 const unsigned nblk = gridDim.x;
                 const int shd = blockIdx.x & 7, nsh = nblk < 8 ? (int)nblk : 8;
                 if (tid == 0) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // outputs, list entries, hand-overs
                     const unsigned shard_n = (nblk - shd + 7) >> 3;
-                    const unsigned prev = __hip_atomic_fetch_add(&q.hdr->arrive_sh[shd][0], 1u, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned prev = __hip_atomic_fetch_add(&q.hdr->arrive_sh[shd][0], 1u + (handed << 16),
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     int lst = 0;
-                    if (prev == shard_n - 1) {
-                        const unsigned pt = __hip_atomic_fetch_add(&q.hdr->arrive_top[0], 1u, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT);
-                        lst = pt == (unsigned)nsh - 1;
+                    if ((prev & 0xFFFFu) == shard_n - 1) {
+                        const unsigned sho = (prev >> 16) + handed;  // the shard's hand-overs
+                        const unsigned pt = __hip_atomic_fetch_add(&q.hdr->arrive_top[0], 1u + (sho << 16),
+                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        lst = (pt & 0xFFFFu) == (unsigned)nsh - 1;
+                        if (lst) {
+                            SSPP_QUEUE_ACQUIRE();
+                            no = (pt >> 16) + sho;
+                        }
                     }
                     s_last[0] = lst;
-                    if (lst) {
-                        SSPP_QUEUE_ACQUIRE();
-                        no = __hip_atomic_load(&q.hdr->norphan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
+                    s_last[1] = (int)no;  // (s_last[1] is s_defer[0], which only the producers use)
                 }
                 __syncthreads();
                 const int lst = __builtin_amdgcn_readfirstlane(s_last[0]);
                 SSPP_BEACON(9 + lst, no, 0);
                 if (!lst) return;
+                if (__builtin_amdgcn_readfirstlane(s_last[1]) == 0) break;  // nothing was handed over
                 last = true;
                 continue;
             }
@@ -1918,51 +1948,25 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
 #ifdef SSPP_WG_TIMING
         const unsigned long long t_ep = wall_clock64();
 #endif
-        // the last workgroup: every handed-over slot is finished; count the finished survivors
-        // against the reserved slots and re-arm every reserved slot's ready word
-        {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the outputs, list entries and counts
-            __syncthreads();
-            SSPP_BEACON(12, no, 0);
-            // one shard per thread of the first wave (independent loads: a loop over the shards
-            // made 64 dependent round trips on the launch's critical path), then the re-arm stores
-            unsigned nlost = 0;
-            unsigned* s_cnt_sh = (unsigned*)smem;  // [kSurvShards] reserved slots per shard (the rows are done)
-            if (tid < kSurvShards) {
-                const unsigned c = __hip_atomic_load(&q.hdr->shard[tid].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned sv = __hip_atomic_load(&q.hdr->shard[tid].served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_cnt_sh[tid] = c;
-                nlost = sv < c ? c - sv : 0u;
-            }
-            if (tid < 64) nlost = (unsigned)wave_sum_u32((int)nlost);
-            __syncthreads();
-            for (int s = 0; s < kSurvShards; ++s) {
-                const unsigned c = s_cnt_sh[s];
-                for (unsigned e = tid; e < c; e += NT)
-                    __hip_atomic_store(q.rec + (unsigned)s * (unsigned)q.shard_cap + e, 0ull, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (tid == 0) {
-                if (nlost) {
-                    __hip_atomic_fetch_add(&q.hdr->lost, nlost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(&q.hdr->lost_total, (unsigned long long)nlost, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                }
-                if (no) __hip_atomic_fetch_add(&q.hdr->handoffs, (unsigned long long)no, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
-        // LDS is free: the per-step minimum bits, ids and feasible counts
+        // the last workgroup: every handed-over slot is finished
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the outputs, list entries and counts
+        __syncthreads();
+        SSPP_BEACON(12, no, 0);
+        // LDS is free: the per-step minimum bits, ids and feasible counts, the lost survivors
         unsigned long long* s_bits = (unsigned long long*)smem;
         unsigned long long* s_id = s_bits + kMaxSteps;
         unsigned* s_cnt = (unsigned*)(s_id + kMaxSteps);
+        unsigned* s_lost = s_cnt + kMaxSteps;
         const int nsteps = a.nsteps;
-        // one round trip for the header and the list's first NT entries: each thread reads
-        // entry tid before it knows the list's length (entries past it are stale and unused)
+        // one round trip for the header, the list's first NT entries (each thread reads entry tid
+        // before it knows the list's length; entries past it are stale and unused) and, one shard
+        // per thread, the reserved and the finished slots: the lost-work check
         const unsigned nl = __hip_atomic_load(&q.hdr->nlist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned lost = __hip_atomic_load(&q.hdr->lost, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned c_sh = 0, sv_sh = 0;
+        if (tid < kSurvShards) {
+            c_sh = __hip_atomic_load(&q.hdr->shard[tid].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sv_sh = __hip_atomic_load(&q.hdr->shard[tid].served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         unsigned long long rb = 0ull, rid = 0ull, rst = 0ull;
         if (best_base) {
             rb = __hip_atomic_load(&q.res[tid].bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1974,7 +1978,25 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             s_cnt[e] = __hip_atomic_load(q.hdr->count_feas + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_id[e] = ~0ull;
         }
+        const unsigned short_sh = c_sh > sv_sh ? c_sh - sv_sh : 0u;  // this shard's survivors not finished
+        if (tid < 64) {
+            const unsigned tot = (unsigned)wave_sum_u32((int)short_sh);
+            if (tid == 0) s_lost[0] = tot;
+        }
         __syncthreads();
+        const unsigned lost = (unsigned)__builtin_amdgcn_readfirstlane((int)s_lost[0]);
+        // a shard with unfinished slots still holds their ready words: re-armed here (every finished
+        // slot was re-armed by its consumer), so nothing stale reaches the next launch
+        if (short_sh)
+            for (unsigned e = 0; e < c_sh; ++e)
+                __hip_atomic_store(q.rec + (unsigned)tid * (unsigned)q.shard_cap + e, 0ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+            if (lost) __hip_atomic_fetch_add(&q.hdr->lost_total, (unsigned long long)lost, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+            if (no) __hip_atomic_fetch_add(&q.hdr->handoffs, (unsigned long long)no, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (best_base) {
             if ((unsigned)tid < nl && rb == s_bits[rst]) atomicMin(s_id + rst, rid);
             for (unsigned i = tid + NT; i < nl; i += NT) {
@@ -2008,7 +2030,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             __hip_atomic_store(&q.hdr->nlist, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->lost, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->norphan, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            SSPP_BEACON(13, nl, lost);
+            SSPP_BEACON(13, (unsigned)wall_clock64(), lost);
 #ifdef SSPP_WG_TIMING
             g_p2_t[8 * 4095] = t_ep;
             g_p2_t[8 * 4095 + 1] = wall_clock64();

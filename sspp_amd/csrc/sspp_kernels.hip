@@ -1091,7 +1091,9 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
     // candidates with collision, one output row per candidate; launch_c2f_nt
     // splits only a launch that is one resident round (c2f_one_round)
     c.nsteps = steps;
+    // (a split launch's arrival counters hold up to 65535 workgroups per shard in their low half)
     c.split = j->opt_split && (int64_t)steps * B >= kSplitMinCands && !d_ctrl && !d_ctrl_out && !j->arc_all &&
+              (int64_t)nblk * steps < 65536 &&
               c.has_scene && c.sc.npairs > 0 && !c.sc.static_block && j->nm == 1 && c.sc.onegeom && !c.sc.cylbox &&
               cpb >= 3;  // the consumers' control words live in s_surv (cpb + 1 ints)
     SurvPtrs q{};
@@ -1107,7 +1109,7 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         c.linger = (unsigned long long)j->opt_linger_us * 100ull;  // the 100 MHz wall clock
         c.drop_orphans = j->opt_split_drop;
         // the last workgroup's per-step minimum bits, ids and counts reuse the LDS from offset 0
-        c.lds = std::max(c.lds, (int)(20 * kMaxSteps));
+        c.lds = std::max(c.lds, (int)(20 * kMaxSteps + 16));
     }
     SsppPtrs o{d_ctrl, d_ctrl_out, d_arc, d_feasible, d_best, q, &split_used};
     const int nb = nblk * steps;
