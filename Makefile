@@ -20,7 +20,7 @@ PYMOD2   = sspp/_tsp$(PYEXT)
 PYINC    = $(shell $(PY) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
 PBINC    = $(shell $(PY) -c "import pybind11;print(pybind11.get_include())")
 
-HDRS = include/sspp_hip.h $(SRC)/model.h $(SRC)/sspp_device.h $(SRC)/sspp_filter.h $(SRC)/xml_lite.h $(SRC)/sspp_kern.h
+HDRS = include/sspp_hip.h $(SRC)/sspp_logtab.h $(SRC)/model.h $(SRC)/sspp_device.h $(SRC)/sspp_filter.h $(SRC)/xml_lite.h $(SRC)/sspp_kern.h
 # kernel instantiations, one translation unit per (dof, degree) (+ d0: TaskSpacePlanner), compiled
 # in parallel (one unit per degree also keeps the register allocation of each kernel its own)
 INST = $(OBJDIR)/sspp_inst_d0.o $(foreach d,1 2 3 4 6 7 9,$(foreach p,2 3,$(OBJDIR)/sspp_inst_d$(d)_p$(p).o))

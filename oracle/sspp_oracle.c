@@ -8,6 +8,7 @@
  * GPU kernels, which follow the same operation order, can be compared bit for bit.
  */
 #include "sspp_oracle.h"
+#include "../sspp_amd/csrc/sspp_logtab.h" /* data only: the sampler's ln table */
 
 #include <math.h>
 #include <stdlib.h>
@@ -281,33 +282,38 @@ static void or_sincospi(double x, double* s, double* c) {
 
 /* FP64 Box-Muller, the default normals of both planners (reference: std::normal_distribution
    <double>, include/sspp.h:116,125 and include/sspp/tsp_sampler.h:17): the kernels' normal_pair
-   (sspp_amd/csrc/sspp_kernels.hip) operation for operation — ln u1 by the atanh series of the
-   mantissa to s^20, sin / cos of 2 pi u2 by Taylor polynomials on |a| <= pi/4 after an exact
-   quarter-turn reduction, explicit fma, IEEE division and sqrt — so every normal is bit-identical.
+   (sspp_amd/csrc/sspp_kern.h) operation for operation — ln u1 division-free: k = round(64 m),
+   r = RN(64/k) and -ln r = hi + lo from the shared data table (sspp_amd/csrc/sspp_logtab.h,
+   generated by tools/gen_log_table.py and checked entry by entry in
+   tests/test_oracle_golden.py::test_log_table), t = fma(m, r, -1), ln(1 + t) by its series to
+   t^8; sin / cos of 2 pi u2 by Taylor polynomials on |a| <= pi/4 (to a^17 / a^16) after an exact
+   quarter-turn reduction; explicit fma, IEEE sqrt — so every normal is bit-identical.
    Accuracy against libm: tests/test_oracle_golden.py::test_normal_pair64_accuracy. */
+static const double bm_logtab[64][4] = {SSPP_LOGTAB_ENTRIES};
 static double bm_log64(double u) {
     uint64_t bits;
     memcpy(&bits, &u, 8);
+    const uint64_t mb = bits & 0x000fffffffffffffull;
     int e = (int)(bits >> 52) - 1023;
-    uint64_t mb = (bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
+    int k = (int)((mb + (1ull << 45)) >> 46);
+    const uint64_t mbits = mb | 0x3ff0000000000000ull;
     double m;
-    memcpy(&m, &mb, 8);
-    if (m > 0x1.6a09e667f3bcdp+0) { m = m * 0.5; e += 1; }
-    const double s = (m - 1.0) / (m + 1.0);
-    const double s2 = s * s;
-    double p = 0x1.8618618618618p-5;
-    p = fma(s2, p, 0x1.af286bca1af28p-5);
-    p = fma(s2, p, 0x1.e1e1e1e1e1e1ep-5);
-    p = fma(s2, p, 0x1.1111111111111p-4);
-    p = fma(s2, p, 0x1.3b13b13b13b14p-4);
-    p = fma(s2, p, 0x1.745d1745d1746p-4);
-    p = fma(s2, p, 0x1.c71c71c71c71cp-4);
-    p = fma(s2, p, 0x1.2492492492492p-3);
-    p = fma(s2, p, 0x1.999999999999ap-3);
-    p = fma(s2, p, 0x1.5555555555555p-2);
-    p = fma(s2, p, 1.0);
+    memcpy(&m, &mbits, 8);
+    if (k == 64) { k = 0; e += 1; m = m * 0.5; }
+    const double t = fma(m, bm_logtab[k][0], -1.0);
+    const double t2 = t * t;
+    double p = -0.125;
+    p = fma(t, p, 0x1.2492492492492p-3);
+    p = fma(t, p, -0x1.5555555555555p-3);
+    p = fma(t, p, 0x1.999999999999ap-3);
+    p = fma(t, p, -0.25);
+    p = fma(t, p, 0x1.5555555555555p-2);
+    p = fma(t, p, -0.5);
+    const double l1 = fma(t2, p, t);
     const double de = (double)e;
-    return fma(de, 0x1.62e42fefa3800p-1, fma(de, 0x1.ef35793c76730p-45, (s + s) * p));
+    const double hi = fma(de, 0x1.62e42fefa3800p-1, bm_logtab[k][1]);
+    const double lo = fma(de, 0x1.ef35793c76730p-45, bm_logtab[k][2]) + l1;
+    return hi + lo;
 }
 static void bm_sincos2pi64(double u, double* sn, double* cs) {
     const double q = rint(4.0 * u);
@@ -323,8 +329,7 @@ static void bm_sincos2pi64(double u, double* sn, double* cs) {
     sp = fma(a2, sp, 0x1.1111111111111p-7);
     sp = fma(a2, sp, -0x1.5555555555555p-3);
     const double sa = fma(a * a2, sp, a);
-    double cp = -0x1.6827863b97d97p-53;
-    cp = fma(a2, cp, 0x1.ae7f3e733b81fp-45);
+    double cp = 0x1.ae7f3e733b81fp-45;
     cp = fma(a2, cp, -0x1.93974a8c07c9dp-37);
     cp = fma(a2, cp, 0x1.1eed8eff8d898p-29);
     cp = fma(a2, cp, -0x1.27e4fb7789f5cp-22);

@@ -57,6 +57,7 @@ __device__ unsigned long long g_p2_w[8 << 13];  // split launch per queue slot: 
 #endif
 #include "sspp_device.h"
 #include "sspp_filter.h"
+#include "sspp_logtab.h"
 
 using namespace sspd;
 
@@ -257,30 +258,36 @@ __device__ __forceinline__ void philox_words(unsigned long long seed, unsigned l
 // reference, include/sspp.h:116,125 and include/sspp/tsp_sampler.h:17): one Philox4x32-10 call
 // gives two 53-bit uniforms u1 in (0, 1], u2 in [0, 1) -> z0 = r cos(2 pi u2), z1 = r sin(2 pi u2),
 // r = sqrt(-2 ln u1), |z| <= 8.57.  ln and sincos are written out as FP64 polynomials with
-// explicit fma (full double accuracy: the atanh series of ln m on m in [sqrt(1/2), sqrt(2)] to
-// s^20, Taylor sin / cos on |a| <= pi/4 to a^17 / a^18) and IEEE division and sqrt, so
-// oracle/sspp_oracle.c::or_normal_pair reproduces every normal bit for bit (libm's log and
-// sincospi agreed only to ~1 ulp).
+// explicit fma (sin / cos: Taylor on |a| <= pi/4 to a^17 / a^16), an IEEE sqrt, and no division:
+// ln u = e ln 2 + ln m with m = k/64 (1 + t), k = round(64 m) — a 64-entry table (sspp_logtab.h,
+// tools/gen_log_table.py) holds r = RN(64/k) and -ln r as hi + lo, t = fma(m, r, -1) is one
+// rounding with |t| <= 2^-7, and ln(1 + t) is its series to t^8 (remainder < 2e-20).  m near 2
+// takes the next exponent's entry k = 64 (r = 1, t = m/2 - 1 exact), so ln u keeps its relative
+// precision as u -> 1.  (Round 5 computed ln m by the atanh series of s = (m-1)/(m+1), an IEEE
+// FP64 division: v_div_scale x2, v_rcp_f64, four fma, v_div_fmas / fixup per pair.)
+// oracle/sspp_oracle.c::or_normal_pair reproduces every normal bit for bit.
 __device__ __forceinline__ double bm_log64(double u) {  // ln u, u in [2^-53, 1]
+    static const double tab[64][4] = {SSPP_LOGTAB_ENTRIES};
     const unsigned long long bits = (unsigned long long)__double_as_longlong(u);
+    const unsigned long long mb = bits & 0x000fffffffffffffull;
     int e = (int)(bits >> 52) - 1023;
-    double m = __longlong_as_double((long long)((bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull));
-    if (m > 0x1.6a09e667f3bcdp+0) { m = m * 0.5; e += 1; }  // m in [sqrt(1/2), sqrt(2)]
-    const double s = (m - 1.0) / (m + 1.0);                  // |s| <= 0.1716; m - 1 exact
-    const double s2 = s * s;
-    double p = 0x1.8618618618618p-5;                         // 1/21
-    p = fma(s2, p, 0x1.af286bca1af28p-5);                    // 1/19
-    p = fma(s2, p, 0x1.e1e1e1e1e1e1ep-5);                    // 1/17
-    p = fma(s2, p, 0x1.1111111111111p-4);                    // 1/15
-    p = fma(s2, p, 0x1.3b13b13b13b14p-4);                    // 1/13
-    p = fma(s2, p, 0x1.745d1745d1746p-4);                    // 1/11
-    p = fma(s2, p, 0x1.c71c71c71c71cp-4);                    // 1/9
-    p = fma(s2, p, 0x1.2492492492492p-3);                    // 1/7
-    p = fma(s2, p, 0x1.999999999999ap-3);                    // 1/5
-    p = fma(s2, p, 0x1.5555555555555p-2);                    // 1/3
-    p = fma(s2, p, 1.0);
-    const double de = (double)e;                             // ln 2 = hi + lo (hi: 42 bits)
-    return fma(de, 0x1.62e42fefa3800p-1, fma(de, 0x1.ef35793c76730p-45, (s + s) * p));
+    int k = (int)((mb + (1ull << 45)) >> 46);  // round(64 m) - 64, 0..64
+    double m = __longlong_as_double((long long)(mb | 0x3ff0000000000000ull));
+    if (k == 64) { k = 0; e += 1; m = m * 0.5; }  // m in [2 - 2^-7, 2): its half, next to 1
+    const double t = fma(m, tab[k][0], -1.0);     // m r - 1
+    const double t2 = t * t;
+    double p = -0.125;                             // -1/8
+    p = fma(t, p, 0x1.2492492492492p-3);           // 1/7
+    p = fma(t, p, -0x1.5555555555555p-3);          // -1/6
+    p = fma(t, p, 0x1.999999999999ap-3);           // 1/5
+    p = fma(t, p, -0.25);                          // -1/4
+    p = fma(t, p, 0x1.5555555555555p-2);           // 1/3
+    p = fma(t, p, -0.5);                           // -1/2
+    const double l1 = fma(t2, p, t);               // ln(1 + t)
+    const double de = (double)e;                   // ln 2 = hi + lo (hi: 42 bits, e hi exact)
+    const double hi = fma(de, 0x1.62e42fefa3800p-1, tab[k][1]);
+    const double lo = fma(de, 0x1.ef35793c76730p-45, tab[k][2]) + l1;
+    return hi + lo;
 }
 __device__ __forceinline__ void bm_sincos2pi64(double u, double* sn, double* cs) {  // u in [0, 1)
     const double q = rint(4.0 * u);
@@ -296,8 +303,7 @@ __device__ __forceinline__ void bm_sincos2pi64(double u, double* sn, double* cs)
     sp = fma(a2, sp, 0x1.1111111111111p-7);
     sp = fma(a2, sp, -0x1.5555555555555p-3);   // -1/3!
     const double sa = fma(a * a2, sp, a);
-    double cp = -0x1.6827863b97d97p-53;        // -1/18!
-    cp = fma(a2, cp, 0x1.ae7f3e733b81fp-45);
+    double cp = 0x1.ae7f3e733b81fp-45;         // 1/16! (the a^18 term: < 2.1e-18 on |a| <= pi/4)
     cp = fma(a2, cp, -0x1.93974a8c07c9dp-37);
     cp = fma(a2, cp, 0x1.1eed8eff8d898p-29);
     cp = fma(a2, cp, -0x1.27e4fb7789f5cp-22);
@@ -824,9 +830,12 @@ __device__ BlockBest reduce_recs(BlockBest* recs, int idx0, int stride, int n, d
 }
 
 // All NT threads of the workgroup call this after thread 0 filled `bb`.
+// (inline, bb by value: an out-of-line call took bb's address, so every lane of every workgroup
+// wrote the 32-byte record to scratch first — 64 B per lane of private segment for the
+// robocrane kernels and a third of their HBM writes)
 template <int NT = kBlock>
-__device__ void finish_batch(const BlockBest& bb, BlockBest* __restrict__ part, ArgminSync* sync,
-                             sspp_best* out, int nblk = -1, int b = -1) {
+__device__ __forceinline__ void finish_batch(const BlockBest bb, BlockBest* __restrict__ part, ArgminSync* sync,
+                                             sspp_best* out, int nblk = -1, int b = -1) {
     __shared__ double scratch[16];
     if (nblk < 0) { nblk = gridDim.x; b = blockIdx.x; }
     const int sh = b & 7;
@@ -1013,8 +1022,9 @@ struct SurvPtrs {
     float* ctrl32;     // [cap][nrd]  their FP32 copies
     SurvBest* res;     // [cap]       the argmin list (SurvQ::nlist entries)
     unsigned* orphan;  // [cap]       handed-over tickets (global slots; one per workgroup at most)
-    unsigned* beacon;  // debugging builds (-DSSPP_DEBUG_PROGRESS): [grid][4] progress words in mapped
-                       // host memory (SSPP_OPT_DEBUG_BEACONS); null otherwise
+#ifdef SSPP_DEBUG_PROGRESS
+    unsigned* beacon;  // debugging builds: [grid][8] progress / timing words (SSPP_BEACON)
+#endif
     long long cap;
     int shard_cap;     // slots per shard: shard s owns [s * shard_cap, (s + 1) * shard_cap)
 };

@@ -1104,7 +1104,10 @@ static int run_sspp(sspp_job* j, const double* d_ctrl, int64_t first_id, int64_t
         const int shard_cap = ((nb_all + kSurvShards - 1) / kSurvShards) * cpb;
         int rc = survq_reserve(j, (int64_t)shard_cap * kSurvShards, nrd);
         if (rc) return rc;
-        q = SurvPtrs{j->d_sq_hdr, j->d_sq_rec, j->d_sq_ctrl, j->d_sq_ctrl32, j->d_sq_res, j->d_sq_orphan, j->dbg_beacon,
+        q = SurvPtrs{j->d_sq_hdr, j->d_sq_rec, j->d_sq_ctrl, j->d_sq_ctrl32, j->d_sq_res, j->d_sq_orphan,
+#ifdef SSPP_DEBUG_PROGRESS
+                     j->dbg_beacon,
+#endif
                      j->sq_cap, shard_cap};
         c.linger = (unsigned long long)j->opt_linger_us * 100ull;  // the 100 MHz wall clock
         c.drop_orphans = j->opt_split_drop;

@@ -209,3 +209,24 @@ def test_reference_robot_path_fixture():
     assert np.abs(pts - np.array(d["bspline"])).max() <= 1e-13
     arc, feas = O.sspp_score(None, knots, k, ctrl[None], d["W"])
     assert feas[0] == 1 and abs(arc[0] - d["arc_length"]) <= 1e-12
+
+
+def test_log_table():
+    """The FP64 sampler's ln table (sspp_amd/csrc/sspp_logtab.h, shared data of the kernels and the
+    oracle), recomputed here independently: entry k - 64 holds r = RN(64 / k) and -ln r as
+    hi + lo, hi the double nearest -ln r and lo the double nearest the remainder (40-digit
+    decimal logarithms); the table's hex literals are parsed from the header text."""
+    import os
+    import re
+    from decimal import Decimal, getcontext
+    getcontext().prec = 40
+    path = os.path.join(os.path.dirname(__file__), "..", "sspp_amd", "csrc", "sspp_logtab.h")
+    rows = re.findall(r"\{(0x[^}]*)\}", open(path).read())
+    assert len(rows) == 64
+    for k, row in zip(range(64, 128), rows):
+        r, hi, lo, pad = (float.fromhex(x.strip()) for x in row.split(","))
+        assert r == 64.0 / k and pad == 0.0
+        L = -Decimal(r).ln()
+        assert hi == float(L)
+        assert lo == float(L - Decimal(hi))
+        assert abs(Decimal(hi) + Decimal(lo) - L) < Decimal(2) ** -105
