@@ -949,10 +949,16 @@ constexpr unsigned long long kLingerTicksDefault = 1000000;  // 10 ms of the 100
     do {                                                                                                        \
         if (q.beacon && threadIdx.x == 0) q.beacon[8 * blockIdx.x + 4 + (B_K)] = (unsigned)wall_clock64();    \
     } while (0)
+// the last workgroup's epilogue stages: word B_K after the grid's records
+#define SSPP_BEACON_E(B_K)                                                                                      \
+    do {                                                                                                        \
+        if (q.beacon && threadIdx.x == 0) q.beacon[8 * gridDim.x + (B_K)] = (unsigned)wall_clock64();          \
+    } while (0)
 #else
 #define SSPP_BEACON(B_PH, B_X, B_Y) do { } while (0)
 #define SSPP_BEACON1(B_PH) do { } while (0)
 #define SSPP_BEACON_T(B_K) do { } while (0)
+#define SSPP_BEACON_E(B_K) do { } while (0)
 #endif
 // Ready-word ordering.  Every access to the queue's shared data (rows, ready words, counters)
 // is an agent-scope atomic (global_load / global_store ... sc1: coherent across the XCDs, not
@@ -974,6 +980,12 @@ constexpr unsigned long long kLingerTicksDefault = 1000000;  // 10 ms of the 100
 #else
 #define SSPP_QUEUE_RELEASE_ORDER __ATOMIC_RELAXED
 #define SSPP_QUEUE_ACQUIRE() do { } while (0)
+#endif
+#ifndef SSPP_SPLIT_PRIO  // split launches: issue priority by phase (s_setprio; A/B: 0)
+#define SSPP_SPLIT_PRIO 1
+#endif
+#ifndef SSPP_SPLIT_PRIO_CONSUMER  // the priority of a wave past phase 1 (push, queued survivors)
+#define SSPP_SPLIT_PRIO_CONSUMER 0
 #endif
 #ifndef SSPP_QUEUE_WAITERS  // tickets per shard that may wait for slots not reserved yet
 #define SSPP_QUEUE_WAITERS 4
@@ -1467,7 +1479,6 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
     unsigned w_np = 0, w_nf = 0;
 #endif
     SSPP_BEACON(20, slot, 0);
-    SSPP_BEACON1(20);
     for (int jb = 0; jb < R; jb += NT) {  // workgroup-uniform
         // a uniform exit once a pass has found a contact (every thread's read precedes the barrier)
         if (jb > 0 && !__syncthreads_or(__hip_atomic_load(s_ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
@@ -1507,11 +1518,9 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
 #endif
     }
     SSPP_BEACON(21, slot, 0);
-    SSPP_BEACON1(21);
     __syncthreads();
     const bool feas = __builtin_amdgcn_readfirstlane(s_ctl[0]) != 0;
     SSPP_BEACON(22, slot, feas);
-    SSPP_BEACON1(22);
 #ifdef SSPP_WG_TIMING
     const unsigned long long c1 = clock64();
 #endif
@@ -1534,7 +1543,6 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
             if (lane == 0) s_vsum[vw] = acc;
         }
         SSPP_BEACON(23, slot, 0);
-        SSPP_BEACON1(23);
         __syncthreads();
         total = s_vsum[0];
         for (int w = 1; w < nvw; ++w) total = total + s_vsum[w];
@@ -1566,7 +1574,6 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
     }
     (void)slot;
     SSPP_BEACON(24, slot, 0);
-    SSPP_BEACON1(24);
     __syncthreads();  // the next survivor may overwrite the rows and the flags
 }
 
@@ -1620,6 +1627,11 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     const long long first_id = a.first_id + step * a.step_stride;
     if (ABL & 64) return;
     if constexpr (SPLIT) SSPP_BEACON_T(0);
+    // split launches: issue priority by phase — a wave still sampling goes before one in phase 1,
+    // which goes before one finishing queued survivors.  The SIMD's arbiter otherwise favours the
+    // oldest waves: at 5 waves per SIMD the first-dispatched waves finished phase 1 at ~12 us and
+    // the last at ~25-36 us (profiles/r06c_beacons*), whose survivors then formed the launch's tail
+    if constexpr (SPLIT && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(2);
 #ifdef SSPP_WG_TIMING
     const unsigned long long wg_t0 = wall_clock64();
     int wg_ns = -1;
@@ -1716,6 +1728,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         __syncthreads();
     }
     WG_PH(2);
+    if constexpr (SPLIT && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(1);
 
     const SceneT TT = T;
     const bool collide_on = a.has_scene && !(ABL & 2);
@@ -1756,6 +1769,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     }
     __syncthreads();
     WG_PH(3);
+    if constexpr (SPLIT && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(SSPP_SPLIT_PRIO_CONSUMER);
     if constexpr (SPLIT) {
         static_assert(NM == 1 && ONEGEOM && !CBX, "split launches: single-geom movers without cylinder-box pairs");
         SSPP_BEACON(3, 0, 0);
@@ -1802,7 +1816,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         if (tid == 0)
             __hip_atomic_fetch_add(&q.hdr->shard[blockIdx.x % kSurvShards].pushed, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-        SSPP_BEACON(4, 0, 0);
+        SSPP_BEACON(4, __popcll(__ballot(tid < nvalid && s_surv[tid] >= 0)), __smid());
         SSPP_BEACON_T(2);
         // ---- consumers: every workgroup pops survivors until the queue is empty; the launch's last
         // workgroup to arrive then finishes the handed-over slots in the same loop (one copy of
@@ -1816,6 +1830,9 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         bool last = false;        // workgroup-uniform: the launch's last workgroup, on the hand-over list
         unsigned ko = 0, no = 0;  // (thread 0) position in the hand-over list, its length
         unsigned handed = 0;      // (thread 0) this workgroup handed a ticket over (it then leaves)
+#ifdef SSPP_DEBUG_PROGRESS
+        unsigned nfin = 0;        // (thread 0) survivors this workgroup finished (beacon word 3)
+#endif
         for (;;) {  // workgroup-uniform (the slot and word come from LDS through readfirstlane)
             if (tid == 0) {
                 unsigned t = ~0u;
@@ -1938,6 +1955,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
                 __syncthreads();
                 const int lst = __builtin_amdgcn_readfirstlane(s_last[0]);
                 SSPP_BEACON(9 + lst, no, 0);
+                if (lst) SSPP_BEACON_E(0);
                 if (!lst) return;
                 if (__builtin_amdgcn_readfirstlane(s_last[1]) == 0) break;  // nothing was handed over
                 last = true;
@@ -1946,7 +1964,6 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             const unsigned long long w = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(s_ctl[2]) << 32) |
                                          (unsigned)__builtin_amdgcn_readfirstlane(s_ctl[3]);
             SSPP_BEACON(7, t, (unsigned)w);
-            SSPP_BEACON1(7);
             surv_load_rows<NT>(q, t, nrd, smem, s_f32, o_own);
             __syncthreads();
             surv_finish<D, NM, P, ONEGEOM, NT>(a, TT, otab, otab32, ospan, atab, aspan, smem, s_f32, o_fix, o_own,
@@ -1954,6 +1971,9 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             if (tid == 0)
                 __hip_atomic_fetch_add(&q.hdr->shard[t / (unsigned)q.shard_cap].served, 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+#ifdef SSPP_DEBUG_PROGRESS
+            if (tid == 0 && q.beacon) q.beacon[8 * blockIdx.x + 3] = ++nfin;
+#endif
         }
 #ifdef SSPP_WG_TIMING
         const unsigned long long t_ep = wall_clock64();
@@ -1962,6 +1982,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the outputs, list entries and counts
         __syncthreads();
         SSPP_BEACON(12, no, 0);
+        SSPP_BEACON_E(1);
         // LDS is free: the per-step minimum bits, ids and feasible counts, the lost survivors
         unsigned long long* s_bits = (unsigned long long*)smem;
         unsigned long long* s_id = s_bits + kMaxSteps;
@@ -1995,6 +2016,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         }
         __syncthreads();
         const unsigned lost = (unsigned)__builtin_amdgcn_readfirstlane((int)s_lost[0]);
+        SSPP_BEACON_E(2);
         // a shard with unfinished slots still holds their ready words: re-armed here (every finished
         // slot was re-armed by its consumer), so nothing stale reaches the next launch
         if (short_sh)
@@ -2017,6 +2039,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             }
         }
         __syncthreads();
+        SSPP_BEACON_E(3);
         for (int e = tid; e < nsteps; e += NT) {
             if (best_base) {
                 const bool has = s_id[e] != ~0ull;
