@@ -604,7 +604,7 @@ def run_dropin(args):
         # the cold side: a fresh planner's first plan() (its job is created in that call: tables,
         # device buffers, pinned outputs; the hit-order pre-pass runs asynchronously beside it)
         # and its next calls, in this already-initialised process
-        cold = []
+        cold, cold_parts = [], []
         for _ in range(3):
             fresh = _sspp.SamplingPathPlanner7(os.path.join(S.SCENE_DIR, "robocrane.xml"))
             ts = []
@@ -613,6 +613,7 @@ def run_dropin(args):
                 fresh.plan(start, end, 0.08, limits, B, W, n)
                 ts.append((time.perf_counter() - ta) * 1e6)
             cold.append(ts)
+            cold_parts.append({k: round(v, 1) for k, v in fresh._timings().items()})
             del fresh
     finally:
         sys.stdout.flush()
@@ -646,9 +647,14 @@ def run_dropin(args):
         "latency_us": {"median": float(np.median(lat_us)), "p10": float(np.percentile(lat_us, 10)),
                        "p90": float(np.percentile(lat_us, 90)), "mean": float(lat_us.mean())},
         "feasible_per_plan": float(np.mean(nfeas)),
-        # a fresh SamplingPathPlanner7: first plan() (job creation included), then calls 2-4
+        # a fresh SamplingPathPlanner7: first plan() (scene tables, planner stream, job creation
+        # included), then calls 2-4; median and max over the fresh objects, with the first call's
+        # parts (cold_call_parts_us) — the first fresh object in a process also creates a new HIP
+        # hardware queue for its stream (drop-in)
         "first_call_us": float(np.median([c[0] for c in cold])),
+        "first_call_us_max": float(np.max([c[0] for c in cold])),
         "cold_calls_us": [[round(x, 1) for x in c] for c in cold],
+        "cold_call_parts_us": cold_parts,
         "isolated_step_kernel_us": float(np.median(ks)),
         "dtype": "f64", "data": "synthetic (on-device Philox candidates around a linear init spline)",
         "config": {"workload": "robocrane SamplingPathPlanner7.plan(start, end, 0.08, ones(7), %d, %d, %d)"

@@ -67,4 +67,9 @@ int job_create_sspp_async(const sspp_scene* scene, const sspp_sspp_args* a, int6
 void job_set_ctrl_feasible_only(sspp_job* j, int on);
 // sspp_plan_sspp's cached planners (planner.hip): dropped when their scene is freed
 void planner_cache_drop(const sspp_scene* scene);
+// Process-wide HIP streams (created on first use, never destroyed): 0 = every drop-in planner's
+// plan() stream, 1 = every job's asynchronous hit-order pre-pass.  A new stream can cost a new
+// hardware queue (5.7 ms measured for a fresh planner's stream, the first in a process to need
+// one: profiles/r06j_bench_dropin.json), so planners and pre-passes share these two
+void* shared_stream(int which);  // a hipStream_t
 }  // namespace sspp

@@ -81,7 +81,7 @@ struct JobRef {
 struct sspp_planner {
     const sspp_scene* scene = nullptr;
     int D = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // sspp::shared_stream(0), not owned
     // plan(): job of the last shape
     JobRef plan_job;
     int plan_n = 0, plan_W = 0;
@@ -103,25 +103,37 @@ struct sspp_planner {
     Pinned<sspp_best> h_sbest;
     Dev<double> d_in;
     ~sspp_planner() {
+        if (stream) (void)hipStreamSynchronize(stream);  // this planner's work on the shared stream
         plan_job.reset();
         score_job.reset();
-        if (stream) (void)hipStreamDestroy(stream);
     }
 };
 
 extern "C" int sspp_planner_create(const sspp_scene* scene, int dof, sspp_planner** out) {
     sspp::clear_error();
     if (!out || dof < 1 || dof > 16) return sspp::set_error(SSPP_E_INVAL, "sspp_planner_create: bad argument");
+    hipStream_t st = (hipStream_t)sspp::shared_stream(0);
+    if (!st) return sspp::set_error(SSPP_E_HIP, "hipStreamCreate (shared planner stream)");
     auto* p = new sspp_planner();
     p->scene = scene;
     p->D = dof;
-    hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-        delete p;
-        return hipck(e, "hipStreamCreate");
-    }
+    p->stream = st;
     *out = p;
     return SSPP_OK;
+}
+
+// One stream for every planner's plan() and one for every job's pre-pass, for the process: a
+// planner used to create its own stream, and the first fresh planner after the process's first
+// three streams paid 5.7 ms for a new hardware queue in its first plan().
+// plan() synchronises the stream it enqueued on, so planners used from one host thread never wait
+// for each other; planners driven from several host threads share the GPU queue in order.
+void* sspp::shared_stream(int which) {
+    static std::mutex mu;
+    static hipStream_t st[2] = {nullptr, nullptr};
+    if (which < 0 || which > 1) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    if (!st[which] && hipStreamCreateWithFlags(&st[which], hipStreamNonBlocking) != hipSuccess) st[which] = nullptr;
+    return (void*)st[which];
 }
 
 extern "C" void sspp_planner_free(sspp_planner* p) { delete p; }

@@ -984,6 +984,9 @@ constexpr unsigned long long kLingerTicksDefault = 1000000;  // 10 ms of the 100
 #ifndef SSPP_SPLIT_PRIO  // split launches: issue priority by phase (s_setprio; A/B: 0)
 #define SSPP_SPLIT_PRIO 1
 #endif
+#ifndef SSPP_PRIO_ALL  // the same priorities in the unsplit instances (A/B)
+#define SSPP_PRIO_ALL 0
+#endif
 #ifndef SSPP_SPLIT_PRIO_CONSUMER  // the priority of a wave past phase 1 (push, queued survivors)
 #define SSPP_SPLIT_PRIO_CONSUMER 0
 #endif
@@ -1631,7 +1634,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     // which goes before one finishing queued survivors.  The SIMD's arbiter otherwise favours the
     // oldest waves: at 5 waves per SIMD the first-dispatched waves finished phase 1 at ~12 us and
     // the last at ~25-36 us (profiles/r06c_beacons*), whose survivors then formed the launch's tail
-    if constexpr (SPLIT && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(2);
+    if constexpr ((SPLIT || SSPP_PRIO_ALL) && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(2);
 #ifdef SSPP_WG_TIMING
     const unsigned long long wg_t0 = wall_clock64();
     int wg_ns = -1;
@@ -1728,7 +1731,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         __syncthreads();
     }
     WG_PH(2);
-    if constexpr (SPLIT && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr ((SPLIT || SSPP_PRIO_ALL) && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(1);
 
     const SceneT TT = T;
     const bool collide_on = a.has_scene && !(ABL & 2);
@@ -1769,7 +1772,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     }
     __syncthreads();
     WG_PH(3);
-    if constexpr (SPLIT && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(SSPP_SPLIT_PRIO_CONSUMER);
+    if constexpr ((SPLIT || SSPP_PRIO_ALL) && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(SSPP_SPLIT_PRIO_CONSUMER);
     if constexpr (SPLIT) {
         static_assert(NM == 1 && ONEGEOM && !CBX, "split launches: single-geom movers without cylinder-box pairs");
         SSPP_BEACON(3, 0, 0);

@@ -814,7 +814,8 @@ static int prepass_start(sspp_job* j, const double* init_ctrl, double sigma, con
     const auto t0 = std::chrono::steady_clock::now();
     const int M = kCensus, nw = (j->W + 64) >> 6;
     const size_t nh = (size_t)M * nw;
-    HIPCHK(hipStreamCreateWithFlags(&j->pre_stream, hipStreamNonBlocking));
+    j->pre_stream = (hipStream_t)sspp::shared_stream(1);  // shared by every job's pre-pass, not owned
+    if (!j->pre_stream) return sspp::set_error(SSPP_E_HIP, "hipStreamCreate (shared pre-pass stream)");
     HIPCHK(hipEventCreateWithFlags(&j->pre_ev, hipEventDisableTiming));
     HIPCHK(hipMalloc((void**)&j->d_hits, sizeof(unsigned long long) * nh));
     HIPCHK(hipHostMalloc((void**)&j->h_hits, sizeof(unsigned long long) * nh, hipHostMallocDefault));
@@ -1573,7 +1574,7 @@ extern "C" void sspp_job_free(sspp_job* j) {
     for (void* q : {(void*)j->d_hits, (void*)j->d_census_pairs}) if (q) (void)hipFree(q);
     if (j->h_hits) (void)hipHostFree(j->h_hits);
     if (j->pre_ev) (void)hipEventDestroy(j->pre_ev);
-    if (j->pre_stream) (void)hipStreamDestroy(j->pre_stream);
+
     for (double* p : {j->d_knots, j->d_tab, j->d_init, j->d_limits, j->d_Minv, j->d_mean, j->d_sigma})
         if (p) (void)hipFree(p);
     if (j->d_span) (void)hipFree(j->d_span);

@@ -22,6 +22,7 @@
 #include <cmath>
 #include <iostream>
 #include <memory>
+#include <chrono>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -279,6 +280,8 @@ private:
 
     void ensure_planner() {
         if (planner_) return;
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
         if (!scene_) {
             sspp_scene* s = nullptr;
             // count_static = 1: checkCollision's ncon is the whole scene's (include/sspp.h:143-144,
@@ -286,10 +289,30 @@ private:
             ck(sspp_scene_create(model_.get(), SSPP_MODE_QPOS, N, 1, &s), "scene");
             scene_.reset(s);
         }
+        const auto t1 = clk::now();
         sspp_planner* p = nullptr;
         ck(sspp_planner_create(scene_.get(), N, &p), "planner");
         planner_.reset(p);
+        scene_us_ = std::chrono::duration<double, std::micro>(t1 - t0).count();
+        planner_us_ = std::chrono::duration<double, std::micro>(clk::now() - t1).count();
     }
+
+public:
+    // diagnostics, not the reference's API: where a fresh object's first plan() spends its time —
+    // the device scene tables, the planner (its HIP stream), and the job of the plan() shape
+    // (tables, buffers, the asynchronous pre-pass's start), microseconds
+    py::dict timings() {
+        py::dict d;
+        d["scene_create_us"] = scene_us_;
+        d["planner_create_us"] = planner_us_;
+        int64_t v = -1;
+        if (planner_ && sspp_planner_get_option(planner_.get(), SSPP_OPT_CREATE_US, &v) == SSPP_OK)
+            d["job_create_us"] = (double)v;
+        return d;
+    }
+
+private:
+    double scene_us_ = 0.0, planner_us_ = 0.0;
 
     std::string xml_path_;
     std::unique_ptr<sspp_model, ModelDel> model_;
@@ -336,7 +359,8 @@ void bind(py::module& m, const std::string& planner_name, const std::string& spl
         .def_readwrite("seed", &P::seed)
         .def_readonly("last_best_cost", &P::last_best_cost)
         .def_readonly("last_best_index", &P::last_best_index)
-        .def_readonly("last_feasible_ids", &P::last_feasible_ids);
+        .def_readonly("last_feasible_ids", &P::last_feasible_ids)
+        .def("_timings", &P::timings);
 }
 
 }  // namespace
