@@ -23,6 +23,21 @@
 namespace sspd {
 
 constexpr double kDeep = -1e-3;     // include/Collision.h:93 "col_dist < -1e-3"
+// kDeep as a scalar-register value at each use: a 64-bit constant in VALU code is materialised in
+// a VGPR pair, which the compiler hoisted out of the pair loops and then spilled to scratch in the
+// multi-goal / stacking kernels; through an empty asm it is two s_mov at the use instead
+#ifndef SSPP_DEEP_SGPR
+#define SSPP_DEEP_SGPR 1
+#endif
+__host__ __device__ __forceinline__ double deep_thr() {
+#if defined(__HIP_DEVICE_COMPILE__) && SSPP_DEEP_SGPR
+    double c = kDeep;
+    asm volatile("" : "+s"(c));
+    return c;
+#else
+    return kDeep;
+#endif
+}
 constexpr double kMinVal = 1e-15;   // mjMINVAL
 constexpr int kMaxP = 7;            // max spline degree in kernels
 
@@ -188,7 +203,7 @@ SSPP_HD int col_plane_box(const double* pp, const double* pm, const double* bp, 
         const double t = d0 + l;
         // mjc_PlaneBox: a corner counts unless dist + ldist > margin or ldist > 0 (the corners
         // of the half turned away from the plane never count), at most 4
-        if (!(t > margin) && !(l > 0.0) && nc < 4) { nc++; if (t < kDeep) ndd++; }
+        if (!(t > margin) && !(l > 0.0) && nc < 4) { nc++; if (t < deep_thr()) ndd++; }
     }
     *nd = ndd;
     return nc;
@@ -199,7 +214,7 @@ SSPP_HD int col_plane_sphere(const double* pp, const double* pm, const double* s
     col3(pm, 2, n);
     d[0] = sp[0] - pp[0]; d[1] = sp[1] - pp[1]; d[2] = sp[2] - pp[2];
     double dist = dot3(d, n) - r;
-    *nd = dist < kDeep;
+    *nd = dist < deep_thr();
     return dist <= margin;  // mjc_PlaneSphere: no contact only when dist > margin
 }
 SSPP_HD int col_plane_cyl(const double* pp, const double* pm, const double* cp, const double* cm,
@@ -219,14 +234,14 @@ SSPP_HD int col_plane_cyl(const double* pp, const double* pm, const double* cp, 
     const double nearc = dn - ha;
     const double p1 = nearc - rim, p2 = (dn + ha) - rim, pt = nearc + 0.5 * rim;
     if (p1 > margin) { *nd = 0; return 0; }
-    *nd = (p1 < kDeep) + (p2 < kDeep) + 2 * (pt < kDeep);
+    *nd = (p1 < deep_thr()) + (p2 < deep_thr()) + 2 * (pt < deep_thr());
     return 1 + (p2 <= margin) + 2 * (pt <= margin);
 }
 SSPP_HD int col_sphere_sphere(const double* p1, double r1, const double* p2, double r2,
                               double margin, int* nd) {
     double d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
     double dist = sqrt(dot3(d, d)) - (r1 + r2);
-    *nd = dist < kDeep;
+    *nd = dist < deep_thr();
     return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 SSPP_HD int col_sphere_box(const double* sp, double r, const double* bp, const double* bm,
@@ -244,7 +259,7 @@ SSPP_HD int col_sphere_box(const double* sp, double r, const double* bp, const d
         if (f < mind) mind = f;
     }
     double dist = inside ? (-mind - r) : (sqrt(out2) - r);
-    *nd = dist < kDeep;
+    *nd = dist < deep_thr();
     return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 SSPP_HD int col_sphere_cyl(const double* sp, double r, const double* cp, const double* cm,
@@ -261,7 +276,7 @@ SSPP_HD int col_sphere_cyl(const double* sp, double r, const double* cp, const d
         double oz = dz > 0.0 ? dz : 0.0, orr = dr > 0.0 ? dr : 0.0;
         dist = sqrt(fma(orr, orr, oz * oz)) - r;
     }
-    *nd = dist < kDeep;
+    *nd = dist < deep_thr();
     return dist <= margin;  // MuJoCo: no contact only when dist > margin
 }
 
@@ -358,8 +373,8 @@ SSPP_HD int bb_clip_2d(const double* cu, const double* cv, const double* cd, dou
         }
         if (ok && t0 <= t1) {
             const double dd = cd[e2] - cd[e];
-            if (-fma(t0, dd, cd[e]) < kDeep) ++nd;
-            if (t1 < 1.0 && -fma(t1, dd, cd[e]) < kDeep) ++nd;
+            if (-fma(t0, dd, cd[e]) < deep_thr()) ++nd;
+            if (t1 < 1.0 && -fma(t1, dd, cd[e]) < deep_thr()) ++nd;
         }
     }
     // ... and the rectangle's corners strictly inside the incident parallelogram
@@ -372,7 +387,7 @@ SSPP_HD int bb_clip_2d(const double* cu, const double* cv, const double* cd, dou
         const double al = (wu * bv - wv * bu) * idet, be = (au * wv - av * wu) * idet;
         if (al > 0.0 && al < 1.0 && be > 0.0 && be < 1.0) {
             const double d = fma(be, cd[3] - cd[0], fma(al, cd[1] - cd[0], cd[0]));
-            if (-d < kDeep) ++nd;
+            if (-d < deep_thr()) ++nd;
         }
     }
     return nd > 0 ? nd : 1;
@@ -551,7 +566,7 @@ SSPP_HD int box_box_deep_class(const double* pa, const double* ma, const double*
     for (int i = 0; i < 3; ++i) {  // faces of A
         const double rb = fma(eb[2], AR[i][2], fma(eb[1], AR[i][1], eb[0] * AR[i][0]));
         const double sep = fabs(t[i]) - (ea[i] + rb);
-        if (sep >= kDeep) return -1;
+        if (sep >= deep_thr()) return -1;
         if (sep > best_face) { best_face = sep; fi = i; }
     }
 #pragma unroll
@@ -559,7 +574,7 @@ SSPP_HD int box_box_deep_class(const double* pa, const double* ma, const double*
         const double pr = fabs(fma(t[2], R[2][j], fma(t[1], R[1][j], t[0] * R[0][j])));
         const double ra = fma(ea[2], AR[2][j], fma(ea[1], AR[1][j], ea[0] * AR[0][j]));
         const double sep = pr - (ra + eb[j]);
-        if (sep >= kDeep) return -1;
+        if (sep >= deep_thr()) return -1;
         if (sep > best_face) { best_face = sep; fi = 3 + j; }
     }
     bool edge = false;  // some edge axis separates by more than best_face + 1e-12
@@ -584,7 +599,7 @@ SSPP_HD int box_box_deep_class(const double* pa, const double* ma, const double*
                 rb = fma(eb[k], fabs(dot3(bk, L)), rb);
             }
             const double num = pr - (ra + rb), len = sqrt(len2);
-            if (num >= kDeep * len) return -1;
+            if (num >= deep_thr() * len) return -1;
             edge = edge || num > fthr * len;
         }
     }
@@ -621,23 +636,23 @@ SSPP_HD int box_box_deep_class_up(const double* pa, const double* ma, const doub
     int fi;
     // faces of A
     sep = fabs(t0) - (ea[0] + fma(eb[1], A01, eb[0] * A00));
-    if (sep >= kDeep) return -1;
+    if (sep >= deep_thr()) return -1;
     best_face = sep; fi = 0;
     sep = fabs(t1) - (ea[1] + fma(eb[1], A11, eb[0] * A10));
-    if (sep >= kDeep) return -1;
+    if (sep >= deep_thr()) return -1;
     if (sep > best_face) { best_face = sep; fi = 1; }
     sep = fabs(t2) - (ea[2] + eb[2] * A22);
-    if (sep >= kDeep) return -1;
+    if (sep >= deep_thr()) return -1;
     if (sep > best_face) { best_face = sep; fi = 2; }
     // faces of B
     sep = fabs(fma(t1, R10, t0 * R00)) - (fma(ea[1], A10, ea[0] * A00) + eb[0]);
-    if (sep >= kDeep) return -1;
+    if (sep >= deep_thr()) return -1;
     if (sep > best_face) { best_face = sep; fi = 3; }
     sep = fabs(fma(t1, R11, t0 * R01)) - (fma(ea[1], A11, ea[0] * A01) + eb[1]);
-    if (sep >= kDeep) return -1;
+    if (sep >= deep_thr()) return -1;
     if (sep > best_face) { best_face = sep; fi = 4; }
     sep = fabs(t2 * R22) - (ea[2] * A22 + eb[2]);
-    if (sep >= kDeep) return -1;
+    if (sep >= deep_thr()) return -1;
     if (sep > best_face) { best_face = sep; fi = 5; }
     bool edge = false;
     const double fthr = best_face + 1e-12;
@@ -645,7 +660,7 @@ SSPP_HD int box_box_deep_class_up(const double* pa, const double* ma, const doub
     auto ax = [&](double len2, double pr, double ra, double rb) -> int {
         if (len2 < 1e-12) return 1;
         const double num = pr - (ra + rb), len = sqrt(len2);
-        if (num >= kDeep * len) return 0;
+        if (num >= deep_thr() * len) return 0;
         edge = edge || num > fthr * len;
         return 1;
     };
@@ -1124,7 +1139,7 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
         if (CB == 2 || (!DEFER && cyl_vertical(m1) && upright3(m2))) {
             const double sd = cb_upright_sd(p1, s1, p2, m2, s2);
             if (NEED_DEEP) {
-                const int d = (margin >= kDeep) ? (sd < kDeep) : (sd < margin && sd < kDeep);
+                const int d = (margin >= deep_thr()) ? (sd < deep_thr()) : (sd < margin && sd < deep_thr());
                 *nd = d;
                 return d;
             }
@@ -1132,9 +1147,9 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
         }
         if (DEFER && !NEED_DEEP) return -1;
         if (NEED_DEEP) {
-            int d = (margin >= kDeep) ? (int)cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, kDeep)
+            int d = (margin >= deep_thr()) ? (int)cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, deep_thr())
                                       : (int)(cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, margin) &&
-                                              cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, kDeep));
+                                              cyl_box_overlap<OUTLINE>(p1, m1, s1, p2, m2, s2, deep_thr()));
             *nd = d;
             return d;
         }
@@ -1146,10 +1161,10 @@ SSPP_HD int collide(int t1, const double* p1, const double* m1, const double* s1
         // UP: every box-box pair of the job is upright (a per-pair run-time dispatch for the
         // generic kernels measured neutral on multi-goal: 31.4-31.5 vs 31.8 M cand/s)
         if (UP)
-            *nd = (margin >= kDeep || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
+            *nd = (margin >= deep_thr() || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
                       ? box_box_deep_count_up(p1, m1, s1, p2, m2, s2) : 0;
         else
-            *nd = (margin >= kDeep || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
+            *nd = (margin >= deep_thr() || sat_box_box(p1, m1, s1, p2, m2, s2, margin))
                       ? box_box_deep_count(p1, m1, s1, p2, m2, s2) : 0;
         if (*nd > 0) SSPP_NP_STAT(14);
         return *nd;
