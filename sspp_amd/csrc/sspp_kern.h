@@ -2509,6 +2509,9 @@ __device__ __forceinline__ void tsp_prologue(const TspK& a, const TspVar& pv, co
 // wave that happen to hold one), and each lane sums its records in pair order: the same additions
 // in the same order as the inline form, so the costs are bit-identical.
 constexpr int kDefPairs = 8;
+#ifndef SSPP_TSP_SUB_LAUNDER
+#define SSPP_TSP_SUB_LAUNDER 1
+#endif
 // 4 waves per SIMD, no spills.  5 waves (96 VGPRs, ~75 spilled) measured 106.0 against 101.6 M
 // cand/s on stacking, but its spills raised the HBM traffic from 1.4x to 140x the algorithmic bytes
 #ifndef SSPP_TSP_WAVES_PER_EU_DEF
@@ -2553,7 +2556,16 @@ __device__ __forceinline__ void tsp_body(
     tsp_prologue(a, pv, Minv, mean, sigma, vias_in, vias_out, tid, kBlock, cpr, candR, nvR, nfx, s_V, s_ctrl);
 
     // one sub-batch; the forms without sub-batches compile it once, with no loop around it
+    const int tid_o = tid, slot_o = slot, lane_o = lane;
     auto sub = [&](const int r) -> bool {
+#if SSPP_TSP_SUB_LAUNDER
+    // the lane's indices through an empty asm per sub-batch: what derives from them (LDS record
+    // pointers, the basis rows of its waypoint) is recomputed per sub-batch instead of being
+    // hoisted in front of the loop and held (spilled) across it
+    int tid = tid_o;
+    if constexpr (REP_OK) asm volatile("" : "+v"(tid));
+    const int slot = REP_OK ? tid / lpc : slot_o, lane = REP_OK ? tid - slot * lpc : lane_o;
+#endif
     const long long cand0 = candR + (long long)r * cpb;
     const long long nvalid = min((long long)cpb, a.B - cand0);  // <= 0 past a ragged batch's end
     if (REP_OK && nvalid <= 0) return false;  // past a ragged batch's end
