@@ -2585,7 +2585,6 @@ __device__ __forceinline__ void tsp_body(
         double* rt = s_rterm + tid * npr;
         for (int k = 0; k < npr; ++k) rn[k] = 0;
         const bool has = valid && lane < cp;
-        double pz = 0.0;
         if (has) {
             const int i = lane + 1;
             double pv[4], pc[4];
@@ -2594,10 +2593,13 @@ __device__ __forceinline__ void tsp_body(
             for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pc[d], 1, 64);
             if ((tid & 63) == 0) eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
             aL = aL + dist_nd<D>(pv, pc);
-            pz = pc[2];
+            // (the waypoint's height pz is read back from the recorded mover pose after the
+            // records are counted: a register less across the pair loop)
 #ifndef SSPP_PROF_NOCOLL  // profiling variant only
             point_collide<D, NM, 1, true, ONEGEOM, CB, 3, UP>(pc, a.sc, T, mask, nullptr, nullptr, rn, rt,
                                                              s_rpose + tid * 8);
+#else
+            s_rpose[tid * 8 + 2] = pc[2];
 #endif
         }
         __syncthreads();
@@ -2643,6 +2645,7 @@ __device__ __forceinline__ void tsp_body(
                 for (int r = 0; r < nd; ++r) acc = acc + term;
             }
             const double c = acc + a.sc.static_cost;
+            const double pz = s_rpose[tid * 8 + 2];  // the mover position is the waypoint's (MODE 1)
             const double deficit = (a.floor_z_min + a.floor_margin) - pz;
             const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
             aC = aC + c;
@@ -2653,7 +2656,6 @@ __device__ __forceinline__ void tsp_body(
         double* ps = s_rpose + tid * 8;
         for (int k = 0; k < npr; ++k) rn[k] = 0;
         const bool has = valid && lane < cp;
-        double pz = 0.0;
         if (has) {
             const int i = lane + 1;
             double pv[4], pc[4];
@@ -2662,11 +2664,11 @@ __device__ __forceinline__ void tsp_body(
             for (int d = 0; d < D; ++d) pv[d] = __shfl_up(pc[d], 1, 64);
             if ((tid & 63) == 0) eval_pt<D, P>(myc, tab + (i - 1) * P1, span[i - 1], pv);
             aL = aL + dist_nd<D>(pv, pc);
-            pz = pc[2];
             point_collide<D, NM, 1, true, ONEGEOM, CB, 4, UP>(pc, a.sc, T, mask, nullptr, nullptr, rn, nullptr, ps);
         }
         const double c = tsp_lane_sum<UP>(has, rn, ps, npr, a.sc, T);  // every lane: wave ballots
         if (has) {
+            const double pz = ps[2];  // the mover position is the waypoint's (MODE 1)
             const double deficit = (a.floor_z_min + a.floor_margin) - pz;
             const double fp = deficit > 0.0 ? (a.floor_scale * deficit) * deficit : 0.0;
             aC = aC + c;
