@@ -29,15 +29,13 @@ constexpr double kDeep = -1e-3;     // include/Collision.h:93 "col_dist < -1e-3"
 #ifndef SSPP_DEEP_SGPR
 #define SSPP_DEEP_SGPR 1
 #endif
-__host__ __device__ __forceinline__ double deep_thr() {
+__host__ __device__ __forceinline__ double in_sgpr(double c) {
 #if defined(__HIP_DEVICE_COMPILE__) && SSPP_DEEP_SGPR
-    double c = kDeep;
     asm volatile("" : "+s"(c));
-    return c;
-#else
-    return kDeep;
 #endif
+    return c;
 }
+__host__ __device__ __forceinline__ double deep_thr() { return in_sgpr(kDeep); }
 constexpr double kMinVal = 1e-15;   // mjMINVAL
 constexpr int kMaxP = 7;            // max spline degree in kernels
 
@@ -1197,14 +1195,14 @@ SSPP_HD bool pair_near(const DPair& pr, double rg, const double* gp,
             const double lz = fma(om[8], dc[2], fma(om[5], dc[1], om[2] * dc[0]));
             const double ex = fmax(fabs(lx) - pr.osize[0], 0.0), ey = fmax(fabs(ly) - pr.osize[1], 0.0),
                          ez = fmax(fabs(lz) - pr.osize[2], 0.0);
-            const double lim = rg + pr.margin + kHullPad;
+            const double lim = rg + pr.margin + in_sgpr(kHullPad);  // (the pad: see deep_thr)
             return !(fma(ez, ez, fma(ey, ey, ex * ex)) > lim * lim);
         }
         return true;
     }
     if (pr.otype == 0 && rg > 0.0) {
         const double h = (gp[0] - op[0]) * om[2] + (gp[1] - op[1]) * om[5] + (gp[2] - op[2]) * om[8];
-        return !(h - rg > pr.margin + kHullPad);
+        return !(h - rg > pr.margin + in_sgpr(kHullPad));
     }
     return true;
 }

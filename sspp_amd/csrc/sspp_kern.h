@@ -1449,7 +1449,9 @@ __device__ SSPP_CB_INLINE bool c2f_cb_exact(const double* sm, int mine, int fix,
 template <int NT>
 __device__ __forceinline__ void surv_load_rows(const SurvPtrs& q, unsigned t, int nrd, double* smem, float* s_f32,
                                                int o_own) {
-    for (int e = threadIdx.x; e < nrd; e += NT) {
+    int e0 = threadIdx.x;
+    asm volatile("" : "+v"(e0));  // (the LDS offsets per survivor, not held across the queue loop)
+    for (int e = e0; e < nrd; e += NT) {
         const long long o = (long long)t * nrd + e;
         smem[o_own + e] = __longlong_as_double(
             (long long)__hip_atomic_load((unsigned long long*)q.ctrl + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1473,7 +1475,9 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
                                             double* __restrict__ arc, unsigned char* __restrict__ feasible,
                                             bool with_best, const SurvPtrs& q) {
     constexpr int P1 = P + 1;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // what derives from the lane index is recomputed here, not held
+    const int lane = tid & 63, wv = tid >> 6;
     const int r0 = a.r0, r1 = a.r1, nch = a.W - 1;
     const int step = (int)((word >> 32) & 0xFFu), lc = (int)(unsigned)word;
     const int j0 = a.n1, R = a.npts - j0;
@@ -1775,6 +1779,11 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
     if constexpr ((SPLIT || SSPP_PRIO_ALL) && SSPP_SPLIT_PRIO) __builtin_amdgcn_s_setprio(SSPP_SPLIT_PRIO_CONSUMER);
     if constexpr (SPLIT) {
         static_assert(NM == 1 && ONEGEOM && !CBX, "split launches: single-geom movers without cylinder-box pairs");
+        // the lane index through an empty asm: the split tail's LDS / output offsets are
+        // recomputed from it instead of the prologue's being held (spilled) across phase 1
+        int tid_s = threadIdx.x;
+        asm volatile("" : "+v"(tid_s));
+        const int tid = tid_s;
         SSPP_BEACON(3, 0, 0);
         SSPP_BEACON_T(1);
         // ---- producer: one queue reservation per workgroup (survivors in candidate order), the
@@ -1987,6 +1996,9 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         SSPP_BEACON(12, no, 0);
         SSPP_BEACON_E(1);
         // LDS is free: the per-step minimum bits, ids and feasible counts, the lost survivors
+        int tid_e = threadIdx.x;
+        asm volatile("" : "+v"(tid_e));  // (as at the producer: no offsets held across the queue)
+        const int tid_ep = tid_e;
         unsigned long long* s_bits = (unsigned long long*)smem;
         unsigned long long* s_id = s_bits + kMaxSteps;
         unsigned* s_cnt = (unsigned*)(s_id + kMaxSteps);
@@ -1997,25 +2009,25 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         // per thread, the reserved and the finished slots: the lost-work check
         const unsigned nl = __hip_atomic_load(&q.hdr->nlist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned c_sh = 0, sv_sh = 0;
-        if (tid < kSurvShards) {
-            c_sh = __hip_atomic_load(&q.hdr->shard[tid].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sv_sh = __hip_atomic_load(&q.hdr->shard[tid].served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid_ep < kSurvShards) {
+            c_sh = __hip_atomic_load(&q.hdr->shard[tid_ep].count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sv_sh = __hip_atomic_load(&q.hdr->shard[tid_ep].served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         unsigned long long rb = 0ull, rid = 0ull, rst = 0ull;
         if (best_base) {
-            rb = __hip_atomic_load(&q.res[tid].bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            rid = __hip_atomic_load(&q.res[tid].id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            rst = __hip_atomic_load(&q.res[tid].step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rb = __hip_atomic_load(&q.res[tid_ep].bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rid = __hip_atomic_load(&q.res[tid_ep].id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rst = __hip_atomic_load(&q.res[tid_ep].step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        for (int e = tid; e < nsteps; e += NT) {
+        for (int e = tid_ep; e < nsteps; e += NT) {
             s_bits[e] = __hip_atomic_load(q.hdr->bestbits + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_cnt[e] = __hip_atomic_load(q.hdr->count_feas + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_id[e] = ~0ull;
         }
         const unsigned short_sh = c_sh > sv_sh ? c_sh - sv_sh : 0u;  // this shard's survivors not finished
-        if (tid < 64) {
+        if (tid_ep < 64) {
             const unsigned tot = (unsigned)wave_sum_u32((int)short_sh);
-            if (tid == 0) s_lost[0] = tot;
+            if (tid_ep == 0) s_lost[0] = tot;
         }
         __syncthreads();
         const unsigned lost = (unsigned)__builtin_amdgcn_readfirstlane((int)s_lost[0]);
@@ -2024,17 +2036,17 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         // slot was re-armed by its consumer), so nothing stale reaches the next launch
         if (short_sh)
             for (unsigned e = 0; e < c_sh; ++e)
-                __hip_atomic_store(q.rec + (unsigned)tid * (unsigned)q.shard_cap + e, 0ull, __ATOMIC_RELAXED,
+                __hip_atomic_store(q.rec + (unsigned)tid_ep * (unsigned)q.shard_cap + e, 0ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) {
+        if (tid_ep == 0) {
             if (lost) __hip_atomic_fetch_add(&q.hdr->lost_total, (unsigned long long)lost, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
             if (no) __hip_atomic_fetch_add(&q.hdr->handoffs, (unsigned long long)no, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
         }
         if (best_base) {
-            if ((unsigned)tid < nl && rb == s_bits[rst]) atomicMin(s_id + rst, rid);
-            for (unsigned i = tid + NT; i < nl; i += NT) {
+            if ((unsigned)tid_ep < nl && rb == s_bits[rst]) atomicMin(s_id + rst, rid);
+            for (unsigned i = tid_ep + NT; i < nl; i += NT) {
                 const unsigned long long bits = __hip_atomic_load(&q.res[i].bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long id = __hip_atomic_load(&q.res[i].id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const int st = (int)__hip_atomic_load(&q.res[i].step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2043,7 +2055,7 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
         }
         __syncthreads();
         SSPP_BEACON_E(3);
-        for (int e = tid; e < nsteps; e += NT) {
+        for (int e = tid_ep; e < nsteps; e += NT) {
             if (best_base) {
                 const bool has = s_id[e] != ~0ull;
                 best_base[e].cost = has ? __longlong_as_double((long long)s_bits[e]) : INFINITY;
@@ -2054,13 +2066,13 @@ __global__ __launch_bounds__(NT, (NT <= SSPP_C2F_FIVE_MAX && ONEGEOM) ? SSPP_C2F
             __hip_atomic_store(q.hdr->bestbits + e, 0x7FF0000000000000ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(q.hdr->count_feas + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        for (int e = tid; e < kSurvShards; e += NT) {
+        for (int e = tid_ep; e < kSurvShards; e += NT) {
             __hip_atomic_store(&q.hdr->shard[e].count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->shard[e].taken, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->shard[e].pushed, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->shard[e].served, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (tid == 0) {
+        if (tid_ep == 0) {
             for (int k = 0; k < 8; ++k) __hip_atomic_store(&q.hdr->arrive_sh[k][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->arrive_top[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&q.hdr->nlist, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
