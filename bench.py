@@ -39,7 +39,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 # kernel revision: PMC records (profiles/*_latest.json) measured on another revision of the
 # kernels are not attached to a line (tools/update_latest.py stamps them)
-KERNEL_REV = "r05"
+KERNEL_REV = "r06"
 FP64_PEAK_TFLOPS = 78.6    # FP64 vector (VALU) spec
 
 
