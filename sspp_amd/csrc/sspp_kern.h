@@ -87,6 +87,11 @@ struct SceneT {
     const DGeom* __restrict__ geoms;
     const DPair* __restrict__ pairs;
     const DMover* __restrict__ movers;
+    // the scene's pairs (<= 64) in an order grouped by moving geom, for the pair loops whose
+    // order does not enter a sum (point_collide REC 4: per-pair records, summed in pair order
+    // afterwards), so a geom's pose is formed once per group instead of at every geom change of
+    // the reference's (g1, g2) order
+    const unsigned char* __restrict__ visit;
 };
 
 // Constant address space (4): loads through these are scalar (SMEM) whenever the address
@@ -173,11 +178,12 @@ __host__ __device__ __forceinline__ bool pair_may_touch(const DPair& pr, const D
 template <int D, int NM, int MODE>
 __device__ __forceinline__ unsigned long long hull_mask(const double* ctrl, int n, int npairs,
                                                         cpair_t pairs, cgeom_t geoms,
-                                                        cmover_t movers) {
+                                                        cmover_t movers,
+                                                        const unsigned char* visit = nullptr) {
     const int lane = threadIdx.x & 63;
     bool act = false;
-    if (lane < npairs) {
-        const DPair pr = load_pair(pairs + lane);
+    if (lane < npairs) {  // bit v: pair visit[v] (the identity without a visit order)
+        const DPair pr = load_pair(pairs + (visit ? (int)visit[lane] : lane));
         const DGeom G = load_geom(geoms + pr.gm);
         const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
         double lo[3], hi[3];
@@ -615,14 +621,18 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
         geom_rot_t<ZR>(mR[0], G, gmat);
     }
     const int np = sc.npairs;
-    for (int k = 0; k < np; ++k) {
-        if (k < 64) {
+    // REC 4 with a visit order: v runs over the geom-grouped order (the mask's bits are in that
+    // order too), k is the pair's index for its record
+    const bool VIS = REC == 4 && T.visit != nullptr;
+    for (int v = 0; v < np; ++v) {
+        if (v < 64) {
             // skip culled pairs with a scalar bit scan
-            const unsigned long long rest = mask >> k;
+            const unsigned long long rest = mask >> v;
             if (rest == 0ull) break;
-            k += __builtin_ctzll(rest);
-            if (k >= np) break;
+            v += __builtin_ctzll(rest);
+            if (v >= np) break;
         }
+        const int k = VIS ? (int)T.visit[v] : v;
         const DPair pr = load_pair(pairs + k);
         if (!ONEGEOM && pr.gm != cur) {
             cur = pr.gm;
@@ -1584,16 +1594,18 @@ __device__ __forceinline__ void surv_finish(const SsppC2F& a, const SceneT& TT, 
     __syncthreads();  // the next survivor may overwrite the rows and the flags
 }
 
-// Occupancy per shape: one-wave workgroups of a single-geom mover at 5 waves per SIMD (96 VGPRs,
-// no spill: 20 workgroups per CU, so a 20-step launch of 4096-candidate steps is one resident
-// round); 4-wave workgroups and multi-geom movers at 4 (128 VGPRs; at 5 they spill).
+// Occupancy per shape: one- and two-wave workgroups of a single-geom mover at 5 waves per SIMD
+// (96 VGPRs: 20 waves per CU, so the 20-step launch of 4096-candidate steps at 128 x 4 is one
+// resident round); 4-wave workgroups and multi-geom movers at 4 (128 VGPRs; at 5 they spill).
+// Round 6 (tools/kres.py, profiles/r06pmc_*): the robocrane d7 instances at 128 threads spill
+// no VGPR, split and unsplit; the split one has no scratch at all (Registers).
 #ifndef SSPP_C2F_WAVES_PER_EU
 #define SSPP_C2F_WAVES_PER_EU 5
 #endif
 #ifndef SSPP_C2F_WAVES_PER_EU_WIDE
 #define SSPP_C2F_WAVES_PER_EU_WIDE 4
 #endif
-// Workgroups of up to 128 threads run at SSPP_C2F_WAVES_PER_EU (96 VGPRs, no spill); the 256-thread
+// Workgroups of up to 128 threads run at SSPP_C2F_WAVES_PER_EU (96 VGPRs); the 256-thread
 // latency shape carries the phase-2 pair groups (few survivor items over many lanes), which
 // cost registers (at 5 waves per SIMD they spill), and runs at SSPP_C2F_WAVES_PER_EU_WIDE.
 // profiling builds only (tools/build_variant.sh -DSSPP_ABLATE=mask): 1 no sampling, 2 no
@@ -2586,7 +2598,8 @@ __device__ __forceinline__ void tsp_body(
     const bool valid = slot < nvalid;
     const double* myc = s_ctrl + (r * cpb + slot) * ndof;
     const unsigned long long mask = hull_mask<D, NM, 1>(myc, n, a.sc.npairs, (cpair_t)T.pairs,
-                                                        (cgeom_t)T.geoms, (cmover_t)T.movers);
+                                                        (cgeom_t)T.geoms, (cmover_t)T.movers,
+                                                        DEF == 2 ? T.visit : nullptr);
     double aL = 0.0, aC = 0.0, aW = 0.0;
     // cp <= lpc: one waypoint per lane, so s((i-1)du) is the previous lane's s(i du); take it
     // by shuffle (bit-identical: same eval_pt inputs) except on a wave's first lane
@@ -3025,6 +3038,7 @@ struct sspp_scene {
     DGeom* d_geoms = nullptr;
     DPair* d_pairs = nullptr;
     DMover* d_movers = nullptr;
+    unsigned char* d_visit = nullptr;  // pair visit order grouped by moving geom (SceneT::visit)
     int device = 0;
 };
 
@@ -3155,6 +3169,10 @@ inline SceneT scene_t(const sspp_scene* s) {
     t.geoms = s->d_geoms;
     t.pairs = s->d_pairs;
     t.movers = s->d_movers;
+#ifndef SSPP_TSP_VISIT
+#define SSPP_TSP_VISIT 1
+#endif
+    t.visit = SSPP_TSP_VISIT ? s->d_visit : nullptr;
     return t;
 }
 
@@ -3171,7 +3189,7 @@ struct SsppPtrs {
 // the job's pair table: sampled candidates use the reachable subset, caller splines the full one
 inline SceneT scene_t_job(const sspp_job* j, bool sampled) {
     SceneT t = scene_t(j->scene);
-    if (j->d_pairs) t.pairs = sampled ? j->d_pairs_s : j->d_pairs;
+    if (j->d_pairs) { t.pairs = sampled ? j->d_pairs_s : j->d_pairs; t.visit = nullptr; }  // (another order)
     return t;
 }
 inline KScene kscene_job(const sspp_job* j, bool sampled) {
@@ -3248,7 +3266,7 @@ hipError_t launch_census(const sspp_job* j, int M, unsigned long long seed, unsi
                          const DPair* pairs, hipStream_t st) {
     const KScene sc = kscene_job(j, true);
     SceneT T = scene_t_job(j, true);
-    if (pairs) T.pairs = pairs;  // the asynchronous pre-pass's own copy of the sampled table
+    if (pairs) { T.pairs = pairs; T.visit = nullptr; }  // the asynchronous pre-pass's own copy of the sampled table
     const int r0 = std::min(P, j->n), r1 = std::max(r0, j->n - P);
     const size_t lds = sizeof(double) * ((size_t)j->n * D + (size_t)(r1 - r0) * D + D);
     if (NM == 1 && sc.onegeom && sc.npairs > 0)

@@ -305,10 +305,20 @@ int sspp_scene_create(const sspp_model* m, int mode, int arg, int count_static, 
         for (int k = 0; k < 7; ++k) mv.qpos0[k] = m->qpos0[mv.qpos_adr + k];
         s->movers.push_back(mv);
     }
+    // the pair visit order of the record-form pair loops (SceneT::visit): grouped by moving geom,
+    // the reference's order within a group; only for tables a mask word can cover
+    std::vector<unsigned char> visit;
+    if (!s->pairs.empty() && s->pairs.size() <= 64) {
+        std::vector<int> ix(s->pairs.size());
+        for (size_t i = 0; i < ix.size(); ++i) ix[i] = (int)i;
+        std::stable_sort(ix.begin(), ix.end(), [&](int x, int y) { return s->pairs[x].gm < s->pairs[y].gm; });
+        for (int i : ix) visit.push_back((unsigned char)i);
+    }
     int rc;
     if ((rc = upload(&s->d_geoms, s->geoms.data(), s->geoms.size())) ||
         (rc = upload(&s->d_pairs, s->pairs.data(), s->pairs.size())) ||
-        (rc = upload(&s->d_movers, s->movers.data(), s->movers.size()))) {
+        (rc = upload(&s->d_movers, s->movers.data(), s->movers.size())) ||
+        (rc = upload(&s->d_visit, visit.data(), visit.size()))) {
         sspp_scene_free(s);
         return rc;
     }
@@ -334,6 +344,7 @@ void sspp_scene_free(sspp_scene* s) {
     if (s->d_geoms) (void)hipFree(s->d_geoms);
     if (s->d_pairs) (void)hipFree(s->d_pairs);
     if (s->d_movers) (void)hipFree(s->d_movers);
+    if (s->d_visit) (void)hipFree(s->d_visit);
     delete s;
 }
 
