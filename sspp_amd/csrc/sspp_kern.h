@@ -91,7 +91,7 @@ struct SceneT {
     // order does not enter a sum (point_collide REC 4: per-pair records, summed in pair order
     // afterwards), so a geom's pose is formed once per group instead of at every geom change of
     // the reference's (g1, g2) order
-    const unsigned char* __restrict__ visit;
+    const int* __restrict__ visit;
 };
 
 // Constant address space (4): loads through these are scalar (SMEM) whenever the address
@@ -102,6 +102,7 @@ struct SceneT {
 #define SSPP_CONST
 #endif
 typedef const SSPP_CONST DGeom* cgeom_t;
+typedef const SSPP_CONST int* cint_t;
 typedef const SSPP_CONST DPair* cpair_t;
 typedef const SSPP_CONST DMover* cmover_t;
 
@@ -179,11 +180,11 @@ template <int D, int NM, int MODE>
 __device__ __forceinline__ unsigned long long hull_mask(const double* ctrl, int n, int npairs,
                                                         cpair_t pairs, cgeom_t geoms,
                                                         cmover_t movers,
-                                                        const unsigned char* visit = nullptr) {
+                                                        const int* visit = nullptr) {
     const int lane = threadIdx.x & 63;
     bool act = false;
     if (lane < npairs) {  // bit v: pair visit[v] (the identity without a visit order)
-        const DPair pr = load_pair(pairs + (visit ? (int)visit[lane] : lane));
+        const DPair pr = load_pair(pairs + (visit ? visit[lane] : lane));
         const DGeom G = load_geom(geoms + pr.gm);
         const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
         double lo[3], hi[3];
@@ -591,6 +592,13 @@ __device__ __forceinline__ void geom_rot_t(const double* R, const DGeom& G, doub
 // REC 4 (k_tsp<..., DEF 2>): the records of REC 3 without the terms — the lane itself sums its
 // records after the pair loop (tsp_lane_sum), recomputing each term from the recorded pose.
 constexpr int kBbPend = 16;
+#ifndef SSPP_TSP_LEAN_GEOM
+#ifdef SSPP_TSP_STATS  // (the statistics read the geom record at every pair)
+#define SSPP_TSP_LEAN_GEOM 0
+#else
+#define SSPP_TSP_LEAN_GEOM 1
+#endif
+#endif
 template <int D, int NM, int MODE, bool DEEP, bool ONEGEOM, int CB = 1, int REC = 0, bool UP = false>
 __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
                              unsigned long long mask, double* cost, int* stop = nullptr,
@@ -613,6 +621,12 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
     double gp[3], gmat[9];
     bool have_rot = true;  // multi-geom movers: a geom's rotation is formed at its first near pair
     DGeom G;
+    // LEAN (several moving geoms): across the pair loop only the current geom's index, bounding
+    // radius and position live; its record and rotation are formed again at each near pair
+    // (scalar loads and a few FMAs for ~3 pairs per waypoint) instead of ~40 VGPRs of geom record
+    // and rotation cache held through every pair
+    constexpr bool LEAN = !ONEGEOM && SSPP_TSP_LEAN_GEOM;
+    double grb = 0.0;
     constexpr bool ZR = MODE == 1;  // yaw-only mover rotation
     if (ONEGEOM) {  // every pair shares one moving geom: pose once, mover pose dies here
         cur = pairs[0].gm;
@@ -632,9 +646,15 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             v += __builtin_ctzll(rest);
             if (v >= np) break;
         }
-        const int k = VIS ? (int)T.visit[v] : v;
+        const int k = VIS ? ((cint_t)T.visit)[v] : v;
         const DPair pr = load_pair(pairs + k);
-        if (!ONEGEOM && pr.gm != cur) {
+        if (LEAN && pr.gm != cur) {
+            cur = pr.gm;
+            const DGeom Gn = load_geom(geoms + cur);
+            grb = Gn.rbound;
+            const bool second = NM > 1 && Gn.mover == 1;
+            geom_pos_t<ZR>(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], Gn, gp);
+        } else if (!ONEGEOM && !LEAN && pr.gm != cur) {
             cur = pr.gm;
             G = load_geom(geoms + cur);
             const bool second = NM > 1 && G.mover == 1;
@@ -654,7 +674,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             matmul3(R, pr.omat, om_);
             op = op_; om = om_;
         }
-        const bool near = pair_near(pr, G.rbound, gp, op, om);
+        const bool near = pair_near(pr, LEAN ? grb : G.rbound, gp, op, om);
         int nd = 0, nc = 0;
         if (DEEP) {
             TSP_STAT(0, true);
@@ -664,7 +684,11 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             TSP_STAT(4, near && (G.type == 0 || pr.otype == 0));
         }
         if (near) {
-            if (!ONEGEOM && !have_rot) {
+            if (LEAN) {
+                G = load_geom(geoms + cur);
+                const bool second = NM > 1 && G.mover == 1;
+                geom_rot_t<ZR>(second ? mR[NM - 1] : mR[0], G, gmat);
+            } else if (!ONEGEOM && !have_rot) {
                 const bool second = NM > 1 && G.mover == 1;
                 geom_rot_t<ZR>(second ? mR[NM - 1] : mR[0], G, gmat);
                 have_rot = true;
@@ -3038,7 +3062,7 @@ struct sspp_scene {
     DGeom* d_geoms = nullptr;
     DPair* d_pairs = nullptr;
     DMover* d_movers = nullptr;
-    unsigned char* d_visit = nullptr;  // pair visit order grouped by moving geom (SceneT::visit)
+    int* d_visit = nullptr;  // pair visit order grouped by moving geom (SceneT::visit)
     int device = 0;
 };
 
