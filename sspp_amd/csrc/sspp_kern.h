@@ -91,7 +91,8 @@ struct SceneT {
     // order does not enter a sum (point_collide REC 4: per-pair records, summed in pair order
     // afterwards), so a geom's pose is formed once per group instead of at every geom change of
     // the reference's (g1, g2) order
-    const int* __restrict__ visit;
+    // (a copy of the pairs in that order, each record's `pad` holding its index in `pairs`)
+    const DPair* __restrict__ visit;
 };
 
 // Constant address space (4): loads through these are scalar (SMEM) whenever the address
@@ -102,7 +103,6 @@ struct SceneT {
 #define SSPP_CONST
 #endif
 typedef const SSPP_CONST DGeom* cgeom_t;
-typedef const SSPP_CONST int* cint_t;
 typedef const SSPP_CONST DPair* cpair_t;
 typedef const SSPP_CONST DMover* cmover_t;
 
@@ -129,7 +129,7 @@ __device__ __forceinline__ DPair load_pair(cpair_t p) {
     r.otype = p->otype;
     r.oorig = p->oorig;
     r.omover = p->omover;
-    r.pad = 0;
+    r.pad = p->pad;
     r.margin = p->margin;
 #pragma unroll
     for (int k = 0; k < 3; ++k) r.opos[k] = p->opos[k];
@@ -180,11 +180,11 @@ template <int D, int NM, int MODE>
 __device__ __forceinline__ unsigned long long hull_mask(const double* ctrl, int n, int npairs,
                                                         cpair_t pairs, cgeom_t geoms,
                                                         cmover_t movers,
-                                                        const int* visit = nullptr) {
+                                                        const DPair* visit = nullptr) {
     const int lane = threadIdx.x & 63;
     bool act = false;
-    if (lane < npairs) {  // bit v: pair visit[v] (the identity without a visit order)
-        const DPair pr = load_pair(pairs + (visit ? visit[lane] : lane));
+    if (lane < npairs) {  // bit v: the visit order's pair v (the identity without a visit order)
+        const DPair pr = load_pair(visit ? (cpair_t)visit + lane : pairs + lane);
         const DGeom G = load_geom(geoms + pr.gm);
         const int m = (NM > 1 && G.mover == 1) ? 1 : 0;
         double lo[3], hi[3];
@@ -621,11 +621,12 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
     double gp[3], gmat[9];
     bool have_rot = true;  // multi-geom movers: a geom's rotation is formed at its first near pair
     DGeom G;
-    // LEAN (several moving geoms): across the pair loop only the current geom's index, bounding
-    // radius and position live; its record and rotation are formed again at each near pair
-    // (scalar loads and a few FMAs for ~3 pairs per waypoint) instead of ~40 VGPRs of geom record
-    // and rotation cache held through every pair
-    constexpr bool LEAN = !ONEGEOM && SSPP_TSP_LEAN_GEOM;
+    // Several moving geoms: SSPP_TSP_LEAN_GEOM bit 0 keeps only the current geom's index, bounding
+    // radius and position across the pair loop and re-loads its record (scalar loads) at each
+    // near pair, instead of ~26 VGPRs of record held through every pair; bit 1 also re-forms its
+    // rotation per near pair instead of caching it (measured slower: the default is bit 0 only)
+    constexpr bool LREC = !ONEGEOM && (SSPP_TSP_LEAN_GEOM & 1) != 0;  // record re-loaded per near pair
+    constexpr bool LROT = !ONEGEOM && (SSPP_TSP_LEAN_GEOM & 2) != 0;  // rotation re-formed per near pair
     double grb = 0.0;
     constexpr bool ZR = MODE == 1;  // yaw-only mover rotation
     if (ONEGEOM) {  // every pair shares one moving geom: pose once, mover pose dies here
@@ -646,19 +647,20 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             v += __builtin_ctzll(rest);
             if (v >= np) break;
         }
-        const int k = VIS ? ((cint_t)T.visit)[v] : v;
-        const DPair pr = load_pair(pairs + k);
-        if (LEAN && pr.gm != cur) {
+        const DPair pr = load_pair(VIS ? (cpair_t)T.visit + v : pairs + v);
+        const int k = VIS ? pr.pad : v;  // the pair's record index
+        if (!ONEGEOM && pr.gm != cur) {
             cur = pr.gm;
-            const DGeom Gn = load_geom(geoms + cur);
-            grb = Gn.rbound;
-            const bool second = NM > 1 && Gn.mover == 1;
-            geom_pos_t<ZR>(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], Gn, gp);
-        } else if (!ONEGEOM && !LEAN && pr.gm != cur) {
-            cur = pr.gm;
-            G = load_geom(geoms + cur);
-            const bool second = NM > 1 && G.mover == 1;
-            geom_pos_t<ZR>(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp);
+            if (LREC) {
+                const DGeom Gn = load_geom(geoms + cur);
+                grb = Gn.rbound;
+                const bool second = NM > 1 && Gn.mover == 1;
+                geom_pos_t<ZR>(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], Gn, gp);
+            } else {
+                G = load_geom(geoms + cur);
+                const bool second = NM > 1 && G.mover == 1;
+                geom_pos_t<ZR>(second ? mp[NM - 1] : mp[0], second ? mR[NM - 1] : mR[0], G, gp);
+            }
             have_rot = false;
         }
         double op_[3], om_[9];
@@ -674,7 +676,7 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             matmul3(R, pr.omat, om_);
             op = op_; om = om_;
         }
-        const bool near = pair_near(pr, LEAN ? grb : G.rbound, gp, op, om);
+        const bool near = pair_near(pr, LREC ? grb : G.rbound, gp, op, om);
         int nd = 0, nc = 0;
         if (DEEP) {
             TSP_STAT(0, true);
@@ -684,11 +686,8 @@ __device__ int point_collide(const double* q, const KScene& sc, const SceneT& T,
             TSP_STAT(4, near && (G.type == 0 || pr.otype == 0));
         }
         if (near) {
-            if (LEAN) {
-                G = load_geom(geoms + cur);
-                const bool second = NM > 1 && G.mover == 1;
-                geom_rot_t<ZR>(second ? mR[NM - 1] : mR[0], G, gmat);
-            } else if (!ONEGEOM && !have_rot) {
+            if (LREC) G = load_geom(geoms + cur);
+            if (LROT || (!ONEGEOM && !have_rot)) {
                 const bool second = NM > 1 && G.mover == 1;
                 geom_rot_t<ZR>(second ? mR[NM - 1] : mR[0], G, gmat);
                 have_rot = true;
@@ -3062,7 +3061,7 @@ struct sspp_scene {
     DGeom* d_geoms = nullptr;
     DPair* d_pairs = nullptr;
     DMover* d_movers = nullptr;
-    int* d_visit = nullptr;  // pair visit order grouped by moving geom (SceneT::visit)
+    DPair* d_visit = nullptr;  // the pairs grouped by moving geom (SceneT::visit)
     int device = 0;
 };
 

@@ -307,12 +307,16 @@ int sspp_scene_create(const sspp_model* m, int mode, int arg, int count_static, 
     }
     // the pair visit order of the record-form pair loops (SceneT::visit): grouped by moving geom,
     // the reference's order within a group; only for tables a mask word can cover
-    std::vector<int> visit;
+    std::vector<DPair> visit;
     if (!s->pairs.empty() && s->pairs.size() <= 64) {
         std::vector<int> ix(s->pairs.size());
         for (size_t i = 0; i < ix.size(); ++i) ix[i] = (int)i;
         std::stable_sort(ix.begin(), ix.end(), [&](int x, int y) { return s->pairs[x].gm < s->pairs[y].gm; });
-        for (int i : ix) visit.push_back(i);
+        for (int i : ix) {
+            DPair q = s->pairs[i];
+            q.pad = i;  // its record index
+            visit.push_back(q);
+        }
     }
     int rc;
     if ((rc = upload(&s->d_geoms, s->geoms.data(), s->geoms.size())) ||
