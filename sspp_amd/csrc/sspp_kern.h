@@ -3192,10 +3192,7 @@ inline SceneT scene_t(const sspp_scene* s) {
     t.geoms = s->d_geoms;
     t.pairs = s->d_pairs;
     t.movers = s->d_movers;
-#ifndef SSPP_TSP_VISIT
-#define SSPP_TSP_VISIT 1
-#endif
-    t.visit = SSPP_TSP_VISIT ? s->d_visit : nullptr;
+    t.visit = s->d_visit;
     return t;
 }
 
